@@ -1,0 +1,183 @@
+// ba_device.h — device-side math shared by the libmiba HIP kernels.
+//
+// Per-observation residual + analytic local Jacobian (the replacement of the
+// reference's two AutoDiff cost functors, Jet<double,14> x 2 per observation):
+//   ReprojectionConstraint::operator()  /root/reference/src/OptimizationUtils.cpp:25-49
+//   DepthPrior::operator()              /root/reference/src/OptimizationUtils.cpp:72-94
+// robustified with Ceres HuberLoss(HUB_P_*) + Corrector (rho'' <= 0 => sqrt(rho')
+// scaling), see OptimizationUtils.cpp:223-226, BundleAdjustmentConfig.h:47-50.
+// The pose Jacobian is taken w.r.t. the Sophus right perturbation T*exp(delta),
+// delta = [upsilon, omega] (local_parameterization_se3.hpp:17-37), which equals
+// Ceres' ambient Jacobian x Dx_this_mul_exp_x_at_0 (se3.hpp:113-182).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+
+namespace miba {
+
+struct BaConsts {
+    double sw_r, sw_d, sw_k;   // sqrt(1/N), sqrt(WEIGHT_UNPR/N), sqrt(WEIGHT_INTRINSICS)
+    double a_r, b_r, a_d, b_d; // Huber a and b = a^2 (reprojection, depth)
+    double min_diag, max_diag; // LM diagonal clamp
+};
+
+// Eigen toRotationMatrix of q = (w=p[3], x=p[0], y=p[1], z=p[2])  (OptimizationUtils.cpp:36-41)
+__device__ __forceinline__ void quat_R(const double* __restrict__ p, double R[9]) {
+    const double x = p[0], y = p[1], z = p[2], w = p[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+
+// Huber rho(s) and sqrt(rho'(s))  (Ceres HuberLoss::Evaluate; Corrector)
+__device__ __forceinline__ void huber(double s, double a, double b, double& rho0, double& sq_rho1) {
+    if (s > b) {
+        const double r = sqrt(s);
+        rho0 = 2.0 * a * r - b;
+        sq_rho1 = sqrt(fmax(DBL_MIN, a / r));
+    } else {
+        rho0 = s;
+        sq_rho1 = 1.0;
+    }
+}
+
+struct ObsEval {
+    double f[3];   // robustified residual (reproj u, v, depth)
+    double cost;   // 0.5 rho_r + 0.5 rho_d
+    bool ok;
+};
+
+// Residual only (candidate evaluation).
+__device__ __forceinline__ void eval_obs(const BaConsts& c, const double* __restrict__ pose,
+                                         const double* __restrict__ X, const double* __restrict__ K,
+                                         double uo, double vo, double depth, ObsEval& o) {
+    double R[9];
+    quat_R(pose, R);
+    const double d0 = X[0] - pose[4], d1 = X[1] - pose[5], d2 = X[2] - pose[6];
+    const double x = R[0] * d0 + R[3] * d1 + R[6] * d2;
+    const double y = R[1] * d0 + R[4] * d1 + R[7] * d2;
+    const double z = R[2] * d0 + R[5] * d1 + R[8] * d2;
+    const double u = (K[0] * x + K[2] * z) / z;
+    const double v = (K[1] * y + K[3] * z) / z;
+    const double r0 = c.sw_r * (u - uo), r1 = c.sw_r * (v - vo), r2 = c.sw_d * (depth - z);
+    double rr, gr, rd, gd;
+    huber(r0 * r0 + r1 * r1, c.a_r, c.b_r, rr, gr);
+    huber(r2 * r2, c.a_d, c.b_d, rd, gd);
+    o.cost = 0.5 * rr + 0.5 * rd;
+    o.f[0] = gr * r0; o.f[1] = gr * r1; o.f[2] = gd * r2;
+    o.ok = isfinite(o.cost) && isfinite(u) && isfinite(v);
+}
+
+// Residual + robustified local Jacobians.
+//   jc[r*6+d] (d: upsilon xyz, omega xyz), jp[r*3+i], jk[r*4+i] (rows 0,1; depth row has none)
+__device__ __forceinline__ void lin_obs(const BaConsts& c, const double* __restrict__ pose,
+                                        const double* __restrict__ X, const double* __restrict__ K,
+                                        double uo, double vo, double depth, ObsEval& o, double jc[18],
+                                        double jp[9], double jk[8]) {
+    double R[9];
+    quat_R(pose, R);
+    const double d0 = X[0] - pose[4], d1 = X[1] - pose[5], d2 = X[2] - pose[6];
+    const double x = R[0] * d0 + R[3] * d1 + R[6] * d2;
+    const double y = R[1] * d0 + R[4] * d1 + R[7] * d2;
+    const double z = R[2] * d0 + R[5] * d1 + R[8] * d2;
+    const double fx = K[0], fy = K[1], cx = K[2], cy = K[3];
+    const double u = (fx * x + cx * z) / z;
+    const double v = (fy * y + cy * z) / z;
+    const double r0 = c.sw_r * (u - uo), r1 = c.sw_r * (v - vo), r2 = c.sw_d * (depth - z);
+    double rr, gr, rd, gd;
+    huber(r0 * r0 + r1 * r1, c.a_r, c.b_r, rr, gr);
+    huber(r2 * r2, c.a_d, c.b_d, rd, gd);
+    o.cost = 0.5 * rr + 0.5 * rd;
+    o.f[0] = gr * r0; o.f[1] = gr * r1; o.f[2] = gd * r2;
+    o.ok = isfinite(o.cost) && isfinite(u) && isfinite(v);
+    const double iz = 1.0 / z;
+    const double su = gr * c.sw_r;
+    const double a00 = su * fx * iz, a02 = -su * fx * x * iz * iz;
+    const double a11 = su * fy * iz, a12 = -su * fy * y * iz * iz;
+    const double dz = -gd * c.sw_d;
+    // row 0: [a00, 0, a02] ; row 1: [0, a11, a12] ; row 2: [0, 0, dz]
+    // d pC / d upsilon = -I ; d pC / d omega = [pC]x = [[0,-z,y],[z,0,-x],[-y,x,0]]
+    // translation columns: -A ; omega columns: A . P
+    jc[0] = -a00; jc[1] = 0.0; jc[2] = -a02;
+    jc[3] = -a02 * y; jc[4] = a02 * x - a00 * z; jc[5] = a00 * y;
+    jc[6] = 0.0; jc[7] = -a11; jc[8] = -a12;
+    jc[9] = a11 * z - a12 * y; jc[10] = a12 * x; jc[11] = -a11 * x;
+    jc[12] = 0.0; jc[13] = 0.0; jc[14] = -dz;
+    jc[15] = -dz * y; jc[16] = dz * x; jc[17] = 0.0;
+    // d pC / d X = R^T : (R^T)_{k i} = R[i*3+k]
+    jp[0] = a00 * R[0] + a02 * R[2];
+    jp[1] = a00 * R[3] + a02 * R[5];
+    jp[2] = a00 * R[6] + a02 * R[8];
+    jp[3] = a11 * R[1] + a12 * R[2];
+    jp[4] = a11 * R[4] + a12 * R[5];
+    jp[5] = a11 * R[7] + a12 * R[8];
+    jp[6] = dz * R[2];
+    jp[7] = dz * R[5];
+    jp[8] = dz * R[8];
+    jk[0] = su * x * iz; jk[1] = 0.0; jk[2] = su; jk[3] = 0.0;
+    jk[4] = 0.0; jk[5] = su * y * iz; jk[6] = 0.0; jk[7] = su;
+}
+
+// Sophus T * exp(delta)  (se3.hpp:725-746, so3.hpp:537-571, so3.hpp:339-356)
+__device__ __forceinline__ void se3_plus(const double* __restrict__ T, const double* __restrict__ d,
+                                         double* __restrict__ out) {
+    const double ox = d[3], oy = d[4], oz = d[5];
+    const double theta_sq = ox * ox + oy * oy + oz * oz;
+    const double theta = sqrt(theta_sq);
+    double imag, real;
+    if (theta < 1e-10) {
+        const double t4 = theta_sq * theta_sq;
+        imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * t4;
+        real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * t4;
+    } else {
+        double sh, ch;
+        sincos(0.5 * theta, &sh, &ch);
+        imag = sh / theta;
+        real = ch;
+    }
+    const double qd[4] = {imag * ox, imag * oy, imag * oz, real};
+    double V[9];
+    if (theta < 1e-10) {
+        quat_R(qd, V);
+    } else {
+        const double Om[9] = {0, -oz, oy, oz, 0, -ox, -oy, ox, 0};
+        double s, cth;
+        sincos(theta, &s, &cth);
+        const double a = (1.0 - cth) / theta_sq;
+        const double b = (theta - s) / (theta_sq * theta);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const double o2 = Om[i * 3 + 0] * Om[0 * 3 + j] + Om[i * 3 + 1] * Om[1 * 3 + j] + Om[i * 3 + 2] * Om[2 * 3 + j];
+                V[i * 3 + j] = (i == j ? 1.0 : 0.0) + a * Om[i * 3 + j] + b * o2;
+            }
+    }
+    double td[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) td[i] = V[i * 3 + 0] * d[0] + V[i * 3 + 1] * d[1] + V[i * 3 + 2] * d[2];
+    const double qx = T[0], qy = T[1], qz = T[2], qw = T[3];
+    const double uv0 = 2 * (qy * td[2] - qz * td[1]);
+    const double uv1 = 2 * (qz * td[0] - qx * td[2]);
+    const double uv2 = 2 * (qx * td[1] - qy * td[0]);
+    out[4] = T[4] + (td[0] + qw * uv0 + (qy * uv2 - qz * uv1));
+    out[5] = T[5] + (td[1] + qw * uv1 + (qz * uv0 - qx * uv2));
+    out[6] = T[6] + (td[2] + qw * uv2 + (qx * uv1 - qy * uv0));
+    const double bx = qd[0], by = qd[1], bz = qd[2], bw = qd[3];
+    double nw = qw * bw - qx * bx - qy * by - qz * bz;
+    double nx = qw * bx + qx * bw + qy * bz - qz * by;
+    double ny = qw * by + qy * bw + qz * bx - qx * bz;
+    double nz = qw * bz + qz * bw + qx * by - qy * bx;
+    const double sq = nx * nx + ny * ny + nz * nz + nw * nw;
+    if (sq != 1.0) {
+        const double f = 2.0 / (1.0 + sq);
+        nx *= f; ny *= f; nz *= f; nw *= f;
+    }
+    out[0] = nx; out[1] = ny; out[2] = nz; out[3] = nw;
+}
+
+}  // namespace miba

@@ -1,0 +1,116 @@
+// ba_kernels.h — device data layout and kernel launchers of libmiba (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ba_device.h"
+
+namespace miba {
+
+// per-active-camera linearisation record: U upper-packed (21) | C 6x4 (24) | g (6)
+static constexpr int CAMDATA = 51;
+// per camera-segment intrinsics partial: Ukk packed (10) | gk (4) | cost (1)
+static constexpr int SEGINTR = 15;
+// per active point Schur record: V~^-1 packed (6) | e~ (3) | K~ 4x3 (12)
+static constexpr int PDATA = 21;
+
+// partial-sum slots (each slot holds part_stride doubles, one per producing block)
+enum {
+    PART_PT_GMAX = 0,
+    PART_PT_BAD,
+    PART_UPD_SN2,
+    PART_UPD_MCC,
+    PART_UPD_COST,
+    PART_BS_SN2,
+    PART_BS_MCC,
+    PART_BS_COST,
+    PART_BS_BAD,
+    PART_NSLOTS
+};
+// final scalars
+enum { SC_MCC = 0, SC_CAND, SC_SN2, SC_GMAX_PT, SC_BAD, SC_N = 8 };
+// lin record: [0] cost(x), [1] gmax cams+intr, [2..12) Ukk packed (+prior), [12..16) gk (+prior)
+static constexpr int LIN_N = 16;
+
+// Flattened window on the device (all indices 32-bit).
+struct DevProblem {
+    double* cams[2];  // [n_cams*7]  x and candidate (ping-pong)
+    double* pts[2];   // [n_points*3]
+    double* K[2];     // [4]
+    const double* prior;
+    // admissible observations grouped by active point (point-major)
+    const int* po_cam;     // camera index
+    const int* po_ac;      // active camera index or -1 (gauge / unobserved)
+    const double2* po_uv;  // pixel
+    const double* po_depth;
+    const int* po_ap;      // active point index
+    const int* pt_ptr;     // [n_ap+1]
+    const int* pt_idx;     // active point -> point index
+    // admissible observations grouped by camera (camera-major)
+    const int* co_pt;
+    const double2* co_uv;
+    const double* co_depth;
+    const int* seg_ptr;  // [n_seg+1]
+    const int* seg_cam;  // [n_seg]
+    const int* seg_ac;   // [n_seg]
+    const int* ac_cam;   // active camera -> camera index
+    int n_seg, n_ap, n_adm, nac;
+    int n;     // reduced system size 6*nac + 4
+    int npad;  // n rounded up to 16
+    int kb;    // first intrinsics row = 6*nac
+    int off_pt, off_k;  // scale-vector offsets
+    int part_stride;
+};
+
+struct DevWork {
+    double* camdata;
+    double* seg_intr;
+    double* lin;
+    double* scale;
+    double* cnp;
+    double* pdata;
+    double* S;
+    double* rhs;  // rhs in, y out (after factor)
+    double* delta;
+    double* part;
+    double* scal;
+    int* chol_flag;
+    int* fcol;
+    int* rptr;
+    int* rows;
+};
+
+// kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
+enum KernelId {
+    K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_OBS_PAIRS,
+    K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_COUNT
+};
+static const char* const kKernelNames[K_COUNT] = {
+    "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "obs_pairs",
+    "chol", "update_cams", "backsub_eval", "final"};
+
+// Records an event pair around each launch on the launch stream.
+struct Prof {
+    static constexpr int MAXP = 64;
+    int on = 0;
+    int n = 0;
+    int id[MAXP];
+    hipEvent_t ev[2 * MAXP];
+    void begin(int k, hipStream_t s) {
+        if (on && n < MAXP) { (void)hipEventRecord(ev[2 * n], s); id[n] = k; }
+    }
+    void end(hipStream_t s) {
+        if (on && n < MAXP) { (void)hipEventRecord(ev[2 * n + 1], s); ++n; }
+    }
+};
+
+hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int cur, int jacobi, DevWork& W, hipStream_t s,
+                        Prof* pf);
+hipError_t launch_build(const DevProblem& P, const BaConsts& c, int cur, double radius, DevWork& W, hipStream_t s,
+                        Prof* pf);
+hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_update(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, int cur, double* res, double* jc, double* jp,
+                            double* jk, hipStream_t s);
+
+}  // namespace miba

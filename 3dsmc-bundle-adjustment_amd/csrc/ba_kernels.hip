@@ -1,0 +1,875 @@
+// ba_kernels.hip — libmiba HIP kernels for gfx950 (MI355X / CDNA4), f64 throughout.
+//
+// One LM iteration of the reference's ceres::Solve (OptimizationUtils.cpp:300;
+// LM + SPARSE_SCHUR, BundleAdjustmentConfig.h:61-67) is, on the device:
+//
+//   k_cam_side      camera-major pass: per camera  U=Jc^T Jc, C=Jc^T Jk, g=Jc^T f
+//                   (+ intrinsics JkJk, Jk^T f, cost)  [only after an accepted step]
+//   k_lin_finalize  reduce intrinsics partials, gradient max-norm of cams/intrinsics
+//   k_point_prep    point-major pass: per point V, e, K (scaled, LM-damped), V^-1,
+//                   intrinsics Schur term                           [every iteration]
+//   k_assemble      reduced camera system S = blocks(U + D^2, C, Ukk) and rhs
+//   k_obs_pairs     Schur scatter  S -= W V^-1 W^T, rhs -= W V^-1 e (global f64 atomics)
+//   k_chol          envelope-blocked Cholesky of S + forward/back solve (1 workgroup,
+//                   v_mfma_f64_16x16x4_f64 for the trailing 16x16 tile updates)
+//   k_update_cams   delta = -s*y, Sophus T*exp(delta), prior-block terms
+//   k_backsub_eval  point back-substitution, model cost change -(J d)^T(f + J d/2),
+//                   candidate cost at x + delta
+//   k_final         deterministic reduction of the per-block partials
+//
+// The residual/Jacobian is never stored: it is recomputed from the 32-byte
+// observation record + the resident pose/point (cheaper than 304 B/obs of
+// stored Jacobian blocks; DESIGN.md "Roofline").
+#include <hip/hip_runtime.h>
+
+#include "ba_device.h"
+#include "ba_kernels.h"
+
+namespace miba {
+
+static constexpr int TPB = 256;
+
+// ---------------------------------------------------------------- reductions
+template <int NV>
+__device__ __forceinline__ void wave_sum(double (&v)[NV]) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
+}
+
+// Block (256 threads) sum of NV values; result valid in out[0..NV) after return (LDS).
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* lds /*4*NV*/, double* out /*NV*/) {
+    wave_sum<NV>(v);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < NV; i += blockDim.x)
+        out[i] = lds[0 * NV + i] + lds[1 * NV + i] + lds[2 * NV + i] + lds[3 * NV + i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ double block_max(double v, double* lds) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) lds[wave] = v;
+    __syncthreads();
+    const double r = fmax(fmax(lds[0], lds[1]), fmax(lds[2], lds[3]));
+    __syncthreads();
+    return r;
+}
+
+// ---------------------------------------------------------------- camera side
+// One workgroup per camera segment of the camera-major observation list.
+// camdata[ac*CAMDATA + ..]: U upper-packed (21), C (6x4 = 24), g (6)
+// seg_intr[s*SEGINTR + ..]: Ukk upper-packed (10), gk (4), cost (1)
+__global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, int cur, double* __restrict__ camdata,
+                                                  double* __restrict__ seg_intr) {
+    __shared__ double lds[4 * 66];
+    __shared__ double out[66];
+    const int s = blockIdx.x;
+    const int cam = P.seg_cam[s];
+    const int ac = P.seg_ac[s];
+    const double* pose = P.cams[cur] + 7 * cam;
+    const double* pts = P.pts[cur];
+    const double* K = P.K[cur];
+    double acc[66];
+#pragma unroll
+    for (int i = 0; i < 66; ++i) acc[i] = 0.0;
+    const int o0 = P.seg_ptr[s], o1 = P.seg_ptr[s + 1];
+    for (int o = o0 + threadIdx.x; o < o1; o += TPB) {
+        const double2 uv = P.co_uv[o];
+        ObsEval e;
+        double jc[18], jp[9], jk[8];
+        lin_obs(c, pose, pts + 3 * P.co_pt[o], K, uv.x, uv.y, P.co_depth[o], e, jc, jp, jk);
+        (void)jp;
+        if (ac >= 0) {
+            int q = 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = i; j < 6; ++j, ++q) acc[q] += jc[i] * jc[j] + jc[6 + i] * jc[6 + j] + jc[12 + i] * jc[12 + j];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc[21 + i * 4 + m] += jc[i] * jk[m] + jc[6 + i] * jk[4 + m];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) acc[45 + i] += jc[i] * e.f[0] + jc[6 + i] * e.f[1] + jc[12 + i] * e.f[2];
+        }
+        int q = 51;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int l = m; l < 4; ++l, ++q) acc[q] += jk[m] * jk[l] + jk[4 + m] * jk[4 + l];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[61 + m] += jk[m] * e.f[0] + jk[4 + m] * e.f[1];
+        acc[65] += e.ok ? e.cost : __builtin_nan("");
+    }
+    block_sum<66>(acc, lds, out);
+    if (ac >= 0)
+        for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)ac * CAMDATA + i] = out[i];
+    for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = out[51 + i];
+}
+
+// Reduce intrinsics partials (fixed order), add the IntrinsicsPrior block
+// (OptimizationUtils.cpp:117-125, squared loss), compute the gradient max-norm of
+// cameras + intrinsics: ||x - Plus(x, -g)||_inf (Ceres 2.0 trust_region_minimizer).
+// lin[0] = cost(x), lin[1] = gmax(cams, intr), lin[2..12) = Ukk packed, lin[12..16) = gk
+__global__ __launch_bounds__(TPB) void k_lin_finalize(DevProblem P, BaConsts c, int cur, const double* __restrict__ camdata,
+                                                      const double* __restrict__ seg_intr, double* __restrict__ lin) {
+    __shared__ double lds[4 * SEGINTR];
+    __shared__ double out[SEGINTR];
+    __shared__ double red[4];
+    double acc[SEGINTR];
+#pragma unroll
+    for (int i = 0; i < SEGINTR; ++i) acc[i] = 0.0;
+    // fixed-order: each thread sums a strided subset; block_sum order is fixed too
+    for (int s = threadIdx.x; s < P.n_seg; s += TPB)
+#pragma unroll
+        for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)s * SEGINTR + i];
+    block_sum<SEGINTR>(acc, lds, out);
+    const double* K = P.K[cur];
+    double gm = 0.0;
+    for (int ac = threadIdx.x; ac < P.nac; ac += TPB) {
+        const int cam = P.ac_cam[ac];
+        const double* x = P.cams[cur] + 7 * cam;
+        double ng[6], tp[7];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) ng[d] = -camdata[(size_t)ac * CAMDATA + 45 + d];
+        se3_plus(x, ng, tp);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) gm = fmax(gm, fabs(x[j] - tp[j]));
+    }
+    gm = block_max(gm, red);
+    if (threadIdx.x == 0) {
+        double pc = 0.0;
+        double gk[4];
+        for (int m = 0; m < 4; ++m) {
+            const double fk = c.sw_k * (P.prior[m] - K[m]);
+            pc += fk * fk;
+            gk[m] = out[10 + m] + (-c.sw_k) * fk;
+            gm = fmax(gm, fabs(K[m] - (K[m] + -gk[m])));
+        }
+        lin[0] = out[14] + 0.5 * pc;
+        lin[1] = gm;
+        for (int q = 0; q < 10; ++q) lin[2 + q] = out[q];
+        // prior block: J = -sqrt(w) I adds w on the diagonal of Ukk
+        int q = 0;
+        for (int m = 0; m < 4; ++m)
+            for (int l = m; l < 4; ++l, ++q)
+                if (l == m) lin[2 + q] += c.sw_k * c.sw_k;
+        for (int m = 0; m < 4; ++m) lin[12 + m] = gk[m];
+    }
+}
+
+// ---------------------------------------------------------------- point side
+// mode 0: column norms only (iteration 0, before the Jacobi scale exists)
+// mode 1: full Schur preparation.
+// pdata[ap*PDATA]: Vinv packed (6: 00 01 02 11 12 22), e (3), Kt (12, [m][i])
+__global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, int cur, int mode, double radius,
+                                                    const double* __restrict__ scale, double* __restrict__ cnp,
+                                                    double* __restrict__ pdata, double* __restrict__ S,
+                                                    double* __restrict__ rhs, double* __restrict__ part) {
+    __shared__ double lds[4 * 14];
+    __shared__ double out[14];
+    __shared__ double red[4];
+    const int ap = blockIdx.x * TPB + threadIdx.x;
+    double kk[14];
+#pragma unroll
+    for (int i = 0; i < 14; ++i) kk[i] = 0.0;
+    double gmax = 0.0, bad = 0.0;
+    if (ap < P.n_ap) {
+        const int pi = P.pt_idx[ap];
+        const double* X = P.pts[cur] + 3 * pi;
+        const double* K = P.K[cur];
+        double V[6] = {0, 0, 0, 0, 0, 0}, e[3] = {0, 0, 0}, Kt[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) Kt[i] = 0.0;
+        for (int o = P.pt_ptr[ap]; o < P.pt_ptr[ap + 1]; ++o) {
+            const double2 uv = P.po_uv[o];
+            ObsEval ev;
+            double jc[18], jp[9], jk[8];
+            lin_obs(c, P.cams[cur] + 7 * P.po_cam[o], X, K, uv.x, uv.y, P.po_depth[o], ev, jc, jp, jk);
+            (void)jc;
+            V[0] += jp[0] * jp[0] + jp[3] * jp[3] + jp[6] * jp[6];
+            V[1] += jp[0] * jp[1] + jp[3] * jp[4] + jp[6] * jp[7];
+            V[2] += jp[0] * jp[2] + jp[3] * jp[5] + jp[6] * jp[8];
+            V[3] += jp[1] * jp[1] + jp[4] * jp[4] + jp[7] * jp[7];
+            V[4] += jp[1] * jp[2] + jp[4] * jp[5] + jp[7] * jp[8];
+            V[5] += jp[2] * jp[2] + jp[5] * jp[5] + jp[8] * jp[8];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) e[i] += jp[i] * ev.f[0] + jp[3 + i] * ev.f[1] + jp[6 + i] * ev.f[2];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Kt[m * 3 + i] += jk[m] * jp[i] + jk[4 + m] * jp[3 + i];
+        }
+        if (mode == 0) {
+            cnp[3 * ap + 0] = V[0];
+            cnp[3 * ap + 1] = V[3];
+            cnp[3 * ap + 2] = V[5];
+        } else {
+            // gradient max-norm contribution (points: x - (x + -g))
+#pragma unroll
+            for (int i = 0; i < 3; ++i) gmax = fmax(gmax, fabs(X[i] - (X[i] + -e[i])));
+            const double* sp = scale + P.off_pt + 3 * ap;
+            const double* sk = scale + P.off_k;
+            const double s0 = sp[0], s1 = sp[1], s2 = sp[2];
+            // scaled, damped V  (Ceres: lm_diagonal = sqrt(clamp(diag(JtJ~)) / radius))
+            double v00 = s0 * V[0] * s0, v01 = s0 * V[1] * s1, v02 = s0 * V[2] * s2;
+            double v11 = s1 * V[3] * s1, v12 = s1 * V[4] * s2, v22 = s2 * V[5] * s2;
+            v00 += fmin(fmax(v00, c.min_diag), c.max_diag) / radius;
+            v11 += fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
+            v22 += fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
+            // 3x3 SPD inverse via Cholesky
+            double Vi[6] = {0, 0, 0, 0, 0, 0};
+            const bool pd = v00 > 0.0;
+            const double L00 = sqrt(v00);
+            const double L10 = v01 / L00, L20 = v02 / L00;
+            const double l11 = v11 - L10 * L10;
+            const double L11 = sqrt(l11);
+            const double L21 = (v12 - L20 * L10) / L11;
+            const double l22 = v22 - L20 * L20 - L21 * L21;
+            const double L22 = sqrt(l22);
+            if (pd && l11 > 0.0 && l22 > 0.0 && isfinite(l22)) {
+                const double i00 = 1 / L00, i11 = 1 / L11, i22 = 1 / L22;
+                const double i10 = -L10 * i00 * i11;
+                const double i21 = -L21 * i11 * i22;
+                const double i20 = -(L20 * i00 + L21 * i10) * i22;
+                // Vi = Li^T Li
+                Vi[0] = i00 * i00 + i10 * i10 + i20 * i20;
+                Vi[1] = i10 * i11 + i20 * i21;
+                Vi[2] = i20 * i22;
+                Vi[3] = i11 * i11 + i21 * i21;
+                Vi[4] = i21 * i22;
+                Vi[5] = i22 * i22;
+            } else {
+                bad = 1.0;
+            }
+            double es[3] = {s0 * e[0], s1 * e[1], s2 * e[2]};
+            double Ks[12];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                Ks[m * 3 + 0] = sk[m] * Kt[m * 3 + 0] * s0;
+                Ks[m * 3 + 1] = sk[m] * Kt[m * 3 + 1] * s1;
+                Ks[m * 3 + 2] = sk[m] * Kt[m * 3 + 2] * s2;
+            }
+            double* pd_out = pdata + (size_t)ap * PDATA;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) pd_out[i] = Vi[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) pd_out[6 + i] = es[i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pd_out[9 + i] = Ks[i];
+            // intrinsics Schur terms: -Ks Vi Ks^T (10 packed) and -Ks Vi es (4)
+            const double Vf[9] = {Vi[0], Vi[1], Vi[2], Vi[1], Vi[3], Vi[4], Vi[2], Vi[4], Vi[5]};
+            double YK[12];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    YK[m * 3 + j] = Ks[m * 3 + 0] * Vf[0 * 3 + j] + Ks[m * 3 + 1] * Vf[1 * 3 + j] + Ks[m * 3 + 2] * Vf[2 * 3 + j];
+            int q = 0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int l = m; l < 4; ++l, ++q)
+                    kk[q] = -(YK[m * 3 + 0] * Ks[l * 3 + 0] + YK[m * 3 + 1] * Ks[l * 3 + 1] + YK[m * 3 + 2] * Ks[l * 3 + 2]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) kk[10 + m] = -(YK[m * 3 + 0] * es[0] + YK[m * 3 + 1] * es[1] + YK[m * 3 + 2] * es[2]);
+        }
+    }
+    if (mode == 0) return;
+    block_sum<14>(kk, lds, out);
+    gmax = block_max(gmax, red);
+    bad = block_max(bad, red);
+    if (threadIdx.x == 0) {
+        const int kb = P.kb;
+        int q = 0;
+        for (int m = 0; m < 4; ++m)
+            for (int l = m; l < 4; ++l, ++q) atomicAdd(&S[(size_t)(kb + l) * P.npad + kb + m], out[q]);
+        for (int m = 0; m < 4; ++m) atomicAdd(&rhs[kb + m], out[10 + m]);
+        part[PART_PT_GMAX * P.part_stride + blockIdx.x] = gmax;
+        part[PART_PT_BAD * P.part_stride + blockIdx.x] = bad;
+    }
+}
+
+// Jacobi scale (Ceres: 1 / (1 + sqrt(squared column norm)), iteration 0 only)
+__global__ void k_scale(DevProblem P, const double* __restrict__ camdata, const double* __restrict__ cnp,
+                        const double* __restrict__ lin, int jacobi, double* __restrict__ scale) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ncam = 6 * P.nac, npt = 3 * P.n_ap;
+    double cn = -1.0;
+    int dst = -1;
+    if (t < ncam) {
+        const int ac = t / 6, d = t % 6;
+        // diag of the packed upper U: index of (d,d) = d*6 - d*(d-1)/2
+        cn = camdata[(size_t)ac * CAMDATA + d * 6 - (d * (d - 1)) / 2];
+        dst = t;
+    } else if (t < ncam + npt) {
+        cn = cnp[t - ncam];
+        dst = P.off_pt + (t - ncam);
+    } else if (t < ncam + npt + 4) {
+        const int m = t - ncam - npt;
+        cn = lin[2 + m * 4 - (m * (m - 1)) / 2];
+        dst = P.off_k + m;
+    }
+    if (dst >= 0) scale[dst] = jacobi ? 1.0 / (1.0 + sqrt(cn)) : 1.0;
+}
+
+// ---------------------------------------------------------------- assembly
+// Writes the camera/intrinsics (F-block) part of the damped, scaled normal
+// equations into the lower triangle of S (row-major, npad stride) and rhs = J~^T f.
+__global__ void k_assemble(DevProblem P, BaConsts c, double radius, const double* __restrict__ camdata,
+                           const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
+                           double* __restrict__ rhs) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t ld = P.npad;
+    const int kb = P.kb;
+    const double* sk = scale + P.off_k;
+    if (t < P.nac) {
+        const int ac = t;
+        const double* cd = camdata + (size_t)ac * CAMDATA;
+        const double* sc = scale + 6 * ac;
+        const int b = 6 * ac;
+        int q = 0;
+        for (int i = 0; i < 6; ++i)
+            for (int j = i; j < 6; ++j, ++q) {
+                double v = sc[i] * cd[q] * sc[j];
+                if (i == j) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
+                S[(size_t)(b + j) * ld + b + i] = v;  // lower: row b+j >= col b+i
+            }
+        for (int i = 0; i < 6; ++i)
+            for (int m = 0; m < 4; ++m) S[(size_t)(kb + m) * ld + b + i] = sc[i] * cd[21 + i * 4 + m] * sk[m];
+        for (int i = 0; i < 6; ++i) rhs[b + i] = sc[i] * cd[45 + i];
+    } else if (t == P.nac) {
+        int q = 0;
+        for (int m = 0; m < 4; ++m)
+            for (int l = m; l < 4; ++l, ++q) {
+                double v = sk[m] * lin[2 + q] * sk[l];
+                if (l == m) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
+                S[(size_t)(kb + l) * ld + kb + m] = v;
+            }
+        for (int m = 0; m < 4; ++m) rhs[kb + m] = sk[m] * lin[12 + m];
+        for (int r = P.n; r < P.npad; ++r) { S[(size_t)r * ld + r] = 1.0; rhs[r] = 0.0; }
+    }
+}
+
+// Schur scatter: thread per admissible observation (point-major) whose camera is active.
+__global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+                                                   const double* __restrict__ pdata, double* __restrict__ S,
+                                                   double* __restrict__ rhs) {
+    const int a = blockIdx.x * TPB + threadIdx.x;
+    if (a >= P.n_adm) return;
+    const int ca = P.po_ac[a];
+    if (ca < 0) return;
+    const int ap = P.po_ap[a];
+    const size_t ld = P.npad;
+    const int kb = P.kb;
+    const double* pd = pdata + (size_t)ap * PDATA;
+    const double Vf[9] = {pd[0], pd[1], pd[2], pd[1], pd[3], pd[4], pd[2], pd[4], pd[5]};
+    const double* sp = scale + P.off_pt + 3 * ap;
+    const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
+    const double* K = P.K[cur];
+    // W~_a = s_c (Jc^T Jp) s_p
+    double Y[18];
+    {
+        const double2 uv = P.po_uv[a];
+        ObsEval ev;
+        double jc[18], jp[9], jk[8];
+        lin_obs(c, P.cams[cur] + 7 * P.po_cam[a], X, K, uv.x, uv.y, P.po_depth[a], ev, jc, jp, jk);
+        const double* sc = scale + 6 * ca;
+        double W[18];
+#pragma unroll
+        for (int d = 0; d < 6; ++d)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                W[d * 3 + i] = sc[d] * (jc[d] * jp[i] + jc[6 + d] * jp[3 + i] + jc[12 + d] * jp[6 + i]) * sp[i];
+#pragma unroll
+        for (int d = 0; d < 6; ++d)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                Y[d * 3 + i] = W[d * 3 + 0] * Vf[0 * 3 + i] + W[d * 3 + 1] * Vf[1 * 3 + i] + W[d * 3 + 2] * Vf[2 * 3 + i];
+    }
+    // rhs_c -= Y e ; border -= Y Kt^T
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        atomicAdd(&rhs[6 * ca + d], -(Y[d * 3 + 0] * pd[6] + Y[d * 3 + 1] * pd[7] + Y[d * 3 + 2] * pd[8]));
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            atomicAdd(&S[(size_t)(kb + m) * ld + 6 * ca + d],
+                      -(Y[d * 3 + 0] * pd[9 + m * 3 + 0] + Y[d * 3 + 1] * pd[9 + m * 3 + 1] + Y[d * 3 + 2] * pd[9 + m * 3 + 2]));
+    }
+    // pairs (a,b) with cam(b) > cam(a) or (same cam and b >= a)
+    for (int b = P.pt_ptr[ap]; b < P.pt_ptr[ap + 1]; ++b) {
+        const int cb = P.po_ac[b];
+        if (cb < ca || (cb == ca && b < a)) continue;
+        const double2 uv = P.po_uv[b];
+        ObsEval ev;
+        double jc[18], jp[9], jk[8];
+        lin_obs(c, P.cams[cur] + 7 * P.po_cam[b], X, K, uv.x, uv.y, P.po_depth[b], ev, jc, jp, jk);
+        const double* sc = scale + 6 * cb;
+        double W[18];
+#pragma unroll
+        for (int d = 0; d < 6; ++d)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                W[d * 3 + i] = sc[d] * (jc[d] * jp[i] + jc[6 + d] * jp[3 + i] + jc[12 + d] * jp[6 + i]) * sp[i];
+        // M = Y_a W_b^T  (block (ca, cb)); lower storage S[6cb + e][6ca + d]
+        if (cb > ca) {
+#pragma unroll
+            for (int d = 0; d < 6; ++d)
+#pragma unroll
+                for (int e2 = 0; e2 < 6; ++e2)
+                    atomicAdd(&S[(size_t)(6 * cb + e2) * ld + 6 * ca + d],
+                              -(Y[d * 3 + 0] * W[e2 * 3 + 0] + Y[d * 3 + 1] * W[e2 * 3 + 1] + Y[d * 3 + 2] * W[e2 * 3 + 2]));
+        } else {
+            const bool self = (b == a);
+#pragma unroll
+            for (int d = 0; d < 6; ++d)
+#pragma unroll
+                for (int e2 = d; e2 < 6; ++e2) {
+                    double m = Y[d * 3 + 0] * W[e2 * 3 + 0] + Y[d * 3 + 1] * W[e2 * 3 + 1] + Y[d * 3 + 2] * W[e2 * 3 + 2];
+                    if (!self)
+                        m += Y[e2 * 3 + 0] * W[d * 3 + 0] + Y[e2 * 3 + 1] * W[d * 3 + 1] + Y[e2 * 3 + 2] * W[d * 3 + 2];
+                    atomicAdd(&S[(size_t)(6 * ca + e2) * ld + 6 * ca + d], -m);
+                }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- Cholesky
+// Envelope-blocked right-looking Cholesky of the npad x npad reduced system
+// (lower triangle, row-major), then L z = b, L^T y = z (y overwrites b).
+// One workgroup (4 waves). fcol[i]: first non-zero 16-block column of block row i;
+// rows[rptr[k]..rptr[k+1]): block rows i > k with fcol[i] <= k.
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(TPB) void k_chol(double* __restrict__ A, int npad, int nb, const int* __restrict__ fcol,
+                                              const int* __restrict__ rptr, const int* __restrict__ rows,
+                                              double* __restrict__ b, int* __restrict__ flag) {
+    __shared__ double Lkk[16][17];
+    __shared__ double red[16][17];
+    __shared__ int s_bad;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const size_t ld = npad;
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    for (int kb = 0; kb < nb; ++kb) {
+        const size_t k0 = (size_t)kb * 16;
+        // ---- potrf of the 16x16 diagonal tile, wave 0, lane r holds row r
+        if (wave == 0) {
+            double a[16];
+            const int r = lane & 15;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? A[(k0 + r) * ld + k0 + j] : 0.0;
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                double djj = __shfl(a[j], j);
+                if (!(djj > 0.0) || !isfinite(djj)) { bad = true; djj = 1.0; }
+                const double d = sqrt(djj);
+                double lrj = (r == j) ? d : (r > j ? a[j] / d : 0.0);
+                a[j] = lrj;
+#pragma unroll
+                for (int k = j + 1; k < 16; ++k) {
+                    const double lkj = __shfl(lrj, k);
+                    if (r >= k) a[k] -= lrj * lkj;
+                }
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    Lkk[r][j] = (j <= r) ? a[j] : 0.0;
+                    if (j <= r) A[(k0 + r) * ld + k0 + j] = a[j];
+                }
+            }
+            if (bad && lane == 0) s_bad = 1;
+        }
+        __syncthreads();
+        const int r0 = rptr[kb], r1 = rptr[kb + 1];
+        const int nr = r1 - r0;
+        // ---- TRSM: L_ik = A_ik L_kk^{-T}, thread per row
+        for (int t = tid; t < nr * 16; t += TPB) {
+            const int i = rows[r0 + (t >> 4)];
+            const int r = t & 15;
+            double* row = A + ((size_t)i * 16 + r) * ld + k0;
+            double x[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) x[j] = row[j];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                double s = x[j];
+#pragma unroll
+                for (int m = 0; m < j; ++m) s -= x[m] * Lkk[j][m];
+                x[j] = s / Lkk[j][j];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) row[j] = x[j];
+        }
+        __syncthreads();
+        // ---- trailing update A_ij -= L_ik L_jk^T over tiles (p >= q) of the row list, MFMA f64
+        const int ntiles = nr * (nr + 1) / 2;
+        for (int t = wave; t < ntiles; t += 4) {
+            // map t -> (p, q), q <= p
+            int p = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+            while ((p + 1) * (p + 2) / 2 <= t) ++p;
+            while (p * (p + 1) / 2 > t) --p;
+            const int q = t - p * (p + 1) / 2;
+            const int i = rows[r0 + p], j = rows[r0 + q];
+            const double* Li = A + ((size_t)i * 16) * ld + k0;
+            const double* Lj = A + ((size_t)j * 16) * ld + k0;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            const int rr = lane & 15, kk = lane >> 4;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const double av = Li[(size_t)rr * ld + 4 * s + kk];  // A[i=rr][k]
+                const double bv = Lj[(size_t)rr * ld + 4 * s + kk];  // B[k][j=rr] = L_jk[rr][k]
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+            double* Cij = A + ((size_t)i * 16) * ld + (size_t)j * 16;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int row = kk + 4 * g, col = rr;  // f64 C/D map: row = (lane>>4) + 4*reg
+                Cij[(size_t)row * ld + col] -= acc[g];
+            }
+        }
+        __syncthreads();
+    }
+    // ---- forward solve L z = b
+    for (int i = 0; i < nb; ++i) {
+        const int r = tid & 15, p = tid >> 4;  // 16 rows x 16 parts
+        double s = 0.0;
+        const size_t row = (size_t)i * 16 + r;
+        for (int col = fcol[i] * 16 + p; col < i * 16; col += 16) s += A[row * ld + col] * b[col];
+        red[p][r] = s;
+        __syncthreads();
+        if (wave == 0) {
+            const int rr = lane & 15;
+            double v = b[(size_t)i * 16 + rr];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v -= red[q][rr];
+            // L_ii z = v, lane rr owns row rr
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const double lmm = A[((size_t)i * 16 + m) * ld + (size_t)i * 16 + m];
+                double zm = __shfl(v, m) / lmm;
+                if (rr > m) v -= A[((size_t)i * 16 + rr) * ld + (size_t)i * 16 + m] * zm;
+                if (rr == m) v = zm;
+            }
+            if (lane < 16) b[(size_t)i * 16 + rr] = v;
+        }
+        __syncthreads();
+    }
+    // ---- backward solve L^T y = z
+    for (int i = nb - 1; i >= 0; --i) {
+        const int r = tid & 15, p = tid >> 4;
+        double s = 0.0;
+        const int r0 = rptr[i], r1 = rptr[i + 1];
+        for (int t = r0; t < r1; ++t) {
+            const int j = rows[t];
+            // sum_c L[16j + c][16i + r] y[16j + c], c split over parts p
+            const size_t rowj = (size_t)j * 16 + p;
+            s += A[rowj * ld + (size_t)i * 16 + r] * b[rowj];
+        }
+        red[p][r] = s;
+        __syncthreads();
+        if (wave == 0) {
+            const int rr = lane & 15;
+            double v = b[(size_t)i * 16 + rr];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v -= red[q][rr];
+            // L_ii^T y = v : y_m for m = 15..0 ; (L^T)[rr][m] = L[m][rr]
+#pragma unroll
+            for (int m = 15; m >= 0; --m) {
+                const double lmm = A[((size_t)i * 16 + m) * ld + (size_t)i * 16 + m];
+                double ym = __shfl(v, m) / lmm;
+                if (rr < m) v -= A[((size_t)i * 16 + m) * ld + (size_t)i * 16 + rr] * ym;
+                if (rr == m) v = ym;
+            }
+            if (lane < 16) b[(size_t)i * 16 + rr] = v;
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && s_bad) *flag = 1;
+}
+
+// ---------------------------------------------------------------- update
+// delta = -s * y over cameras and intrinsics; candidate poses; prior-block model
+// change and candidate prior cost. part[PART_UPD_* * stride + block]
+__global__ void k_update_cams(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+                              const double* __restrict__ y, double* __restrict__ delta, double* __restrict__ part) {
+    __shared__ double lds[4 * 3];
+    __shared__ double out[3];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    double acc[3] = {0.0, 0.0, 0.0};  // sn2, mcc, cand cost
+    if (t < P.nac) {
+        const int cam = P.ac_cam[t];
+        double d[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            d[k] = -y[6 * t + k] * scale[6 * t + k];
+            delta[6 * t + k] = d[k];
+        }
+        const double* x = P.cams[cur] + 7 * cam;
+        double* xn = P.cams[cur ^ 1] + 7 * cam;
+        double tp[7];
+        se3_plus(x, d, tp);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            xn[j] = tp[j];
+            const double df = x[j] - tp[j];
+            acc[0] += df * df;
+        }
+    } else if (t == P.nac) {
+        const double* K = P.K[cur];
+        double* Kn = P.K[cur ^ 1];
+        for (int m = 0; m < 4; ++m) {
+            const double dk = -y[P.kb + m] * scale[P.off_k + m];
+            delta[P.kb + m] = dk;
+            const double kn = K[m] + dk;
+            Kn[m] = kn;
+            const double df = K[m] - kn;
+            acc[0] += df * df;
+            const double fk = c.sw_k * (P.prior[m] - K[m]);
+            const double jd = -c.sw_k * dk;
+            acc[1] += -jd * (fk + jd / 2.0);
+            const double fn = c.sw_k * (P.prior[m] - kn);
+            acc[2] += 0.5 * fn * fn;
+        }
+    }
+    block_sum<3>(acc, lds, out);
+    if (threadIdx.x == 0) {
+        part[PART_UPD_SN2 * P.part_stride + blockIdx.x] = out[0];
+        part[PART_UPD_MCC * P.part_stride + blockIdx.x] = out[1];
+        part[PART_UPD_COST * P.part_stride + blockIdx.x] = out[2];
+    }
+}
+
+// Back-substitution y_p = V^-1 (e - sum W^T y_c - Kt^T y_k), delta_p = -s_p y_p,
+// model cost change over the point's observations and the candidate cost.
+__global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+                                                      const double* __restrict__ pdata, const double* __restrict__ y,
+                                                      const double* __restrict__ delta, double* __restrict__ part) {
+    __shared__ double lds[4 * 4];
+    __shared__ double out[4];
+    const int ap = blockIdx.x * TPB + threadIdx.x;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cost, bad
+    if (ap < P.n_ap) {
+        const int pi = P.pt_idx[ap];
+        const double* X = P.pts[cur] + 3 * pi;
+        double* Xn = P.pts[cur ^ 1] + 3 * pi;
+        const double* K = P.K[cur];
+        const double* Kn = P.K[cur ^ 1];
+        const double* pd = pdata + (size_t)ap * PDATA;
+        const double* sp = scale + P.off_pt + 3 * ap;
+        const double* yk = y + P.kb;
+        double t[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            t[i] = pd[6 + i] - (pd[9 + 0 * 3 + i] * yk[0] + pd[9 + 1 * 3 + i] * yk[1] + pd[9 + 2 * 3 + i] * yk[2] +
+                                pd[9 + 3 * 3 + i] * yk[3]);
+        const int o0 = P.pt_ptr[ap], o1 = P.pt_ptr[ap + 1];
+        for (int o = o0; o < o1; ++o) {
+            const int ac = P.po_ac[o];
+            if (ac < 0) continue;
+            const double2 uv = P.po_uv[o];
+            ObsEval ev;
+            double jc[18], jp[9], jk[8];
+            lin_obs(c, P.cams[cur] + 7 * P.po_cam[o], X, K, uv.x, uv.y, P.po_depth[o], ev, jc, jp, jk);
+            const double* sc = scale + 6 * ac;
+            const double* yc = y + 6 * ac;
+            double jy[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                double s = 0.0;
+#pragma unroll
+                for (int d = 0; d < 6; ++d) s += jc[r * 6 + d] * (sc[d] * yc[d]);
+                jy[r] = s;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) t[i] -= sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
+        }
+        double dp[3], xn[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double yp = pd[i == 0 ? 0 : (i == 1 ? 1 : 2)] * t[0] +
+                              pd[i == 0 ? 1 : (i == 1 ? 3 : 4)] * t[1] +
+                              pd[i == 0 ? 2 : (i == 1 ? 4 : 5)] * t[2];
+            dp[i] = -sp[i] * yp;
+            xn[i] = X[i] + dp[i];
+            Xn[i] = xn[i];
+            const double df = X[i] - xn[i];
+            acc[0] += df * df;
+        }
+        const double* dk = delta + P.kb;
+        for (int o = o0; o < o1; ++o) {
+            const int ac = P.po_ac[o];
+            const int cam = P.po_cam[o];
+            const double2 uv = P.po_uv[o];
+            const double dep = P.po_depth[o];
+            ObsEval ev;
+            double jc[18], jp[9], jk[8];
+            lin_obs(c, P.cams[cur] + 7 * cam, X, K, uv.x, uv.y, dep, ev, jc, jp, jk);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                double jd = jp[r * 3 + 0] * dp[0] + jp[r * 3 + 1] * dp[1] + jp[r * 3 + 2] * dp[2];
+                if (ac >= 0) {
+                    const double* dc = delta + 6 * ac;
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) jd += jc[r * 6 + d] * dc[d];
+                }
+                if (r < 2) jd += jk[r * 4 + 0] * dk[0] + jk[r * 4 + 1] * dk[1] + jk[r * 4 + 2] * dk[2] + jk[r * 4 + 3] * dk[3];
+                acc[1] += -jd * (ev.f[r] + jd / 2.0);
+            }
+            ObsEval en;
+            eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, uv.x, uv.y, dep, en);
+            if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
+        }
+        if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
+    }
+    block_sum<4>(acc, lds, out);
+    if (threadIdx.x == 0) {
+        part[PART_BS_SN2 * P.part_stride + blockIdx.x] = out[0];
+        part[PART_BS_MCC * P.part_stride + blockIdx.x] = out[1];
+        part[PART_BS_COST * P.part_stride + blockIdx.x] = out[2];
+        part[PART_BS_BAD * P.part_stride + blockIdx.x] = out[3];
+    }
+}
+
+// ---------------------------------------------------------------- final
+// scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]
+__global__ __launch_bounds__(TPB) void k_final(DevProblem P, int nblk_pt, int nblk_upd, int nblk_bs,
+                                               const double* __restrict__ part, const int* __restrict__ chol_flag,
+                                               double* __restrict__ scal) {
+    __shared__ double lds[4 * 3];
+    __shared__ double out[3];
+    __shared__ double red[4];
+    double acc[3] = {0.0, 0.0, 0.0};
+    double gm = 0.0, bad = 0.0;
+    const size_t st = P.part_stride;
+    for (int i = threadIdx.x; i < nblk_upd; i += TPB) {
+        acc[0] += part[PART_UPD_SN2 * st + i];
+        acc[1] += part[PART_UPD_MCC * st + i];
+        acc[2] += part[PART_UPD_COST * st + i];
+    }
+    for (int i = threadIdx.x; i < nblk_bs; i += TPB) {
+        acc[0] += part[PART_BS_SN2 * st + i];
+        acc[1] += part[PART_BS_MCC * st + i];
+        acc[2] += part[PART_BS_COST * st + i];
+        bad = fmax(bad, part[PART_BS_BAD * st + i]);
+    }
+    for (int i = threadIdx.x; i < nblk_pt; i += TPB) {
+        gm = fmax(gm, part[PART_PT_GMAX * st + i]);
+        bad = fmax(bad, 2.0 * part[PART_PT_BAD * st + i]);
+    }
+    block_sum<3>(acc, lds, out);
+    gm = block_max(gm, red);
+    bad = block_max(bad, red);
+    if (threadIdx.x == 0) {
+        scal[SC_SN2] = out[0];
+        scal[SC_MCC] = out[1];
+        scal[SC_CAND] = out[2];
+        scal[SC_GMAX_PT] = gm;
+        scal[SC_BAD] = bad + (*chol_flag ? 4.0 : 0.0);
+    }
+}
+
+// ---------------------------------------------------------------- debug hook
+// Per admissible observation (point-major order) residual + Jacobians, for the parity tests.
+__global__ void k_debug_lin(DevProblem P, BaConsts c, int cur, double* __restrict__ res, double* __restrict__ jcam,
+                            double* __restrict__ jpt, double* __restrict__ jint) {
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= P.n_adm) return;
+    const int ap = P.po_ap[a];
+    const double2 uv = P.po_uv[a];
+    ObsEval ev;
+    double jc[18], jp[9], jk[8];
+    lin_obs(c, P.cams[cur] + 7 * P.po_cam[a], P.pts[cur] + 3 * P.pt_idx[ap], P.K[cur], uv.x, uv.y, P.po_depth[a], ev,
+            jc, jp, jk);
+    for (int i = 0; i < 3; ++i) res[3 * (size_t)a + i] = ev.f[i];
+    for (int i = 0; i < 18; ++i) jcam[18 * (size_t)a + i] = jc[i];
+    for (int i = 0; i < 9; ++i) jpt[9 * (size_t)a + i] = jp[i];
+    for (int i = 0; i < 8; ++i) jint[8 * (size_t)a + i] = jk[i];
+}
+
+// ---------------------------------------------------------------- launchers
+#define CK(x)                              \
+    do {                                   \
+        hipError_t e_ = (x);               \
+        if (e_ != hipSuccess) return e_;   \
+    } while (0)
+
+static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
+
+#define PL(kid, ...)                        \
+    do {                                    \
+        if (pf) pf->begin(kid, s);          \
+        hipLaunchKernelGGL(__VA_ARGS__);    \
+        if (pf) pf->end(s);                 \
+        CK(hipGetLastError());              \
+    } while (0)
+
+hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf) {
+    if (P.n_seg > 0) PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, cur, W.camdata, W.seg_intr);
+    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, cur, W.camdata, W.seg_intr, W.lin);
+    return hipSuccess;
+}
+
+hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int cur, int jacobi, DevWork& W, hipStream_t s,
+                        Prof* pf) {
+    if (P.n_ap > 0)
+        PL(K_POINT_COLNORM, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, cur, 0, 1.0, W.scale,
+           W.cnp, W.pdata, W.S, W.rhs, W.part);
+    const int nt = 6 * P.nac + 3 * P.n_ap + 4;
+    PL(K_SCALE, k_scale, dim3(nblocks(nt, TPB)), dim3(TPB), 0, s, P, W.camdata, W.cnp, W.lin, jacobi, W.scale);
+    return hipSuccess;
+}
+
+hipError_t launch_build(const DevProblem& P, const BaConsts& c, int cur, double radius, DevWork& W, hipStream_t s,
+                        Prof* pf) {
+    if (pf) pf->begin(K_MEMSET_S, s);
+    CK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
+    CK(hipMemsetAsync(W.chol_flag, 0, sizeof(int), s));
+    if (pf) pf->end(s);
+    PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, radius, W.camdata, W.lin, W.scale,
+       W.S, W.rhs);
+    if (P.n_ap > 0)
+        PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, cur, 1, radius, W.scale,
+           W.cnp, W.pdata, W.S, W.rhs, W.part);
+    if (P.n_adm > 0)
+        PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata, W.S,
+           W.rhs);
+    return hipSuccess;
+}
+
+hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
+    PL(K_CHOL, k_chol, dim3(1), dim3(TPB), 0, s, W.S, P.npad, P.npad / 16, W.fcol, W.rptr, W.rows, W.rhs,
+       W.chol_flag);
+    return hipSuccess;
+}
+
+hipError_t launch_update(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf) {
+    const int nb_upd = nblocks(P.nac + 1, TPB);
+    PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, cur, W.scale, W.rhs, W.delta, W.part);
+    const int nb_bs = nblocks(P.n_ap, TPB);
+    if (P.n_ap > 0)
+        PL(K_BACKSUB_EVAL, k_backsub_eval, dim3(nb_bs), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata, W.rhs, W.delta,
+           W.part);
+    PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0, nb_upd,
+       P.n_ap > 0 ? nb_bs : 0, W.part, W.chol_flag, W.scal);
+    return hipSuccess;
+}
+
+hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, int cur, double* res, double* jc, double* jp,
+                            double* jk, hipStream_t s) {
+    if (P.n_adm > 0)
+        hipLaunchKernelGGL(k_debug_lin, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, cur, res, jc, jp, jk);
+    return hipGetLastError();
+}
+
+}  // namespace miba

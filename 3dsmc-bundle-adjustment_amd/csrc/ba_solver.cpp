@@ -1,0 +1,778 @@
+// ba_solver.cpp — libmiba host side: the C-ABI of include/ba.h.
+//
+// ba_solve() replaces `ceres::Solve(globalProblem.options, &problem, &summary)`
+// at /root/reference/src/OptimizationUtils.cpp:300 for the problem assembled at
+// :236-299. The trust-region control flow below restates Ceres 2.0's
+// TrustRegionMinimizer::Minimize with LevenbergMarquardtStrategy;
+// every numeric pass over observations / points / the reduced camera system runs
+// on the GPU (ba_kernels.hip). Per iteration the host reads back 8 scalars.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstdint>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ba.h"
+#include "ba_kernels.h"
+
+using namespace miba;
+
+namespace {
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+enum BufId {
+    B_CAMS0, B_CAMS1, B_PTS0, B_PTS1, B_K0, B_K1, B_PRIOR,
+    B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PT_PTR, B_PT_IDX,
+    B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
+    B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
+    B_FCOL, B_RPTR, B_ROWS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_DBG0, B_DBG1, B_DBG2, B_DBG3,
+    B_COUNT
+};
+
+}  // namespace
+
+struct ba_context {
+    ba_options opts;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    DevBuf buf[B_COUNT];
+    std::string err;
+    // host-side structure of the last prepared problem
+    std::vector<int> po_orig;  // point-major admissible obs -> original obs index
+    std::vector<int> pt_idx, ac_cam;
+    DevProblem P{};
+    DevWork W{};
+    BaConsts C{};
+    int nblk_pt = 0;
+    bool prepared = false;
+    int prep_nc = -1, prep_np = -1, prep_no = -1;
+    // per-kernel profiling
+    Prof prof;
+    bool prof_events = false;
+    int k_launches[K_COUNT] = {0};
+    double k_ms[K_COUNT] = {0};
+    double k_bytes[K_COUNT] = {0};
+    double k_flops[K_COUNT] = {0};
+    Prof* pf() { return opts.profile_kernels ? &prof : nullptr; }
+};
+
+static void flush_prof(ba_context* ctx) {
+    Prof& P = ctx->prof;
+    for (int i = 0; i < P.n; ++i) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, P.ev[2 * i], P.ev[2 * i + 1]) == hipSuccess) {
+            ctx->k_ms[P.id[i]] += ms;
+            ctx->k_launches[P.id[i]] += 1;
+        }
+    }
+    P.n = 0;
+}
+
+static thread_local std::string g_err;
+
+#define HIPCHECK(ctx, x)                                                                  \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            (ctx)->err = std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x; \
+            return BA_E_DEVICE;                                                           \
+        }                                                                                 \
+    } while (0)
+
+template <class T>
+static hipError_t upload(ba_context* ctx, int id, const T* src, size_t n) {
+    hipError_t e = ctx->buf[id].ensure(sizeof(T) * std::max<size_t>(n, 1));
+    if (e != hipSuccess) return e;
+    if (n) e = hipMemcpyAsync(ctx->buf[id].p, src, sizeof(T) * n, hipMemcpyHostToDevice, ctx->stream);
+    return e;
+}
+
+extern "C" {
+
+int32_t ba_api_version(void) { return BA_API_VERSION; }
+
+const char* ba_build_info(void) {
+    return "libmiba " __DATE__ " gfx950 f64; kernels: cam_side/point_prep/obs_pairs(atomic)/chol(env,mfma_f64_16x16x4)/"
+           "backsub_eval";
+}
+
+void ba_default_options(ba_options* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->hub_p_repr = 1e-3;         // BundleAdjustmentConfig.h:47
+    o->hub_p_unpr = 1e-3;         // :50
+    o->weight_intrinsics = 1e-6;  // :48
+    o->weight_unpr = 10.0;        // :49
+    o->max_num_iterations = 75;   // :64
+    o->minimizer_progress_to_stdout = 1;  // :63
+    o->eta = 1e-6;                // :65
+    o->initial_trust_region_radius = 1e4;  // Ceres 2.0 defaults below
+    o->max_trust_region_radius = 1e16;
+    o->min_trust_region_radius = 1e-32;
+    o->min_relative_decrease = 1e-3;
+    o->min_lm_diagonal = 1e-6;
+    o->max_lm_diagonal = 1e32;
+    o->max_num_consecutive_invalid_steps = 5;
+    o->jacobi_scaling = 1;
+    o->function_tolerance = 1e-6;
+    o->gradient_tolerance = 1e-10;
+    o->parameter_tolerance = 1e-8;
+    o->device = -1;
+    o->deterministic = 0;
+}
+
+ba_context* ba_create(const ba_options* opts) {
+    ba_context* ctx = new ba_context();
+    if (opts) ctx->opts = *opts; else ba_default_options(&ctx->opts);
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) {
+        g_err = std::string("no HIP device available: ") + hipGetErrorString(e);
+        delete ctx;
+        return nullptr;
+    }
+    if (ctx->opts.device >= 0) {
+        if (ctx->opts.device >= ndev) {
+            g_err = "device ordinal out of range";
+            delete ctx;
+            return nullptr;
+        }
+        ctx->device = ctx->opts.device;
+        e = hipSetDevice(ctx->device);
+    } else {
+        e = hipGetDevice(&ctx->device);
+    }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (ctx->opts.profile_kernels) {
+        for (int i = 0; i < 2 * Prof::MAXP && e == hipSuccess; ++i) e = hipEventCreate(&ctx->prof.ev[i]);
+        ctx->prof_events = (e == hipSuccess);
+        ctx->prof.on = 1;
+    }
+    if (e != hipSuccess) {
+        g_err = std::string("HIP init failed: ") + hipGetErrorString(e);
+        delete ctx;
+        return nullptr;
+    }
+    return ctx;
+}
+
+void ba_destroy(ba_context* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    for (auto& b : ctx->buf) b.release();
+    for (auto& e : ctx->ev)
+        if (e) hipEventDestroy(e);
+    if (ctx->prof_events)
+        for (int i = 0; i < 2 * Prof::MAXP; ++i) hipEventDestroy(ctx->prof.ev[i]);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* ba_last_error(const ba_context* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int32_t ba_set_options(ba_context* ctx, const ba_options* opts) {
+    if (!ctx || !opts) return BA_E_INVALID;
+    if (opts->device >= 0 && opts->device != ctx->device) {
+        ctx->err = "ba_set_options cannot move a context to another device";
+        return BA_E_INVALID;
+    }
+    const int dev = ctx->device;
+    ctx->opts = *opts;
+    ctx->opts.device = dev;
+    if (ctx->opts.profile_kernels && !ctx->prof_events) {
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < 2 * Prof::MAXP && e == hipSuccess; ++i) e = hipEventCreate(&ctx->prof.ev[i]);
+        if (e != hipSuccess) { ctx->err = "event creation failed"; return BA_E_DEVICE; }
+        ctx->prof_events = true;
+    }
+    ctx->prof.on = ctx->opts.profile_kernels ? 1 : 0;
+    return BA_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Problem preparation: admissibility (countConstraints :184-213, skip :265-268),
+// active parameter blocks, point-major / camera-major orderings, envelope of S.
+static int prepare(ba_context* ctx, const ba_problem* p) {
+    const ba_options& o = ctx->opts;
+    if (!p || p->n_cams < 0 || p->n_points < 0 || p->n_obs < 0) { ctx->err = "invalid problem sizes"; return BA_E_INVALID; }
+    if ((p->n_cams && !p->cams) || (p->n_points && !p->points) || !p->intr || !p->intr_prior ||
+        (p->n_obs && (!p->obs_cam || !p->obs_pt || !p->obs_uv || !p->obs_depth))) {
+        ctx->err = "null problem buffer";
+        return BA_E_INVALID;
+    }
+    const int nc = p->n_cams, np = p->n_points, no = p->n_obs;
+    std::vector<int> cam_cnt(nc, 0), pt_cnt(np, 0);
+    std::vector<char> adm(no, 0);
+    int n_adm = 0;
+    for (int k = 0; k < no; ++k) {
+        const int ci = p->obs_cam[k], pi = p->obs_pt[k];
+        if (ci < 0 || ci >= nc || pi < 0 || pi >= np) { ctx->err = "observation index out of range"; return BA_E_INVALID; }
+        if (!(p->obs_depth[k] > 1e-15)) continue;
+        adm[k] = 1;
+        ++n_adm;
+        ++cam_cnt[ci];
+        ++pt_cnt[pi];
+    }
+    if (n_adm == 0) { ctx->err = "no admissible observation (all depths <= 1e-15)"; return BA_E_INVALID; }
+    // active cameras (Ceres removes unused blocks; the gauge block is constant, :299)
+    std::vector<int> cam_ac(nc, -1);
+    ctx->ac_cam.clear();
+    for (int i = 0; i < nc; ++i)
+        if (cam_cnt[i] > 0 && i != p->fixed_cam) { cam_ac[i] = (int)ctx->ac_cam.size(); ctx->ac_cam.push_back(i); }
+    const int nac = (int)ctx->ac_cam.size();
+    // per point: min active camera (for ordering and the envelope)
+    std::vector<int> pmin(np, INT32_MAX);
+    for (int k = 0; k < no; ++k)
+        if (adm[k]) {
+            const int a = cam_ac[p->obs_cam[k]];
+            if (a >= 0) pmin[p->obs_pt[k]] = std::min(pmin[p->obs_pt[k]], a);
+        }
+    // active points ordered by (min active camera, index) -> banded locality
+    ctx->pt_idx.clear();
+    for (int i = 0; i < np; ++i)
+        if (pt_cnt[i] > 0) ctx->pt_idx.push_back(i);
+    std::stable_sort(ctx->pt_idx.begin(), ctx->pt_idx.end(), [&](int a, int b) { return pmin[a] < pmin[b]; });
+    const int n_ap = (int)ctx->pt_idx.size();
+    std::vector<int> ap_of(np, -1);
+    for (int a = 0; a < n_ap; ++a) ap_of[ctx->pt_idx[a]] = a;
+    // point-major obs
+    std::vector<int> pt_ptr(n_ap + 1, 0);
+    for (int a = 0; a < n_ap; ++a) pt_ptr[a + 1] = pt_ptr[a] + pt_cnt[ctx->pt_idx[a]];
+    std::vector<int> fill(pt_ptr.begin(), pt_ptr.end() - 1);
+    ctx->po_orig.assign(n_adm, 0);
+    for (int k = 0; k < no; ++k)
+        if (adm[k]) ctx->po_orig[fill[ap_of[p->obs_pt[k]]]++] = k;
+    // within a point: by active camera (gauge/unobserved first), then original order
+    for (int a = 0; a < n_ap; ++a)
+        std::stable_sort(ctx->po_orig.begin() + pt_ptr[a], ctx->po_orig.begin() + pt_ptr[a + 1],
+                         [&](int x, int y) { return cam_ac[p->obs_cam[x]] < cam_ac[p->obs_cam[y]]; });
+    std::vector<int> po_cam(n_adm), po_ac(n_adm), po_ap(n_adm);
+    std::vector<double> po_uv(2 * (size_t)n_adm), po_dep(n_adm);
+    for (int a = 0; a < n_ap; ++a)
+        for (int q = pt_ptr[a]; q < pt_ptr[a + 1]; ++q) {
+            const int k = ctx->po_orig[q];
+            po_cam[q] = p->obs_cam[k];
+            po_ac[q] = cam_ac[p->obs_cam[k]];
+            po_ap[q] = a;
+            po_uv[2 * (size_t)q] = p->obs_uv[2 * (size_t)k];
+            po_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
+            po_dep[q] = p->obs_depth[k];
+        }
+    // camera-major obs: one segment per camera with admissible obs (gauge included)
+    std::vector<int> seg_ptr(1, 0), seg_cam, seg_ac;
+    std::vector<int> cstart(nc + 1, 0);
+    for (int i = 0; i < nc; ++i) cstart[i + 1] = cstart[i] + cam_cnt[i];
+    std::vector<int> cfill(cstart.begin(), cstart.end() - 1);
+    std::vector<int> co_pt(n_adm);
+    std::vector<double> co_uv(2 * (size_t)n_adm), co_dep(n_adm);
+    for (int k = 0; k < no; ++k)
+        if (adm[k]) {
+            const int q = cfill[p->obs_cam[k]]++;
+            co_pt[q] = p->obs_pt[k];
+            co_uv[2 * (size_t)q] = p->obs_uv[2 * (size_t)k];
+            co_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
+            co_dep[q] = p->obs_depth[k];
+        }
+    for (int i = 0; i < nc; ++i)
+        if (cam_cnt[i] > 0) {
+            seg_cam.push_back(i);
+            seg_ac.push_back(cam_ac[i]);
+            seg_ptr.push_back(cstart[i + 1]);
+        }
+    // envelope of S: first co-visible active camera of each active camera
+    std::vector<int> fc(nac);
+    for (int a = 0; a < nac; ++a) fc[a] = a;
+    for (int q = 0; q < n_adm; ++q) {
+        const int a = po_ac[q];
+        if (a >= 0) fc[a] = std::min(fc[a], pmin[ctx->pt_idx[po_ap[q]]]);
+    }
+    const int n = 6 * nac + 4;
+    const int npad = (n + 15) / 16 * 16;
+    const int nb = npad / 16;
+    std::vector<int> fcol(nb, INT32_MAX);
+    for (int r = 0; r < npad; ++r) {
+        const int first = (r < 6 * nac) ? 6 * fc[r / 6] : 0;
+        fcol[r / 16] = std::min(fcol[r / 16], first / 16);
+    }
+    std::vector<int> rptr(nb + 1, 0), rows;
+    for (int k = 0; k < nb; ++k) {
+        for (int i = k + 1; i < nb; ++i)
+            if (fcol[i] <= k) rows.push_back(i);
+        rptr[k + 1] = (int)rows.size();
+    }
+    // ---- uploads
+    hipStream_t s = ctx->stream;
+    HIPCHECK(ctx, upload(ctx, B_CAMS0, p->cams, 7 * (size_t)nc));
+    HIPCHECK(ctx, upload(ctx, B_CAMS1, p->cams, 7 * (size_t)nc));
+    HIPCHECK(ctx, upload(ctx, B_PTS0, p->points, 3 * (size_t)np));
+    HIPCHECK(ctx, upload(ctx, B_PTS1, p->points, 3 * (size_t)np));
+    HIPCHECK(ctx, upload(ctx, B_K0, p->intr, 4));
+    HIPCHECK(ctx, upload(ctx, B_K1, p->intr, 4));
+    HIPCHECK(ctx, upload(ctx, B_PRIOR, p->intr_prior, 4));
+    HIPCHECK(ctx, upload(ctx, B_CAMS_INIT, p->cams, 7 * (size_t)nc));
+    HIPCHECK(ctx, upload(ctx, B_PTS_INIT, p->points, 3 * (size_t)np));
+    HIPCHECK(ctx, upload(ctx, B_K_INIT, p->intr, 4));
+    HIPCHECK(ctx, upload(ctx, B_PO_CAM, po_cam.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_PO_AC, po_ac.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_PO_UV, po_uv.data(), 2 * (size_t)n_adm));
+    HIPCHECK(ctx, upload(ctx, B_PO_DEP, po_dep.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_PO_AP, po_ap.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_PT_PTR, pt_ptr.data(), n_ap + 1));
+    HIPCHECK(ctx, upload(ctx, B_PT_IDX, ctx->pt_idx.data(), n_ap));
+    HIPCHECK(ctx, upload(ctx, B_CO_PT, co_pt.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_CO_UV, co_uv.data(), 2 * (size_t)n_adm));
+    HIPCHECK(ctx, upload(ctx, B_CO_DEP, co_dep.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_SEG_PTR, seg_ptr.data(), seg_ptr.size()));
+    HIPCHECK(ctx, upload(ctx, B_SEG_CAM, seg_cam.data(), seg_cam.size()));
+    HIPCHECK(ctx, upload(ctx, B_SEG_AC, seg_ac.data(), seg_ac.size()));
+    HIPCHECK(ctx, upload(ctx, B_AC_CAM, ctx->ac_cam.data(), nac));
+    HIPCHECK(ctx, upload(ctx, B_FCOL, fcol.data(), nb));
+    HIPCHECK(ctx, upload(ctx, B_RPTR, rptr.data(), nb + 1));
+    HIPCHECK(ctx, upload(ctx, B_ROWS, rows.data(), rows.size()));
+    const int n_seg = (int)seg_cam.size();
+    const int nblk_pt = (n_ap + 255) / 256;
+    const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, 1});
+    HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * CAMDATA * std::max(nac, 1)));
+    HIPCHECK(ctx, ctx->buf[B_SEGINTR].ensure(sizeof(double) * SEGINTR * std::max(n_seg, 1)));
+    HIPCHECK(ctx, ctx->buf[B_LIN].ensure(sizeof(double) * LIN_N));
+    HIPCHECK(ctx, ctx->buf[B_SCALE].ensure(sizeof(double) * (6 * nac + 3 * (size_t)n_ap + 4)));
+    HIPCHECK(ctx, ctx->buf[B_CNP].ensure(sizeof(double) * 3 * std::max(n_ap, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PDATA].ensure(sizeof(double) * PDATA * std::max(n_ap, 1)));
+    HIPCHECK(ctx, ctx->buf[B_S].ensure(sizeof(double) * (size_t)npad * npad));
+    HIPCHECK(ctx, ctx->buf[B_RHS].ensure(sizeof(double) * npad));
+    HIPCHECK(ctx, ctx->buf[B_DELTA].ensure(sizeof(double) * npad));
+    HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
+    HIPCHECK(ctx, ctx->buf[B_SCAL].ensure(sizeof(double) * SC_N));
+    HIPCHECK(ctx, ctx->buf[B_FLAG].ensure(sizeof(int) * 4));
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * part_stride, s));
+
+    DevProblem& P = ctx->P;
+    P.cams[0] = ctx->buf[B_CAMS0].as<double>(); P.cams[1] = ctx->buf[B_CAMS1].as<double>();
+    P.pts[0] = ctx->buf[B_PTS0].as<double>(); P.pts[1] = ctx->buf[B_PTS1].as<double>();
+    P.K[0] = ctx->buf[B_K0].as<double>(); P.K[1] = ctx->buf[B_K1].as<double>();
+    P.prior = ctx->buf[B_PRIOR].as<double>();
+    P.po_cam = ctx->buf[B_PO_CAM].as<int>(); P.po_ac = ctx->buf[B_PO_AC].as<int>();
+    P.po_uv = ctx->buf[B_PO_UV].as<double2>(); P.po_depth = ctx->buf[B_PO_DEP].as<double>();
+    P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.pt_ptr = ctx->buf[B_PT_PTR].as<int>();
+    P.pt_idx = ctx->buf[B_PT_IDX].as<int>();
+    P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
+    P.co_depth = ctx->buf[B_CO_DEP].as<double>();
+    P.seg_ptr = ctx->buf[B_SEG_PTR].as<int>(); P.seg_cam = ctx->buf[B_SEG_CAM].as<int>();
+    P.seg_ac = ctx->buf[B_SEG_AC].as<int>(); P.ac_cam = ctx->buf[B_AC_CAM].as<int>();
+    P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
+    P.n = n; P.npad = npad; P.kb = 6 * nac;
+    P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
+    P.part_stride = part_stride;
+    DevWork& W = ctx->W;
+    W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
+    W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
+    W.cnp = ctx->buf[B_CNP].as<double>(); W.pdata = ctx->buf[B_PDATA].as<double>();
+    W.S = ctx->buf[B_S].as<double>(); W.rhs = ctx->buf[B_RHS].as<double>();
+    W.delta = ctx->buf[B_DELTA].as<double>(); W.part = ctx->buf[B_PART].as<double>();
+    W.scal = ctx->buf[B_SCAL].as<double>(); W.chol_flag = ctx->buf[B_FLAG].as<int>();
+    W.fcol = ctx->buf[B_FCOL].as<int>(); W.rptr = ctx->buf[B_RPTR].as<int>(); W.rows = ctx->buf[B_ROWS].as<int>();
+    BaConsts& C = ctx->C;
+    const double N = (double)n_adm;
+    C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
+    C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
+    C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
+    C.a_r = o.hub_p_repr; C.b_r = o.hub_p_repr * o.hub_p_repr;
+    C.a_d = o.hub_p_unpr; C.b_d = o.hub_p_unpr * o.hub_p_unpr;
+    C.min_diag = o.min_lm_diagonal; C.max_diag = o.max_lm_diagonal;
+    ctx->nblk_pt = nblk_pt;
+    ctx->prepared = true;
+    ctx->prep_nc = nc; ctx->prep_np = np; ctx->prep_no = no;
+    // Algorithmic (compulsory) traffic per launch, DESIGN.md §Roofline:
+    // each input byte read once, each output byte written once.
+    {
+        const double A = n_adm, Pn = n_ap, Cn = nac, Sg = n_seg;
+        double env = 0;  // envelope tiles of the reduced system
+        for (int k = 0; k < nb; ++k) env += (double)(rptr[k + 1] - rptr[k]) + 1.0;
+        const double env_bytes = env * 16 * 16 * 8;
+        double* kb = ctx->k_bytes;
+        double* kf = ctx->k_flops;
+        kb[K_CAM_SIDE] = A * 28 + Pn * 24 + (Cn + 1) * 56 + 32 + Cn * CAMDATA * 8 + Sg * SEGINTR * 8;
+        kf[K_CAM_SIDE] = A * 420;
+        kb[K_LIN_FINALIZE] = Sg * SEGINTR * 8 + Cn * (56 + 48) + LIN_N * 8;
+        kb[K_POINT_COLNORM] = A * 28 + Pn * (8 + 24 + 24);
+        kb[K_SCALE] = (6 * Cn + 3 * Pn + 4) * 16;
+        kb[K_MEMSET_S] = (double)npad * npad * 8;
+        kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
+        kb[K_POINT_PREP] = A * 28 + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
+        kf[K_POINT_PREP] = A * 300 + Pn * 200;
+        kb[K_OBS_PAIRS] = A * 36 + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
+        kb[K_CHOL] = 2 * env_bytes + 3 * npad * 8.0;
+        kf[K_CHOL] = 0;
+        for (int k = 0; k < nb; ++k) {
+            const double r = rptr[k + 1] - rptr[k];
+            kf[K_CHOL] += (r * (r + 1) / 2) * 2.0 * 16 * 16 * 16 + r * 16 * 16 * 16 + 16 * 16 * 16 / 3.0;
+        }
+        kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
+        kb[K_BACKSUB_EVAL] = A * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;
+        kf[K_BACKSUB_EVAL] = A * 700;
+        kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
+    }
+    return BA_OK;
+}
+
+static void print_header() {
+    std::printf("iter      cost      cost_change  |gradient|   |step|    tr_ratio  tr_radius  ls_iter  iter_time  total_time\n");
+}
+static void print_row(int it, double cost, double dc, double g, double st, double rho, double rad, double ti, double tt) {
+    std::printf("% 4d % 3.6e % 3.2e % 3.2e % 3.2e % 3.2e % 3.2e % 4d % 3.2e % 3.2e\n", it, cost, dc, g, st, rho, rad, 0,
+                ti * 1e-3, tt * 1e-3);
+    std::fflush(stdout);
+}
+
+extern "C" int32_t ba_prepare(ba_context* ctx, const ba_problem* p) {
+    if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = prepare(ctx, p);
+    if (rc) return rc;
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return BA_OK;
+}
+
+static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, double t0);
+
+extern "C" int32_t ba_solve(ba_context* ctx, ba_problem* p, ba_summary* sum) {
+    if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
+    if (!sum) { ctx->err = "null summary"; return BA_E_INVALID; }
+    const double t0 = now_ms();
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = prepare(ctx, p);
+    if (rc) return rc;
+    return solve_prepared(ctx, p, sum, t0);
+}
+
+extern "C" int32_t ba_solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum) {
+    if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
+    if (!sum || !p) { ctx->err = "null argument"; return BA_E_INVALID; }
+    if (!ctx->prepared || p->n_cams != ctx->prep_nc || p->n_points != ctx->prep_np || p->n_obs != ctx->prep_no) {
+        ctx->err = "ba_solve_prepared: problem does not match the last ba_prepare()";
+        return BA_E_INVALID;
+    }
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    return solve_prepared(ctx, p, sum, now_ms());
+}
+
+static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, double t0) {
+    std::memset(sum, 0, sizeof(*sum));
+    const ba_options& o = ctx->opts;
+    Prof* pf = ctx->pf();
+    DevProblem& P = ctx->P;
+    DevWork& W = ctx->W;
+    const BaConsts& C = ctx->C;
+    hipStream_t s = ctx->stream;
+    // start from the parameters of the last ba_prepare() (device-to-device)
+    HIPCHECK(ctx, hipMemcpyAsync(P.cams[0], ctx->buf[B_CAMS_INIT].p, sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(P.cams[1], ctx->buf[B_CAMS_INIT].p, sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(P.pts[0], ctx->buf[B_PTS_INIT].p, sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(P.pts[1], ctx->buf[B_PTS_INIT].p, sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(P.K[0], ctx->buf[B_K_INIT].p, sizeof(double) * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(P.K[1], ctx->buf[B_K_INIT].p, sizeof(double) * 4, hipMemcpyDeviceToDevice, s));
+    sum->num_obs_admissible = P.n_adm;
+    sum->num_active_cams = P.nac;
+    sum->num_active_points = P.n_ap;
+    sum->reduced_system_size = P.n;
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    const double tl0 = now_ms();
+    sum->time_setup_ms = tl0 - t0;
+
+    int cur = 0;
+    double lin_h[LIN_N], scal_h[SC_N];
+    // IterationZero: evaluate cost, gradient, Jacobian column norms -> Jacobi scale
+    HIPCHECK(ctx, launch_linearize(P, C, cur, W, s, pf));
+    HIPCHECK(ctx, launch_scale(P, C, cur, o.jacobi_scaling, W, s, pf));
+    HIPCHECK(ctx, hipMemcpyAsync(lin_h, W.lin, sizeof(lin_h), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    flush_prof(ctx);
+    double x_cost = lin_h[0];
+    sum->initial_cost = x_cost;
+    if (!std::isfinite(x_cost)) {
+        sum->termination_type = BA_FAILURE;
+        sum->final_cost = x_cost;
+        std::snprintf(sum->message, sizeof(sum->message), "Residual and Jacobian evaluation failed.");
+        sum->time_total_ms = now_ms() - t0;
+        return BA_OK;
+    }
+    double gmax_ci = lin_h[1];
+    double final_cost = x_cost;
+    double radius = o.initial_trust_region_radius;
+    double decrease_factor = 2.0;
+    int iter = 0, n_succ = 1, n_unsucc = 0, n_invalid = 0;
+    bool step_ok = true;
+    double xnorm2 = -1.0;  // ambient |x|^2 of active blocks (computed lazily on host)
+    const bool progress = o.minimizer_progress_to_stdout != 0;
+    double t_lin = 0, t_build = 0, t_fac = 0, t_upd = 0;
+    bool linearized_this_iter = true;  // iteration-0 linearisation precedes the first step
+
+    // host mirror of the active parameters for |x| (parameter tolerance)
+    auto compute_xnorm2 = [&](int which) -> double {
+        std::vector<double> cams(7 * (size_t)p->n_cams), pts(3 * (size_t)p->n_points), K(4);
+        hipMemcpyAsync(cams.data(), P.cams[which], sizeof(double) * cams.size(), hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(pts.data(), P.pts[which], sizeof(double) * pts.size(), hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(K.data(), P.K[which], sizeof(double) * 4, hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        double acc = 0;
+        for (int c : ctx->ac_cam)
+            for (int j = 0; j < 7; ++j) acc += cams[7 * (size_t)c + j] * cams[7 * (size_t)c + j];
+        for (int i : ctx->pt_idx)
+            for (int j = 0; j < 3; ++j) acc += pts[3 * (size_t)i + j] * pts[3 * (size_t)i + j];
+        for (int j = 0; j < 4; ++j) acc += K[j] * K[j];
+        return acc;
+    };
+    xnorm2 = compute_xnorm2(cur);
+    if (progress) { print_header(); print_row(0, x_cost, 0, gmax_ci, 0, 0, radius, 0, now_ms() - tl0); }
+    double gmax_pt = 0.0;
+    for (;;) {
+        if (iter >= o.max_num_iterations) {
+            sum->termination_type = BA_NO_CONVERGENCE;
+            std::snprintf(sum->message, sizeof(sum->message),
+                          "Maximum number of iterations reached. Number of iterations: %d.", iter);
+            break;
+        }
+        if (radius <= o.min_trust_region_radius) {
+            sum->termination_type = BA_CONVERGENCE;
+            std::snprintf(sum->message, sizeof(sum->message), "Minimum trust region radius reached. Trust region radius: %e <= %e", radius, o.min_trust_region_radius);
+            break;
+        }
+        const double ti0 = now_ms();
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[1], s));
+        HIPCHECK(ctx, launch_build(P, C, cur, radius, W, s, pf));
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[2], s));
+        HIPCHECK(ctx, launch_factor(P, W, s, pf));
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[3], s));
+        HIPCHECK(ctx, launch_update(P, C, cur, W, s, pf));
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[4], s));
+        HIPCHECK(ctx, hipMemcpyAsync(scal_h, W.scal, sizeof(scal_h), hipMemcpyDeviceToHost, s));
+        HIPCHECK(ctx, hipStreamSynchronize(s));
+        flush_prof(ctx);
+        float ms;
+        if (linearized_this_iter && iter > 0) { hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]); t_lin += ms; }
+        hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]); t_build += ms;
+        hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]); t_fac += ms;
+        hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]); t_upd += ms;
+        gmax_pt = scal_h[SC_GMAX_PT];
+        const double gmax = std::max(gmax_ci, gmax_pt);
+        // FinalizeIteration (of the previous iteration): gradient tolerance
+        if (step_ok && gmax <= o.gradient_tolerance) {
+            sum->termination_type = BA_CONVERGENCE;
+            std::snprintf(sum->message, sizeof(sum->message), "Gradient tolerance reached. Gradient max norm: %e <= %e", gmax, o.gradient_tolerance);
+            break;
+        }
+        ++iter;
+        linearized_this_iter = false;
+        const double mcc = scal_h[SC_MCC];
+        const bool lsf = scal_h[SC_BAD] >= 2.0;  // point V not PD or Cholesky failure
+        const bool valid = !lsf && std::isfinite(mcc) && mcc > 0.0;
+        if (!valid) {
+            if (++n_invalid >= o.max_num_consecutive_invalid_steps) {
+                sum->termination_type = BA_FAILURE;
+                std::snprintf(sum->message, sizeof(sum->message),
+                              "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d",
+                              o.max_num_consecutive_invalid_steps);
+                ++n_unsucc;
+                break;
+            }
+            radius /= decrease_factor;
+            decrease_factor *= 2.0;
+            step_ok = false;
+            ++n_unsucc;
+            if (progress) print_row(iter, x_cost, 0, gmax, 0, 0, radius, now_ms() - ti0, now_ms() - tl0);
+            continue;
+        }
+        n_invalid = 0;
+        double cand = scal_h[SC_CAND];
+        if (scal_h[SC_BAD] >= 1.0 || !std::isfinite(cand)) cand = DBL_MAX;
+        const double step_norm = std::sqrt(scal_h[SC_SN2]);
+        const double xnorm = std::sqrt(xnorm2);
+        if (step_norm <= o.parameter_tolerance * (xnorm + o.parameter_tolerance)) {
+            sum->termination_type = BA_CONVERGENCE;
+            std::snprintf(sum->message, sizeof(sum->message), "Parameter tolerance reached. Relative step_norm: %e <= %e.",
+                          step_norm / (xnorm + o.parameter_tolerance), o.parameter_tolerance);
+            break;
+        }
+        const double cost_change = x_cost - cand;
+        if (std::fabs(cost_change) <= o.function_tolerance * x_cost) {
+            sum->termination_type = BA_CONVERGENCE;
+            std::snprintf(sum->message, sizeof(sum->message), "Function tolerance reached. |cost_change|/cost: %e <= %e",
+                          std::fabs(cost_change) / x_cost, o.function_tolerance);
+            break;
+        }
+        const double rho = (cand >= DBL_MAX) ? -DBL_MAX : (x_cost - cand) / mcc;
+        if (rho > o.min_relative_decrease) {
+            // HandleSuccessfulStep: x = candidate, re-linearise
+            cur ^= 1;
+            HIPCHECK(ctx, hipEventRecord(ctx->ev[0], s));
+            HIPCHECK(ctx, launch_linearize(P, C, cur, W, s, pf));
+            HIPCHECK(ctx, hipMemcpyAsync(lin_h, W.lin, sizeof(lin_h), hipMemcpyDeviceToHost, s));
+            HIPCHECK(ctx, hipStreamSynchronize(s));
+            flush_prof(ctx);
+            linearized_this_iter = true;
+            const double ncost = lin_h[0];
+            if (!std::isfinite(ncost)) {
+                sum->termination_type = BA_FAILURE;
+                std::snprintf(sum->message, sizeof(sum->message), "Residual and Jacobian evaluation failed.");
+                break;
+            }
+            x_cost = ncost;
+            gmax_ci = lin_h[1];
+            xnorm2 = compute_xnorm2(cur);
+            radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3));
+            radius = std::min(o.max_trust_region_radius, radius);
+            decrease_factor = 2.0;
+            step_ok = true;
+            ++n_succ;
+            final_cost = std::min(final_cost, x_cost);
+            if (progress) print_row(iter, x_cost, cost_change, gmax, step_norm, rho, radius, now_ms() - ti0, now_ms() - tl0);
+        } else {
+            radius /= decrease_factor;
+            decrease_factor *= 2.0;
+            step_ok = false;
+            ++n_unsucc;
+            final_cost = std::min(final_cost, cand);
+            if (progress) print_row(iter, cand, cost_change, gmax, step_norm, rho, radius, now_ms() - ti0, now_ms() - tl0);
+        }
+    }
+    sum->final_cost = final_cost;
+    sum->num_successful_steps = n_succ;
+    sum->num_unsuccessful_steps = n_unsucc;
+    sum->num_iterations = iter;
+    // copy the best (= last accepted) parameters back in place
+    HIPCHECK(ctx, hipMemcpyAsync(p->cams, P.cams[cur], sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(p->points, P.pts[cur], sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(p->intr, P.K[cur], sizeof(double) * 4, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    const double t1 = now_ms();
+    sum->time_lm_ms = t1 - tl0;
+    sum->time_total_ms = t1 - t0;
+    sum->time_linearize_ms = t_lin;
+    sum->time_schur_ms = t_build;
+    sum->time_factor_ms = t_fac;
+    sum->time_update_ms = t_upd;
+    return BA_OK;
+}
+
+extern "C" int32_t ba_debug_linearize(ba_context* ctx, const ba_problem* p, double* cost, double* res, double* jcam,
+                                      double* jpt, double* jint) {
+    if (!ctx) return BA_E_INVALID;
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = prepare(ctx, p);
+    if (rc) return rc;
+    DevProblem& P = ctx->P;
+    hipStream_t s = ctx->stream;
+    const size_t na = P.n_adm;
+    HIPCHECK(ctx, ctx->buf[B_DBG0].ensure(sizeof(double) * 3 * na));
+    HIPCHECK(ctx, ctx->buf[B_DBG1].ensure(sizeof(double) * 18 * na));
+    HIPCHECK(ctx, ctx->buf[B_DBG2].ensure(sizeof(double) * 9 * na));
+    HIPCHECK(ctx, ctx->buf[B_DBG3].ensure(sizeof(double) * 8 * na));
+    HIPCHECK(ctx, launch_linearize(P, ctx->C, 0, ctx->W, s, nullptr));
+    HIPCHECK(ctx, launch_debug_lin(P, ctx->C, 0, ctx->buf[B_DBG0].as<double>(), ctx->buf[B_DBG1].as<double>(),
+                                   ctx->buf[B_DBG2].as<double>(), ctx->buf[B_DBG3].as<double>(), s));
+    std::vector<double> r(3 * na), jc(18 * na), jp(9 * na), jk(8 * na);
+    double lin_h[LIN_N];
+    HIPCHECK(ctx, hipMemcpyAsync(r.data(), ctx->buf[B_DBG0].p, sizeof(double) * r.size(), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(jc.data(), ctx->buf[B_DBG1].p, sizeof(double) * jc.size(), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(jp.data(), ctx->buf[B_DBG2].p, sizeof(double) * jp.size(), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(jk.data(), ctx->buf[B_DBG3].p, sizeof(double) * jk.size(), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(lin_h, ctx->W.lin, sizeof(lin_h), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    if (cost) *cost = lin_h[0];
+    const size_t no = p->n_obs;
+    if (res) std::memset(res, 0, sizeof(double) * 3 * no);
+    if (jcam) std::memset(jcam, 0, sizeof(double) * 18 * no);
+    if (jpt) std::memset(jpt, 0, sizeof(double) * 9 * no);
+    if (jint) std::memset(jint, 0, sizeof(double) * 8 * no);
+    for (size_t q = 0; q < na; ++q) {
+        const size_t k = ctx->po_orig[q];
+        if (res) std::memcpy(res + 3 * k, &r[3 * q], sizeof(double) * 3);
+        if (jcam) std::memcpy(jcam + 18 * k, &jc[18 * q], sizeof(double) * 18);
+        if (jpt) std::memcpy(jpt + 9 * k, &jp[9 * q], sizeof(double) * 9);
+        if (jint) std::memcpy(jint + 8 * k, &jk[8 * q], sizeof(double) * 8);
+    }
+    return BA_OK;
+}
+
+extern "C" int32_t ba_debug_reduced_system(ba_context* ctx, const ba_problem* p, double radius, int32_t* n_out,
+                                           double* S, double* rhs) {
+    if (!ctx) return BA_E_INVALID;
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = prepare(ctx, p);
+    if (rc) return rc;
+    DevProblem& P = ctx->P;
+    hipStream_t s = ctx->stream;
+    if (n_out) *n_out = P.n;
+    if (!S || !rhs) return BA_OK;
+    if (radius <= 0) radius = ctx->opts.initial_trust_region_radius;
+    HIPCHECK(ctx, launch_linearize(P, ctx->C, 0, ctx->W, s, nullptr));
+    HIPCHECK(ctx, launch_scale(P, ctx->C, 0, ctx->opts.jacobi_scaling, ctx->W, s, nullptr));
+    HIPCHECK(ctx, launch_build(P, ctx->C, 0, radius, ctx->W, s, nullptr));
+    std::vector<double> Sp((size_t)P.npad * P.npad);
+    HIPCHECK(ctx, hipMemcpyAsync(Sp.data(), ctx->W.S, sizeof(double) * Sp.size(), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(rhs, ctx->W.rhs, sizeof(double) * P.n, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    const int n = P.n;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            const double v = Sp[(size_t)i * P.npad + j];
+            S[(size_t)i * n + j] = v;
+            S[(size_t)j * n + i] = v;
+        }
+    return BA_OK;
+}
+
+extern "C" int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, int32_t max_n) {
+    if (!ctx || !out) return 0;
+    int n = 0;
+    for (int k = 0; k < K_COUNT && n < max_n; ++k, ++n) {
+        std::memset(&out[n], 0, sizeof(ba_kernel_stat));
+        std::snprintf(out[n].name, sizeof(out[n].name), "%s", kKernelNames[k]);
+        out[n].launches = ctx->k_launches[k];
+        out[n].total_ms = ctx->k_ms[k];
+        out[n].bytes_per_launch = ctx->k_bytes[k];
+        out[n].flops_per_launch = ctx->k_flops[k];
+    }
+    return n;
+}
+
+extern "C" void ba_reset_kernel_stats(ba_context* ctx) {
+    if (!ctx) return;
+    for (int k = 0; k < K_COUNT; ++k) { ctx->k_launches[k] = 0; ctx->k_ms[k] = 0; }
+}

@@ -1,0 +1,66 @@
+"""Loader for libmiba.so (the HIP product library). No fallback: if the
+library is missing or no GPU is present, calls raise instead of silently
+running something else."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from .capi import BaKernelStat, BaOptions, BaProblem, BaSummary
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmiba.so")
+
+# exported symbols, exactly those declared in include/ba.h
+EXPORTS = (
+    "ba_api_version", "ba_build_info", "ba_default_options", "ba_create", "ba_destroy", "ba_last_error", "ba_set_options",
+    "ba_solve", "ba_prepare", "ba_solve_prepared", "ba_kernel_stats", "ba_reset_kernel_stats",
+    "ba_debug_linearize", "ba_debug_reduced_system",
+)
+
+_lib = None
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libmiba for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    jobs = os.environ.get("MAX_JOBS", "4")
+    out = subprocess.run(["make", "-C", PKG_DIR, f"-j{min(int(jobs), 16)}"], capture_output=not verbose, text=True)
+    if out.returncode != 0:
+        raise RuntimeError(f"libmiba build failed:\n{out.stdout}\n{out.stderr}")
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libmiba.so not found at {LIB_PATH}; run __graft_entry__.build() or `make -C {PKG_DIR}`")
+    L = C.CDLL(LIB_PATH)
+    dp = C.POINTER(C.c_double)
+    L.ba_api_version.restype = C.c_int32
+    L.ba_build_info.restype = C.c_char_p
+    L.ba_default_options.argtypes = [C.POINTER(BaOptions)]
+    L.ba_create.argtypes = [C.POINTER(BaOptions)]
+    L.ba_create.restype = C.c_void_p
+    L.ba_destroy.argtypes = [C.c_void_p]
+    L.ba_last_error.argtypes = [C.c_void_p]
+    L.ba_last_error.restype = C.c_char_p
+    L.ba_set_options.argtypes = [C.c_void_p, C.POINTER(BaOptions)]
+    L.ba_set_options.restype = C.c_int32
+    L.ba_solve.argtypes = [C.c_void_p, C.POINTER(BaProblem), C.POINTER(BaSummary)]
+    L.ba_solve.restype = C.c_int32
+    L.ba_prepare.argtypes = [C.c_void_p, C.POINTER(BaProblem)]
+    L.ba_prepare.restype = C.c_int32
+    L.ba_solve_prepared.argtypes = [C.c_void_p, C.POINTER(BaProblem), C.POINTER(BaSummary)]
+    L.ba_solve_prepared.restype = C.c_int32
+    L.ba_kernel_stats.argtypes = [C.c_void_p, C.POINTER(BaKernelStat), C.c_int32]
+    L.ba_kernel_stats.restype = C.c_int32
+    L.ba_reset_kernel_stats.argtypes = [C.c_void_p]
+    L.ba_debug_linearize.argtypes = [C.c_void_p, C.POINTER(BaProblem), dp, dp, dp, dp, dp]
+    L.ba_debug_linearize.restype = C.c_int32
+    L.ba_debug_reduced_system.argtypes = [C.c_void_p, C.POINTER(BaProblem), C.c_double, C.POINTER(C.c_int32), dp, dp]
+    L.ba_debug_reduced_system.restype = C.c_int32
+    _lib = L
+    return L

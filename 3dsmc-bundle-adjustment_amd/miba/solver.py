@@ -1,0 +1,121 @@
+"""Python front-end of the libmiba C-ABI (include/ba.h).
+
+``Solver`` owns one ``ba_context`` (device buffers cached across calls, like
+the reference re-optimising the same window repeatedly, main.cpp:163-168).
+``Solver.solve`` is the replacement of ``ceres::Solve`` inside
+``windowOptimize`` (OptimizationUtils.cpp:300): it updates the problem's
+poses, points and intrinsics in place and returns the summary.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .capi import BaKernelStat, BaOptions, BaSummary, ProblemArrays
+
+
+def default_options(**overrides) -> BaOptions:
+    o = BaOptions()
+    _lib.lib().ba_default_options(C.byref(o))
+    for k, v in overrides.items():
+        setattr(o, k, v)
+    return o
+
+
+class MibaError(RuntimeError):
+    pass
+
+
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Solver:
+    def __init__(self, options: BaOptions | None = None, **overrides):
+        self._L = _lib.lib()
+        self.options = options if options is not None else default_options()
+        for k, v in overrides.items():
+            setattr(self.options, k, v)
+        h = self._L.ba_create(C.byref(self.options))
+        if not h:
+            raise MibaError("ba_create failed: " + (self._L.ba_last_error(None) or b"").decode())
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = (self._L.ba_last_error(self._h) or b"").decode()
+            raise MibaError(f"{what} failed ({rc}): {msg}")
+
+    def solve(self, prob: ProblemArrays) -> dict:
+        s = BaSummary()
+        ps = prob.struct()
+        self._check(self._L.ba_solve(self._h, C.byref(ps), C.byref(s)), "ba_solve")
+        return s.as_dict()
+
+    def set_options(self, **changes) -> None:
+        for k, v in changes.items():
+            setattr(self.options, k, v)
+        self._check(self._L.ba_set_options(self._h, C.byref(self.options)), "ba_set_options")
+
+    def prepare(self, prob: ProblemArrays) -> None:
+        """Upload the window and build its device structure (ba_prepare)."""
+        self._prepared = prob.struct()
+        self._check(self._L.ba_prepare(self._h, C.byref(self._prepared)), "ba_prepare")
+
+    def solve_prepared(self, prob: ProblemArrays) -> dict:
+        """LM on the resident window from the parameters of the last prepare()."""
+        s = BaSummary()
+        ps = prob.struct()
+        self._check(self._L.ba_solve_prepared(self._h, C.byref(ps), C.byref(s)), "ba_solve_prepared")
+        return s.as_dict()
+
+    def kernel_stats(self) -> list:
+        arr = (BaKernelStat * 32)()
+        n = self._L.ba_kernel_stats(self._h, arr, 32)
+        out = []
+        for i in range(n):
+            k = arr[i]
+            out.append(dict(name=k.name.decode(), launches=k.launches, total_ms=k.total_ms,
+                            bytes_per_launch=k.bytes_per_launch, flops_per_launch=k.flops_per_launch))
+        return out
+
+    def reset_kernel_stats(self) -> None:
+        self._L.ba_reset_kernel_stats(self._h)
+
+    def linearize(self, prob: ProblemArrays) -> dict:
+        n = prob.n_obs
+        res = np.zeros((n, 3)); jc = np.zeros((n, 3, 6)); jp = np.zeros((n, 3, 3)); jk = np.zeros((n, 2, 4))
+        cost = np.zeros(1)
+        ps = prob.struct()
+        self._check(self._L.ba_debug_linearize(self._h, C.byref(ps), _dptr(cost), _dptr(res), _dptr(jc), _dptr(jp),
+                                               _dptr(jk)), "ba_debug_linearize")
+        return dict(cost=float(cost[0]), res=res, jcam=jc, jpt=jp, jint=jk)
+
+    def reduced_system(self, prob: ProblemArrays, radius: float = 0.0):
+        ps = prob.struct()
+        n = C.c_int32(0)
+        self._check(self._L.ba_debug_reduced_system(self._h, C.byref(ps), radius, C.byref(n), None, None),
+                    "ba_debug_reduced_system")
+        S = np.zeros((n.value, n.value)); rhs = np.zeros(n.value)
+        self._check(self._L.ba_debug_reduced_system(self._h, C.byref(ps), radius, C.byref(n), _dptr(S), _dptr(rhs)),
+                    "ba_debug_reduced_system")
+        return S, rhs

@@ -1,0 +1,196 @@
+/*
+ * ba.h — C-ABI of libmiba, the MI355X-native windowed bundle-adjustment solver.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *
+ *   bool windowOptimize(ceresGlobalProblem&, int kf_i, int kf_f,
+ *                       vector<KeyFrame>&, Map3D&,
+ *                       const Vector4d& intrinsics_initial,
+ *                       Vector4d& intrinsics_optimized);
+ *     declared  /root/reference/headers/OptimizationUtils.h:55
+ *     defined   /root/reference/src/OptimizationUtils.cpp:215-313
+ *
+ * whose entire compute is `ceres::Solve(globalProblem.options, &problem, &summary)`
+ * (src/OptimizationUtils.cpp:300) over the residual blocks built at :236-294.
+ * The caller (a host adapter, see INTEGRATION.md and include/ba_window.hpp)
+ * flattens the window into the SoA `ba_problem` below, calls ba_solve(), and
+ * maps the results back (reference :303-310).
+ *
+ * Conventions
+ *  - Plain C types only; every pointer is a caller-owned HOST buffer.
+ *  - Poses use Sophus::SE3d storage order [qx,qy,qz,qw,tx,ty,tz]
+ *    (reference headers/sophus/se3.hpp:469-479), T_w_c (camera -> window frame).
+ *  - Updated in place: cams, points, intr (reference mutates T_w_c, map points
+ *    and intrinsics_optimized in place, OptimizationUtils.cpp:248,274,236).
+ *  - Return value: 0 = ok, <0 = error (see BA_E_*); ba_last_error() has text.
+ *    The reference has no error convention (always returns true, :312); a
+ *    Ceres-level failure (e.g. initial evaluation non-finite) is reported in
+ *    ba_summary.termination_type exactly as Ceres would, with return 0.
+ *  - One context per host thread; contexts cache device buffers across calls
+ *    (the reference re-optimizes the same window repeatedly, main.cpp:163-168).
+ */
+#ifndef MIBA_BA_H
+#define MIBA_BA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BA_API_VERSION 1
+
+/* error codes */
+#define BA_OK 0
+#define BA_E_INVALID (-1)   /* bad argument / malformed problem */
+#define BA_E_DEVICE (-2)    /* HIP runtime error / no device */
+#define BA_E_NOMEM (-3)     /* allocation failed */
+#define BA_E_COMM (-4)      /* RCCL / multi-device error */
+#define BA_E_INTERNAL (-5)
+
+/* Ceres 2.0 ceres::TerminationType values (types.h), mirrored numerically. */
+#define BA_CONVERGENCE 0
+#define BA_NO_CONVERGENCE 1
+#define BA_FAILURE 2
+
+/* Solver configuration.
+ * Field-for-field mirror of ceresGlobalProblem
+ * (/root/reference/headers/BundleAdjustmentConfig.h:44-69) plus the Ceres 2.0
+ * Solver::Options defaults that the reference leaves untouched. */
+typedef struct ba_options {
+    /* ceresGlobalProblem constants, BundleAdjustmentConfig.h:47-50 */
+    double hub_p_repr;         /* HUB_P_REPR = 1e-3: Huber a for reprojection blocks */
+    double hub_p_unpr;         /* HUB_P_UNPR = 1e-3: Huber a for depth-prior blocks  */
+    double weight_intrinsics;  /* WEIGHT_INTRINSICS = 1e-6 (IntrinsicsPrior weight)   */
+    double weight_unpr;        /* WEIGHT_UNPR = 10 (depth prior weight numerator)     */
+    /* Solver::Options set in initialize_options(), BundleAdjustmentConfig.h:61-67 */
+    int32_t max_num_iterations;           /* 75 */
+    int32_t minimizer_progress_to_stdout; /* 1 -> Ceres-style iteration table */
+    double eta;                           /* 1e-6 (no effect on a direct Schur solve) */
+    /* Ceres 2.0 defaults (not set by the reference) */
+    double initial_trust_region_radius; /* 1e4  */
+    double max_trust_region_radius;     /* 1e16 */
+    double min_trust_region_radius;     /* 1e-32 */
+    double min_relative_decrease;       /* 1e-3 */
+    double min_lm_diagonal;             /* 1e-6 */
+    double max_lm_diagonal;             /* 1e32 */
+    int32_t max_num_consecutive_invalid_steps; /* 5 */
+    int32_t jacobi_scaling;             /* 1 */
+    double function_tolerance;          /* 1e-6 */
+    double gradient_tolerance;          /* 1e-10 */
+    double parameter_tolerance;         /* 1e-8 */
+    /* MI355X execution knobs (no reference counterpart) */
+    int32_t device;          /* HIP device ordinal for this context; -1 = current */
+    int32_t deterministic;   /* 1 = fixed-order reductions only (no float atomics) */
+    int32_t profile_kernels; /* 1 = HIP-event timing of every kernel launch (ba_kernel_stats) */
+    int32_t reserved[5];
+} ba_options;
+
+/* One window, flattened. Mirrors what windowOptimize feeds to Ceres
+ * (OptimizationUtils.cpp:236-294). Observations with depth <= 1e-15 are
+ * skipped and excluded from the 1/N weight normaliser exactly like the
+ * reference (countConstraints :184-213 and the skip at :265-268). */
+typedef struct ba_problem {
+    int32_t n_cams;
+    int32_t n_points;
+    int32_t n_obs;
+    int32_t fixed_cam;        /* gauge: SetParameterBlockConstant(kf_i) (:299); -1 = none */
+    double* cams;             /* [n_cams*7]  qx,qy,qz,qw,tx,ty,tz   (in/out) */
+    double* points;           /* [n_points*3] (in/out) */
+    double* intr;             /* [4] fx,fy,cx,cy (intrinsics_optimized, in/out) */
+    const double* intr_prior; /* [4] intrinsics_initial (IntrinsicsPrior target, :238) */
+    const int32_t* obs_cam;   /* [n_obs] camera index of each observation */
+    const int32_t* obs_pt;    /* [n_obs] point index of each observation  */
+    const double* obs_uv;     /* [n_obs*2] keypoint pixel (u,v)  (:262) */
+    const double* obs_depth;  /* [n_obs] measured depth z (:261) */
+} ba_problem;
+
+/* Result summary (subset of ceres::Solver::Summary + per-phase device timings). */
+typedef struct ba_summary {
+    double initial_cost;
+    double final_cost;
+    int32_t num_successful_steps;   /* Ceres convention: includes iteration 0 */
+    int32_t num_unsuccessful_steps;
+    int32_t num_iterations;         /* LM steps computed = iterations after 0 */
+    int32_t termination_type;       /* BA_CONVERGENCE / BA_NO_CONVERGENCE / BA_FAILURE */
+    int32_t num_obs_admissible;     /* N of countConstraints */
+    int32_t num_active_cams;
+    int32_t num_active_points;
+    int32_t reduced_system_size;    /* 6*active_cams + 4 */
+    double time_setup_ms;           /* host prep + H2D + structure build */
+    double time_lm_ms;              /* LM loop wall time (device work + host control) */
+    double time_linearize_ms;       /* device: camera-side / point-side linearisation */
+    double time_schur_ms;           /* device: Schur reduction over points */
+    double time_factor_ms;          /* device: reduced camera system factor + solve */
+    double time_update_ms;          /* device: back-substitution + candidate evaluation */
+    double time_total_ms;
+    char message[160];
+} ba_summary;
+
+/* Library / API identification. */
+int32_t ba_api_version(void);
+const char* ba_build_info(void);
+
+/* Defaults = ceresGlobalProblem() + Ceres 2.0 defaults. */
+void ba_default_options(ba_options* opts);
+
+/* Context lifecycle. Returns NULL on failure (ba_last_error(NULL) explains). */
+typedef struct ba_context ba_context;
+ba_context* ba_create(const ba_options* opts);
+void ba_destroy(ba_context* ctx);
+const char* ba_last_error(const ba_context* ctx);
+/* Replace the solver options of a live context (device buffers are kept;
+ * opts->device must equal the context's device or be -1). */
+int32_t ba_set_options(ba_context* ctx, const ba_options* opts);
+
+/* Solve one window in place (the replacement of ceres::Solve at :300).
+ * Equivalent to ba_prepare() followed by ba_solve_prepared(). */
+int32_t ba_solve(ba_context* ctx, ba_problem* prob, ba_summary* summary);
+
+/* Split form of ba_solve for callers that re-solve a resident window:
+ * ba_prepare() validates the window, builds the point-/camera-major orderings
+ * and the reduced-system envelope on the host and uploads everything to HBM;
+ * ba_solve_prepared() runs the LM loop on the resident window starting from the
+ * parameters uploaded by the last ba_prepare() and writes the result into prob
+ * (which must be the same window, same sizes). */
+int32_t ba_prepare(ba_context* ctx, const ba_problem* prob);
+int32_t ba_solve_prepared(ba_context* ctx, ba_problem* prob, ba_summary* summary);
+
+/* Per-kernel device timing (requires ba_options.profile_kernels = 1).
+ * bytes_per_launch is the ALGORITHMIC traffic model of DESIGN.md §Roofline
+ * for the last prepared window (compulsory bytes, each input/output once). */
+typedef struct ba_kernel_stat {
+    char name[32];
+    int32_t launches;
+    int32_t reserved;
+    double total_ms;
+    double bytes_per_launch;
+    double flops_per_launch;
+} ba_kernel_stat;
+int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, int32_t max_n); /* returns count */
+void ba_reset_kernel_stats(ba_context* ctx);
+
+/* ---- verification hooks (used by the parity tests; not on the hot path) ----
+ * Evaluate per-observation robustified residuals and local Jacobians on the
+ * device at the given parameters. Output layout per admissible observation k
+ * in the ORIGINAL observation order (inadmissible rows are zero):
+ *   res[k*3+{0,1,2}]   : sqrt(rho') * (reproj u, reproj v, depth) residual
+ *   jcam[k*18 + r*6+d] : d res_r / d delta_d, delta = [upsilon(3), omega(3)]
+ *   jpt [k*9  + r*3+i] : d res_r / d X_i
+ *   jint[k*8  + r*4+i] : d res_r / d (fx,fy,cx,cy)_i  (rows 0,1; depth row is 0)
+ * cost receives 0.5 * sum_blocks rho(|f_b|^2) including the intrinsics prior.
+ * Any output pointer may be NULL. */
+int32_t ba_debug_linearize(ba_context* ctx, const ba_problem* prob, double* cost,
+                           double* res, double* jcam, double* jpt, double* jint);
+
+/* Build the damped, Jacobi-scaled reduced camera system exactly as the first
+ * LM iteration would (radius = initial_trust_region_radius unless radius > 0):
+ * S [n*n] row-major dense (full symmetric), rhs [n], scale [6*n_cams + 3*n_points + 4]
+ * where n = 6*active_cams + 4; active cameras in increasing index order. */
+int32_t ba_debug_reduced_system(ba_context* ctx, const ba_problem* prob, double radius,
+                                int32_t* n_out, double* S, double* rhs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIBA_BA_H */
