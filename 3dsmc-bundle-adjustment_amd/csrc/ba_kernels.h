@@ -10,8 +10,12 @@ namespace miba {
 static constexpr int CAMDATA = 51;
 // per camera-segment intrinsics partial: Ukk packed (10) | gk (4) | cost (1)
 static constexpr int SEGINTR = 15;
-// per active point Schur record: V~^-1 packed (6) | e~ (3) | K~ 4x3 (12)
+// per active point Schur record: G = chol(V~)^-1 packed lower (6) | e~ (3) | K~ 4x3 (12)
 static constexpr int PDATA = 21;
+// tiled Schur reduction geometry
+static constexpr int TILE_WIN = 12;    // cameras per tile window
+static constexpr int CHUNK_PTS = 64;   // points per chunk (one 64-bit mask word)
+static constexpr int CHUNK_OBS = 256;  // observations per chunk (one per thread)
 
 // partial-sum slots (each slot holds part_stride doubles, one per producing block)
 enum {
@@ -53,12 +57,21 @@ struct DevProblem {
     const int* seg_cam;  // [n_seg]
     const int* seg_ac;   // [n_seg]
     const int* ac_cam;   // active camera -> camera index
+    // tiled Schur reduction: tile t = chunks [tile_chunk[t], tile_chunk[t+1]),
+    // chunk c = active points [chunk_ap[c], chunk_ap[c+1]); camera window [tile_base, +tile_span)
+    const int* tile_chunk;
+    const int* tile_base;
+    const int* tile_span;
+    const int* chunk_ap;
+    const int* ovf_obs;  // point-major obs of overflow points (active camera only)
+    int n_tiles, n_ovf_obs;
     int n_seg, n_ap, n_adm, nac;
     int n;     // reduced system size 6*nac + 4
     int npad;  // n rounded up to 16
     int kb;    // first intrinsics row = 6*nac
     int off_pt, off_k;  // scale-vector offsets
     int part_stride;
+    int band_w;  // 16x16 tiles below the diagonal in the camera band; <=0 or >6: dense envelope kernel
 };
 
 struct DevWork {
@@ -81,12 +94,12 @@ struct DevWork {
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
 enum KernelId {
-    K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_OBS_PAIRS,
-    K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_COUNT
+    K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
+    K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
-    "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "obs_pairs",
-    "chol", "update_cams", "backsub_eval", "final"};
+    "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
+    "obs_pairs", "chol", "update_cams", "backsub_eval", "final"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {

@@ -22,6 +22,9 @@
 // stored Jacobian blocks; DESIGN.md "Roofline").
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "ba_device.h"
 #include "ba_kernels.h"
 
@@ -167,6 +170,40 @@ __global__ __launch_bounds__(TPB) void k_lin_finalize(DevProblem P, BaConsts c, 
 }
 
 // ---------------------------------------------------------------- point side
+// G = L^-1 of the damped point block, packed lower (g00 g10 g11 g20 g21 g22).
+__device__ __forceinline__ void zk_ze(const double G[6], const double Ks[12], const double es[3], double Zk[12],
+                                      double ze[3]) {
+    // Zk[m][k] = sum_{i<=k} K[m][i] G[k][i] ; ze[k] = sum_{i<=k} G[k][i] e[i]
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        Zk[m * 3 + 0] = Ks[m * 3 + 0] * G[0];
+        Zk[m * 3 + 1] = Ks[m * 3 + 0] * G[1] + Ks[m * 3 + 1] * G[2];
+        Zk[m * 3 + 2] = Ks[m * 3 + 0] * G[3] + Ks[m * 3 + 1] * G[4] + Ks[m * 3 + 2] * G[5];
+    }
+    ze[0] = G[0] * es[0];
+    ze[1] = G[1] * es[0] + G[2] * es[1];
+    ze[2] = G[3] * es[0] + G[4] * es[1] + G[5] * es[2];
+}
+// V~^-1 = G^T G (full 3x3)
+__device__ __forceinline__ void vinv_from_g(const double* G, double Vf[9]) {
+    const double g00 = G[0], g10 = G[1], g11 = G[2], g20 = G[3], g21 = G[4], g22 = G[5];
+    Vf[0] = g00 * g00 + g10 * g10 + g20 * g20;
+    Vf[1] = g10 * g11 + g20 * g21;
+    Vf[2] = g20 * g22;
+    Vf[4] = g11 * g11 + g21 * g21;
+    Vf[5] = g21 * g22;
+    Vf[8] = g22 * g22;
+    Vf[3] = Vf[1]; Vf[6] = Vf[2]; Vf[7] = Vf[5];
+}
+// W~ (6x3) = s_c (Jc^T Jp) s_p  for one observation
+__device__ __forceinline__ void w_tilde(const double jc[18], const double jp[9], const double* sc, const double* sp,
+                                        double W[18]) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            W[d * 3 + i] = sc[d] * (jc[d] * jp[i] + jc[6 + d] * jp[3 + i] + jc[12 + d] * jp[6 + i]) * sp[i];
+}
 // mode 0: column norms only (iteration 0, before the Jacobi scale exists)
 // mode 1: full Schur preparation.
 // pdata[ap*PDATA]: Vinv packed (6: 00 01 02 11 12 22), e (3), Kt (12, [m][i])
@@ -225,8 +262,8 @@ __global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, in
             v00 += fmin(fmax(v00, c.min_diag), c.max_diag) / radius;
             v11 += fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
             v22 += fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
-            // 3x3 SPD inverse via Cholesky
-            double Vi[6] = {0, 0, 0, 0, 0, 0};
+            // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
+            double G[6] = {0, 0, 0, 0, 0, 0};  // g00 g10 g11 g20 g21 g22
             const bool pd = v00 > 0.0;
             const double L00 = sqrt(v00);
             const double L10 = v01 / L00, L20 = v02 / L00;
@@ -237,16 +274,12 @@ __global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, in
             const double L22 = sqrt(l22);
             if (pd && l11 > 0.0 && l22 > 0.0 && isfinite(l22)) {
                 const double i00 = 1 / L00, i11 = 1 / L11, i22 = 1 / L22;
-                const double i10 = -L10 * i00 * i11;
-                const double i21 = -L21 * i11 * i22;
-                const double i20 = -(L20 * i00 + L21 * i10) * i22;
-                // Vi = Li^T Li
-                Vi[0] = i00 * i00 + i10 * i10 + i20 * i20;
-                Vi[1] = i10 * i11 + i20 * i21;
-                Vi[2] = i20 * i22;
-                Vi[3] = i11 * i11 + i21 * i21;
-                Vi[4] = i21 * i22;
-                Vi[5] = i22 * i22;
+                G[0] = i00;
+                G[1] = -L10 * i00 * i11;
+                G[2] = i11;
+                G[4] = -L21 * i11 * i22;
+                G[3] = -(L20 * i00 + L21 * G[1]) * i22;
+                G[5] = i22;
             } else {
                 bad = 1.0;
             }
@@ -260,27 +293,22 @@ __global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, in
             }
             double* pd_out = pdata + (size_t)ap * PDATA;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) pd_out[i] = Vi[i];
+            for (int i = 0; i < 6; ++i) pd_out[i] = G[i];
 #pragma unroll
             for (int i = 0; i < 3; ++i) pd_out[6 + i] = es[i];
 #pragma unroll
             for (int i = 0; i < 12; ++i) pd_out[9 + i] = Ks[i];
-            // intrinsics Schur terms: -Ks Vi Ks^T (10 packed) and -Ks Vi es (4)
-            const double Vf[9] = {Vi[0], Vi[1], Vi[2], Vi[1], Vi[3], Vi[4], Vi[2], Vi[4], Vi[5]};
-            double YK[12];
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    YK[m * 3 + j] = Ks[m * 3 + 0] * Vf[0 * 3 + j] + Ks[m * 3 + 1] * Vf[1 * 3 + j] + Ks[m * 3 + 2] * Vf[2 * 3 + j];
+            // intrinsics Schur terms with Zk = K~ G^T, ze = G e~ :  -Zk Zk^T (10 packed), -Zk ze (4)
+            double Zk[12], ze[3];
+            zk_ze(G, Ks, es, Zk, ze);
             int q = 0;
 #pragma unroll
             for (int m = 0; m < 4; ++m)
 #pragma unroll
                 for (int l = m; l < 4; ++l, ++q)
-                    kk[q] = -(YK[m * 3 + 0] * Ks[l * 3 + 0] + YK[m * 3 + 1] * Ks[l * 3 + 1] + YK[m * 3 + 2] * Ks[l * 3 + 2]);
+                    kk[q] = -(Zk[m * 3 + 0] * Zk[l * 3 + 0] + Zk[m * 3 + 1] * Zk[l * 3 + 1] + Zk[m * 3 + 2] * Zk[l * 3 + 2]);
 #pragma unroll
-            for (int m = 0; m < 4; ++m) kk[10 + m] = -(YK[m * 3 + 0] * es[0] + YK[m * 3 + 1] * es[1] + YK[m * 3 + 2] * es[2]);
+            for (int m = 0; m < 4; ++m) kk[10 + m] = -(Zk[m * 3 + 0] * ze[0] + Zk[m * 3 + 1] * ze[1] + Zk[m * 3 + 2] * ze[2]);
         }
     }
     if (mode == 0) return;
@@ -359,19 +387,22 @@ __global__ void k_assemble(DevProblem P, BaConsts c, double radius, const double
     }
 }
 
-// Schur scatter: thread per admissible observation (point-major) whose camera is active.
+// Schur scatter for the OVERFLOW points (span > TILE_WIN cameras or repeated
+// cameras): thread per listed observation, global f64 atomics.
 __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
                                                    const double* __restrict__ pdata, double* __restrict__ S,
                                                    double* __restrict__ rhs) {
-    const int a = blockIdx.x * TPB + threadIdx.x;
-    if (a >= P.n_adm) return;
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    if (t >= P.n_ovf_obs) return;
+    const int a = P.ovf_obs[t];
     const int ca = P.po_ac[a];
     if (ca < 0) return;
     const int ap = P.po_ap[a];
     const size_t ld = P.npad;
     const int kb = P.kb;
     const double* pd = pdata + (size_t)ap * PDATA;
-    const double Vf[9] = {pd[0], pd[1], pd[2], pd[1], pd[3], pd[4], pd[2], pd[4], pd[5]};
+    double Vf[9];
+    vinv_from_g(pd, Vf);
     const double* sp = scale + P.off_pt + 3 * ap;
     const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
     const double* K = P.K[cur];
@@ -438,6 +469,152 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, int
                         m += Y[e2 * 3 + 0] * W[d * 3 + 0] + Y[e2 * 3 + 1] * W[d * 3 + 1] + Y[e2 * 3 + 2] * W[d * 3 + 2];
                     atomicAdd(&S[(size_t)(6 * ca + e2) * ld + 6 * ca + d], -m);
                 }
+        }
+    }
+}
+
+// Schur reduction over the TILED points (the common, banded case).
+// One workgroup per tile: a run of points (sorted by first camera) whose active
+// cameras all lie in the window [base, base+span), span <= TILE_WIN. The tile
+// is processed in chunks of <= CHUNK_PTS points / <= CHUNK_OBS observations:
+//   phase A (thread per obs): recompute J, W~ = s_c Jc^T Jp s_p, Z = W~ G^T -> LDS;
+//           (thread per point): Zk = K~ G^T, ze = G e~ -> LDS; camera->points bitmasks
+//   phase B (thread per owner slot, registers): pair half-blocks (ca<=cb, rows 3h..3h+2)
+//           acc += sum_{p in mask[ca]&mask[cb]} Z_a Z_b^T ; border/rhs slots
+//           acc += Z_a Zk^T, Z_a ze
+// and the owner registers are flushed once per tile into S / rhs (f64 atomics:
+// ~span^2*18 adds per tile instead of ~220 per observation).
+__global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+                                                    const double* __restrict__ pdata, double* __restrict__ S,
+                                                    double* __restrict__ rhs) {
+    __shared__ double Zs[CHUNK_OBS][18];
+    __shared__ double Zk[CHUNK_PTS][12];
+    __shared__ double ze[CHUNK_PTS][3];
+    __shared__ unsigned long long mask[TILE_WIN];
+    __shared__ unsigned char oidx[CHUNK_PTS][TILE_WIN];
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int base = P.tile_base[tile];
+    const int span = P.tile_span[tile];
+    const int npair = span * (span + 1);  // half-block slots
+    const int nslot = npair + span;       // + border/rhs slots
+    // owner slot decode
+    int ca = -1, cb = -1, h = 0;
+    const bool pair_slot = tid < npair;
+    if (pair_slot) {
+        int pi = tid >> 1;
+        h = tid & 1;
+        int r = 0;
+        while (pi >= span - r) { pi -= span - r; ++r; }
+        ca = r;
+        cb = r + pi;
+    } else if (tid < nslot) {
+        ca = tid - npair;
+    }
+    double acc[30];
+#pragma unroll
+    for (int i = 0; i < 30; ++i) acc[i] = 0.0;
+    const double* K = P.K[cur];
+    for (int ch = P.tile_chunk[tile]; ch < P.tile_chunk[tile + 1]; ++ch) {
+        const int apb = P.chunk_ap[ch], ape = P.chunk_ap[ch + 1];
+        const int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
+        if (tid < TILE_WIN) mask[tid] = 0ull;
+        __syncthreads();
+        // ---- phase A
+        const int npts = ape - apb;
+        if (tid < npts) {
+            const double* pd = pdata + (size_t)(apb + tid) * PDATA;
+            double G[6], Ks[12], es[3], zk[12], z3[3];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) G[i] = pd[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) es[i] = pd[6 + i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Ks[i] = pd[9 + i];
+            zk_ze(G, Ks, es, zk, z3);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Zk[tid][i] = zk[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) ze[tid][i] = z3[i];
+        }
+        const int q = ob + tid;
+        if (q < oe) {
+            const int ac = P.po_ac[q];
+            if (ac >= 0) {
+                const int ap = P.po_ap[q];
+                const int pl = ap - apb;
+                const double2 uv = P.po_uv[q];
+                ObsEval ev;
+                double jc[18], jp[9], jk[8];
+                lin_obs(c, P.cams[cur] + 7 * P.po_cam[q], P.pts[cur] + 3 * P.pt_idx[ap], K, uv.x, uv.y, P.po_depth[q],
+                        ev, jc, jp, jk);
+                double W[18];
+                w_tilde(jc, jp, scale + 6 * ac, scale + P.off_pt + 3 * ap, W);
+                const double* G = pdata + (size_t)ap * PDATA;
+                const double g00 = G[0], g10 = G[1], g11 = G[2], g20 = G[3], g21 = G[4], g22 = G[5];
+#pragma unroll
+                for (int d = 0; d < 6; ++d) {
+                    Zs[tid][d * 3 + 0] = W[d * 3 + 0] * g00;
+                    Zs[tid][d * 3 + 1] = W[d * 3 + 0] * g10 + W[d * 3 + 1] * g11;
+                    Zs[tid][d * 3 + 2] = W[d * 3 + 0] * g20 + W[d * 3 + 1] * g21 + W[d * 3 + 2] * g22;
+                }
+                const int lc = ac - base;
+                oidx[pl][lc] = (unsigned char)tid;
+                atomicOr(&mask[lc], 1ull << pl);
+            }
+        }
+        __syncthreads();
+        // ---- phase B
+        if (pair_slot) {
+            unsigned long long m = mask[ca] & mask[cb];
+            while (m) {
+                const int p = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const double* za = Zs[oidx[p][ca]] + 9 * h;  // rows 3h..3h+2 of Z_a
+                const double* zb = Zs[oidx[p][cb]];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const double a0 = za[r * 3 + 0], a1 = za[r * 3 + 1], a2 = za[r * 3 + 2];
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) acc[r * 6 + e] += a0 * zb[e * 3 + 0] + a1 * zb[e * 3 + 1] + a2 * zb[e * 3 + 2];
+                }
+            }
+        } else if (ca >= 0) {
+            unsigned long long m = mask[ca];
+            while (m) {
+                const int p = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const double* za = Zs[oidx[p][ca]];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const double a0 = za[r * 3 + 0], a1 = za[r * 3 + 1], a2 = za[r * 3 + 2];
+#pragma unroll
+                    for (int mm = 0; mm < 4; ++mm)
+                        acc[r * 4 + mm] += a0 * Zk[p][mm * 3 + 0] + a1 * Zk[p][mm * 3 + 1] + a2 * Zk[p][mm * 3 + 2];
+                    acc[24 + r] += a0 * ze[p][0] + a1 * ze[p][1] + a2 * ze[p][2];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- flush (lower triangle of S, row-major npad)
+    const size_t ld = P.npad;
+    if (pair_slot) {
+        const int gca = 6 * (base + ca), gcb = 6 * (base + cb);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int e = 0; e < 6; ++e) {
+                const int row = gcb + e, col = gca + 3 * h + r;
+                if (row >= col) atomicAdd(&S[(size_t)row * ld + col], -acc[r * 6 + e]);
+            }
+    } else if (ca >= 0) {
+        const int g = 6 * (base + ca);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) atomicAdd(&S[(size_t)(P.kb + mm) * ld + g + r], -acc[r * 4 + mm]);
+            atomicAdd(&rhs[g + r], -acc[24 + r]);
         }
     }
 }
@@ -598,6 +775,343 @@ __global__ __launch_bounds__(TPB) void k_chol(double* __restrict__ A, int npad, 
     if (tid == 0 && s_bad) *flag = 1;
 }
 
+// ---------------------------------------------------------------- banded Cholesky
+// Reduced camera systems of sequential keyframe windows are block-banded
+// (co-visibility of nearby keyframes) plus a dense border (the intrinsics block
+// couples every camera: the last 16-row block). k_chol_band factors such a
+// matrix (band of W 16x16 tiles below the diagonal) in ONE workgroup with the
+// active band in LDS: a ring of W+1 block columns x (W+1 band tiles + 1 border
+// tile). Column k+W+1 is prefetched into registers while column k is factored;
+// the forward substitution L z = b is fused into the factorization and the
+// backward solve L^T y = z streams the factor back with one column of prefetch.
+// Trailing tile updates use v_mfma_f64_16x16x4_f64. Tiles are stored with an
+// 18-double row stride (bank-conflict-free MFMA operand reads).
+static constexpr int TLD = 18;          // LDS row stride of a 16x16 tile
+static constexpr int TSZ = 16 * TLD;    // doubles per LDS tile
+template <int W>
+struct BandLds {
+    static constexpr int TPS = W + 2;                 // tiles per ring slot (W+1 band + border)
+    static constexpr int NT = (W + 1) * TPS + 2;      // + last diagonal tile + backward diagonal tile
+    double tiles[NT][TSZ];
+    double bring[W + 1][16];                          // rhs ring (band rows)
+    double blast[16];                                 // rhs of the last block row
+    double rdiag[16];
+    double red[16][17];
+};
+static constexpr int BAND_MAX_NB = 2048;                // fcol staged in LDS (nb <= 2048)
+
+// Diagnostic stamps (separate build via STAMP=true, MIBA_CHOL_STAMPS=1): cycles per phase
+// accumulated by thread 0: [0] potrf+fwd, [1] trsm, [2] update, [3] retire/install, [4] tail+backward.
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+// uniform broadcast of lane `l`'s double (v_readlane, no LDS round trip)
+__device__ __forceinline__ double bcast(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+// 1/sqrt(x) to full f64 precision: v_rsq_f64 + two Newton steps
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = y * (1.5 - 0.5 * x * y * y);
+    y = y * (1.5 - 0.5 * x * y * y);
+    return y;
+}
+
+// In-register 16x16 Cholesky by one wave: lane r (r < 16; replicated above) holds row r.
+// rdiag[j] = 1 / L_jj. Returns false if not positive definite.
+__device__ __forceinline__ void potrf16_regs(double (&a)[16], double* rdiag, int lane, bool& bad) {
+    const int r = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        double djj = bcast(a[j], j);
+        if (!(djj > 0.0) || !isfinite(djj)) { bad = true; djj = 1.0; }
+        const double inv = rsqrt_nr(djj);
+        const double lrj = (r == j) ? djj * inv : (r > j ? a[j] * inv : 0.0);
+        a[j] = lrj;
+        if (lane == j) rdiag[j] = inv;
+#pragma unroll
+        for (int k = j + 1; k < 16; ++k) {
+            const double lkj = bcast(lrj, k);
+            if (r >= k) a[k] -= lrj * lkj;
+        }
+    }
+}
+
+template <int W, bool STAMP>
+__global__ __launch_bounds__(TPB) void k_chol_band(double* __restrict__ A, int npad, int nb, const int* __restrict__ fcol,
+                                                   double* __restrict__ b, int* __restrict__ flag,
+                                                   unsigned long long* __restrict__ stamps) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    BandLds<W>& L = *reinterpret_cast<BandLds<W>*>(smem);
+    int* fc_s = reinterpret_cast<int*>(smem + sizeof(BandLds<W>));
+    constexpr int TPS = BandLds<W>::TPS;
+    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long t_prev = 0;
+#define STAMP_AT(idx)                                  \
+    if constexpr (STAMP) {                             \
+        const unsigned long long t_ = stamp_now();    \
+        st_acc[idx] += t_ - t_prev;                   \
+        t_prev = t_;                                  \
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const size_t ld = npad;
+    const int last = nb - 1;
+    const int nbb = nb - 1;  // band block columns 0..nb-2
+    for (int i = tid; i < nb; i += TPB) fc_s[i] = fcol[i];
+    bool bad = false;
+    // tile addressing: slot(j) = j % (W+1); band tile (i,j) at offset i-j, border (last,j) at W+1
+    double* lastdiag = L.tiles[(W + 1) * TPS];
+    double* bwdiag = L.tiles[(W + 1) * TPS + 1];
+    const int er = tid >> 4, ec = tid & 15;  // element of a tile handled by this thread (copy loops)
+    // ---- initial fill: columns 0..W, last diagonal tile, rhs
+    for (int j = 0; j <= W; ++j) {
+        const int sj = j % (W + 1);
+        for (int bti = 0; bti < TPS; ++bti) {
+            const int i = (bti == W + 1) ? last : j + bti;
+            const bool ok = (j < nbb) && ((bti == W + 1) || (i < last));
+            L.tiles[sj * TPS + bti][er * TLD + ec] = ok ? A[((size_t)i * 16 + er) * ld + (size_t)j * 16 + ec] : 0.0;
+        }
+        if (tid < 16) L.bring[sj][tid] = (j < nbb) ? b[(size_t)j * 16 + tid] : 0.0;
+    }
+    lastdiag[er * TLD + ec] = A[((size_t)last * 16 + er) * ld + (size_t)last * 16 + ec];
+    if (tid < 16) L.blast[tid] = b[(size_t)last * 16 + tid];
+    __syncthreads();
+    if constexpr (STAMP) t_prev = stamp_now();
+    for (int k = 0; k < nbb; ++k) {
+        const int sk = k % (W + 1);
+        double* colk = L.tiles[sk * TPS];
+        const int kn = k + W + 1;
+        // ---- prefetch column kn into registers
+        double pre[TPS];
+        double preb = 0.0;
+#pragma unroll
+        for (int bti = 0; bti < TPS; ++bti) {
+            const int i = (bti == W + 1) ? last : kn + bti;
+            const bool ok = (kn < nbb) && ((bti == W + 1) || (i < last));
+            pre[bti] = ok ? A[((size_t)i * 16 + er) * ld + (size_t)kn * 16 + ec] : 0.0;
+        }
+        if (tid < 16 && kn < nbb) preb = b[(size_t)kn * 16 + tid];
+        const int wk = min(W, last - 1 - k);  // band rows k+1..k+wk (fcol <= k), then the border
+        // ---- 1. potrf of tile (k,k) and z_k = L_kk^-1 b_k (wave 0, registers + readlane)
+        if (wave == 0) {
+            const int r = lane & 15;
+            double a[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? colk[r * TLD + j] : 0.0;
+            potrf16_regs(a, L.rdiag, lane, bad);
+            if (lane < 16)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) colk[r * TLD + j] = (j <= r) ? a[j] : 0.0;
+            // forward step of the solve with the fresh factor: z_m = v_m / L_mm, v_r -= L_rm z_m
+            double v = L.bring[sk][r];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const double zm = bcast(v, m) * L.rdiag[m];
+                if (r > m) v -= a[m] * zm;
+                if (r == m) v = zm;
+            }
+            if (lane < 16) L.bring[sk][r] = v;
+        }
+        __syncthreads();
+        STAMP_AT(0)
+        // ---- 2. TRSM: L_ik = A_ik L_kk^-T (right-looking substitution, thread per row)
+        if (tid < (W + 1) * 16) {
+            const int bt = (tid >> 4) + 1;  // 1..W+1
+            const int r = tid & 15;
+            const bool border = (bt == W + 1);
+            const int i = border ? last : k + bt;
+            const bool act = border || (bt <= wk && fc_s[i] <= k);
+            if (act) {
+                double* T = L.tiles[sk * TPS + bt];
+                double x[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) x[j] = T[r * TLD + j];
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    x[m] *= L.rdiag[m];
+#pragma unroll
+                    for (int j = m + 1; j < 16; ++j) x[j] -= x[m] * colk[j * TLD + m];
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) T[r * TLD + j] = x[j];
+            }
+        }
+        __syncthreads();
+        STAMP_AT(1)
+        // ---- 3. trailing update over row pairs (p >= q) of {band rows 1..wk, border}; rhs update
+        {
+            const int nr = wk + 1;  // items: 0..wk-1 band (k+1+idx), wk = border
+            const int npairs = nr * (nr + 1) / 2;
+            constexpr int MAXU = ((W + 2) * (W + 1) / 2 + 3) / 4;
+            d4 acc[MAXU];
+            double* dst[MAXU];
+            const int rr = lane & 15, kk = lane >> 4;
+#pragma unroll
+            for (int u = 0; u < MAXU; ++u) {
+                acc[u] = d4{0.0, 0.0, 0.0, 0.0};
+                dst[u] = nullptr;
+                const int t = wave + 4 * u;
+                if (t < npairs) {
+                    int p = 0, rem = t;
+                    while (rem > p) { rem -= p + 1; ++p; }
+                    const int q = rem;
+                    const int ip = (p == wk) ? last : k + 1 + p;
+                    const int iq = (q == wk) ? last : k + 1 + q;
+                    if ((ip == last || fc_s[ip] <= k) && (iq == last || fc_s[iq] <= k)) {
+                        const double* Li = L.tiles[sk * TPS + ((p == wk) ? W + 1 : 1 + p)];
+                        const double* Lj = L.tiles[sk * TPS + ((q == wk) ? W + 1 : 1 + q)];
+                        dst[u] = (ip == last && iq == last)
+                                     ? lastdiag
+                                     : (ip == last ? L.tiles[(iq % (W + 1)) * TPS + W + 1]
+                                                   : L.tiles[(iq % (W + 1)) * TPS + (ip - iq)]);
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4)
+                            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[rr * TLD + 4 * s4 + kk],
+                                                                          Lj[rr * TLD + 4 * s4 + kk], acc[u], 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < MAXU; ++u)
+                if (dst[u])
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) dst[u][(kk + 4 * g) * TLD + rr] -= acc[u][g];
+            // rhs: b_i -= L_ik z_k ; one wave per tile row-block (16 lanes x 4 partial sums)
+            for (int it = wave; it < nr; it += 4) {
+                const int i = (it == wk) ? last : k + 1 + it;
+                if (i != last && fc_s[i] > k) continue;
+                const double* Li = L.tiles[sk * TPS + ((it == wk) ? W + 1 : 1 + it)];
+                const int r = lane & 15, part = lane >> 4;
+                double sacc = 0.0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) sacc += Li[r * TLD + part * 4 + c] * L.bring[sk][part * 4 + c];
+                sacc += __shfl_xor(sacc, 16);
+                sacc += __shfl_xor(sacc, 32);
+                if (lane < 16) {
+                    if (it == wk) L.blast[lane] -= sacc; else L.bring[i % (W + 1)][lane] -= sacc;
+                }
+            }
+        }
+        __syncthreads();
+        STAMP_AT(2)
+        // ---- 4. retire column k to global (L and z), install the prefetched column kn
+        for (int bti = 0; bti <= wk; ++bti) {
+            const int i = k + bti;
+            A[((size_t)i * 16 + er) * ld + (size_t)k * 16 + ec] = L.tiles[sk * TPS + bti][er * TLD + ec];
+        }
+        A[((size_t)last * 16 + er) * ld + (size_t)k * 16 + ec] = L.tiles[sk * TPS + W + 1][er * TLD + ec];
+        if (tid < 16) b[(size_t)k * 16 + tid] = L.bring[sk][tid];
+        __syncthreads();
+#pragma unroll
+        for (int bti = 0; bti < TPS; ++bti) L.tiles[sk * TPS + bti][er * TLD + ec] = pre[bti];
+        if (tid < 16) L.bring[sk][tid] = preb;
+        __syncthreads();
+        STAMP_AT(3)
+    }
+    // ---- last diagonal tile: factor, forward and backward step
+    if (wave == 0) {
+        const int r = lane & 15;
+        double a[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? lastdiag[r * TLD + j] : 0.0;
+        potrf16_regs(a, L.rdiag, lane, bad);
+        double v = L.blast[r];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const double zm = bcast(v, m) * L.rdiag[m];
+            if (r > m) v -= a[m] * zm;
+            if (r == m) v = zm;
+        }
+        // y = L^-T z : (L^T)[r][m] = L[m][r] = lane m's a[r]
+#pragma unroll
+        for (int m = 15; m >= 0; --m) {
+            const double ym = bcast(v, m) * L.rdiag[m];
+            double lmr = 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (q == r) lmr = bcast(a[q], m);  // L[m][r]
+            if (r < m) v -= lmr * ym;
+            if (r == m) v = ym;
+        }
+        if (lane < 16) {
+            L.blast[r] = v;
+            b[(size_t)last * 16 + r] = v;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) A[((size_t)last * 16 + r) * ld + (size_t)last * 16 + j] = (j <= r) ? a[j] : 0.0;
+        }
+    }
+    __syncthreads();
+    // ---- backward solve over band columns k = nb-2 .. 0 ; y ring in L.bring, y_last in L.blast
+    {
+        const int r = tid & 15, p = tid >> 4;
+        double cur[W + 1], nxt[W + 1];
+        double dg_cur = 0.0, dg_nxt = 0.0, zk_cur = 0.0, zk_nxt = 0.0;
+        auto load_col = [&](int k, double* v, double& dg, double& zk) {
+#pragma unroll
+            for (int it = 0; it <= W; ++it) {
+                const int i = (it == W) ? last : k + 1 + it;
+                const bool ok = (k >= 0) && ((it == W) || (i < last));
+                v[it] = ok ? A[((size_t)i * 16 + p) * ld + (size_t)k * 16 + r] : 0.0;
+            }
+            dg = (k >= 0) ? A[((size_t)k * 16 + p) * ld + (size_t)k * 16 + r] : 0.0;
+            zk = (k >= 0 && tid < 16) ? b[(size_t)k * 16 + tid] : 0.0;
+        };
+        load_col(nbb - 1, cur, dg_cur, zk_cur);
+        for (int k = nbb - 1; k >= 0; --k) {
+            load_col(k - 1, nxt, dg_nxt, zk_nxt);
+            const int wk = min(W, last - 1 - k);
+            double sacc = 0.0;
+#pragma unroll
+            for (int it = 0; it <= W; ++it) {
+                const bool border = (it == W);
+                const int i = border ? last : k + 1 + it;
+                const bool act = border || (it < wk && fc_s[i] <= k);
+                if (act) sacc += cur[it] * (border ? L.blast[p] : L.bring[i % (W + 1)][p]);
+            }
+            L.red[p][r] = sacc;
+            bwdiag[p * TLD + r] = dg_cur;
+            if (p == r) L.rdiag[r] = 1.0 / dg_cur;
+            __syncthreads();
+            if (wave == 0) {
+                const int rr = lane & 15;
+                double v = __shfl(zk_cur, rr);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v -= L.red[q][rr];
+                // y_k = L_kk^-T v ; (L^T)[rr][m] = L[m][rr]
+#pragma unroll
+                for (int m = 15; m >= 0; --m) {
+                    const double ym = bcast(v, m) * L.rdiag[m];
+                    if (rr < m) v -= bwdiag[m * TLD + rr] * ym;
+                    if (rr == m) v = ym;
+                }
+                if (lane < 16) {
+                    L.bring[k % (W + 1)][lane] = v;
+                    b[(size_t)k * 16 + lane] = v;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it <= W; ++it) cur[it] = nxt[it];
+            dg_cur = dg_nxt;
+            zk_cur = zk_nxt;
+        }
+    }
+    STAMP_AT(4)
+    if constexpr (STAMP) {
+        if (tid == 0)
+            for (int i = 0; i < 5; ++i) stamps[i] = st_acc[i];
+    }
+#undef STAMP_AT
+    if (bad) *flag = 1;
+}
+
 // ---------------------------------------------------------------- update
 // delta = -s * y over cameras and intrinsics; candidate poses; prior-block model
 // change and candidate prior cost. part[PART_UPD_* * stride + block]
@@ -695,11 +1209,11 @@ __global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, 
             for (int i = 0; i < 3; ++i) t[i] -= sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
         }
         double dp[3], xn[3];
+        double Vf[9];
+        vinv_from_g(pd, Vf);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double yp = pd[i == 0 ? 0 : (i == 1 ? 1 : 2)] * t[0] +
-                              pd[i == 0 ? 1 : (i == 1 ? 3 : 4)] * t[1] +
-                              pd[i == 0 ? 2 : (i == 1 ? 4 : 5)] * t[2];
+            const double yp = Vf[i * 3 + 0] * t[0] + Vf[i * 3 + 1] * t[1] + Vf[i * 3 + 2] * t[2];
             dp[i] = -sp[i] * yp;
             xn[i] = X[i] + dp[i];
             Xn[i] = xn[i];
@@ -841,13 +1355,53 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, int cur, double 
     if (P.n_ap > 0)
         PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, cur, 1, radius, W.scale,
            W.cnp, W.pdata, W.S, W.rhs, W.part);
-    if (P.n_adm > 0)
-        PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata, W.S,
-           W.rhs);
+    if (P.n_tiles > 0)
+        PL(K_SCHUR_TILE, k_schur_tile, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata, W.S, W.rhs);
+    if (P.n_ovf_obs > 0)
+        PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata,
+           W.S, W.rhs);
+    return hipSuccess;
+}
+
+template <int BW>
+static hipError_t launch_band(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
+    const size_t lds = sizeof(BandLds<BW>) + sizeof(int) * BAND_MAX_NB;
+    static bool attr_set = false;
+    static int stamp_mode = -1;
+    if (!attr_set) {
+        CK(hipFuncSetAttribute((const void*)k_chol_band<BW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        CK(hipFuncSetAttribute((const void*)k_chol_band<BW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+        const char* e = getenv("MIBA_CHOL_STAMPS");
+        stamp_mode = (e && e[0] == '1') ? 1 : 0;
+    }
+    if (stamp_mode == 1) {
+        static unsigned long long* dst = nullptr;
+        if (!dst) CK(hipMalloc(&dst, 8 * sizeof(unsigned long long)));
+        PL(K_CHOL, (k_chol_band<BW, true>), dim3(1), dim3(TPB), lds, s, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
+           W.chol_flag, dst);
+        unsigned long long h[8];
+        CK(hipMemcpyAsync(h, dst, sizeof(h[0]) * 5, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        fprintf(stderr, "chol_band<%d> nb=%d cycles: potrf %llu trsm %llu update %llu retire %llu backward %llu\n", BW,
+                P.npad / 16, h[0], h[1], h[2], h[3], h[4]);
+        return hipSuccess;
+    }
+    PL(K_CHOL, (k_chol_band<BW, false>), dim3(1), dim3(TPB), lds, s, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
+       W.chol_flag, (unsigned long long*)nullptr);
     return hipSuccess;
 }
 
 hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
+    switch (P.band_w) {
+        case 1: return launch_band<1>(P, W, s, pf);
+        case 2: return launch_band<2>(P, W, s, pf);
+        case 3: return launch_band<3>(P, W, s, pf);
+        case 4: return launch_band<4>(P, W, s, pf);
+        case 5: return launch_band<5>(P, W, s, pf);
+        case 6: return launch_band<6>(P, W, s, pf);
+        default: break;
+    }
     PL(K_CHOL, k_chol, dim3(1), dim3(TPB), 0, s, W.S, P.npad, P.npad / 16, W.fcol, W.rptr, W.rows, W.rhs,
        W.chol_flag);
     return hipSuccess;

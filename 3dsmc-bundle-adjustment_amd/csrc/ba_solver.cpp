@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,7 +57,7 @@ enum BufId {
     B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_FCOL, B_RPTR, B_ROWS, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3,
     B_COUNT
 };
@@ -78,6 +79,7 @@ struct ba_context {
     BaConsts C{};
     int nblk_pt = 0;
     bool prepared = false;
+    int n_tiles = 0, n_ovf_obs = 0, n_tiled_pts = 0;
     int prep_nc = -1, prep_np = -1, prep_no = -1;
     // per-kernel profiling
     Prof prof;
@@ -256,33 +258,83 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     for (int i = 0; i < nc; ++i)
         if (cam_cnt[i] > 0 && i != p->fixed_cam) { cam_ac[i] = (int)ctx->ac_cam.size(); ctx->ac_cam.push_back(i); }
     const int nac = (int)ctx->ac_cam.size();
-    // per point: min active camera (for ordering and the envelope)
-    std::vector<int> pmin(np, INT32_MAX);
+    // CSR of admissible obs by original point index, each list sorted by active camera
+    std::vector<int> pptr(np + 1, 0);
     for (int k = 0; k < no; ++k)
-        if (adm[k]) {
-            const int a = cam_ac[p->obs_cam[k]];
-            if (a >= 0) pmin[p->obs_pt[k]] = std::min(pmin[p->obs_pt[k]], a);
-        }
-    // active points ordered by (min active camera, index) -> banded locality
-    ctx->pt_idx.clear();
-    for (int i = 0; i < np; ++i)
-        if (pt_cnt[i] > 0) ctx->pt_idx.push_back(i);
-    std::stable_sort(ctx->pt_idx.begin(), ctx->pt_idx.end(), [&](int a, int b) { return pmin[a] < pmin[b]; });
-    const int n_ap = (int)ctx->pt_idx.size();
-    std::vector<int> ap_of(np, -1);
-    for (int a = 0; a < n_ap; ++a) ap_of[ctx->pt_idx[a]] = a;
-    // point-major obs
-    std::vector<int> pt_ptr(n_ap + 1, 0);
-    for (int a = 0; a < n_ap; ++a) pt_ptr[a + 1] = pt_ptr[a] + pt_cnt[ctx->pt_idx[a]];
-    std::vector<int> fill(pt_ptr.begin(), pt_ptr.end() - 1);
-    ctx->po_orig.assign(n_adm, 0);
-    for (int k = 0; k < no; ++k)
-        if (adm[k]) ctx->po_orig[fill[ap_of[p->obs_pt[k]]]++] = k;
-    // within a point: by active camera (gauge/unobserved first), then original order
-    for (int a = 0; a < n_ap; ++a)
-        std::stable_sort(ctx->po_orig.begin() + pt_ptr[a], ctx->po_orig.begin() + pt_ptr[a + 1],
+        if (adm[k]) ++pptr[p->obs_pt[k] + 1];
+    for (int i = 0; i < np; ++i) pptr[i + 1] += pptr[i];
+    std::vector<int> plist(n_adm);
+    {
+        std::vector<int> f(pptr.begin(), pptr.end() - 1);
+        for (int k = 0; k < no; ++k)
+            if (adm[k]) plist[f[p->obs_pt[k]]++] = k;
+    }
+    std::vector<int> pmin(np, INT32_MAX), pmax(np, -1);
+    std::vector<char> pclass(np, -1);  // 0 tiled, 1 overflow (Schur via atomics), 2 gauge-only
+    for (int i = 0; i < np; ++i) {
+        if (pt_cnt[i] == 0) continue;
+        std::stable_sort(plist.begin() + pptr[i], plist.begin() + pptr[i + 1],
                          [&](int x, int y) { return cam_ac[p->obs_cam[x]] < cam_ac[p->obs_cam[y]]; });
-    std::vector<int> po_cam(n_adm), po_ac(n_adm), po_ap(n_adm);
+        bool dup = false;
+        int prev = -2;
+        for (int q = pptr[i]; q < pptr[i + 1]; ++q) {
+            const int a = cam_ac[p->obs_cam[plist[q]]];
+            if (a < 0) continue;
+            pmin[i] = std::min(pmin[i], a);
+            pmax[i] = std::max(pmax[i], a);
+            if (a == prev) dup = true;
+            prev = a;
+        }
+        if (pmax[i] < 0) pclass[i] = 2;
+        else if (dup || pmax[i] - pmin[i] + 1 > TILE_WIN || pt_cnt[i] > CHUNK_OBS) pclass[i] = 1;
+        else pclass[i] = 0;
+    }
+    std::vector<int> cls[3];
+    for (int i = 0; i < np; ++i)
+        if (pclass[i] >= 0) cls[(int)pclass[i]].push_back(i);
+    for (int k = 0; k < 2; ++k)
+        std::stable_sort(cls[k].begin(), cls[k].end(), [&](int a, int b) { return pmin[a] < pmin[b]; });
+    // tiles over the tiled points: window [base, base + span), span <= TILE_WIN, <= TILE_PTS points;
+    // chunks of <= CHUNK_PTS points and <= CHUNK_OBS observations
+    constexpr int TILE_PTS = 128;
+    std::vector<int> tile_chunk(1, 0), tile_base, tile_span, chunk_ap(1, 0);
+    {
+        const std::vector<int>& T = cls[0];
+        const int n0 = (int)T.size();
+        int i = 0;
+        while (i < n0) {
+            const int base = pmin[T[i]];
+            int j = i, hi = base;
+            while (j < n0 && j - i < TILE_PTS && pmax[T[j]] - base < TILE_WIN) { hi = std::max(hi, pmax[T[j]]); ++j; }
+            // chunks
+            int c0 = i;
+            while (c0 < j) {
+                int c1 = c0, nob = 0;
+                while (c1 < j && c1 - c0 < CHUNK_PTS && nob + pt_cnt[T[c1]] <= CHUNK_OBS) { nob += pt_cnt[T[c1]]; ++c1; }
+                chunk_ap.push_back(c1);
+                c0 = c1;
+            }
+            tile_chunk.push_back((int)chunk_ap.size() - 1);
+            tile_base.push_back(base);
+            tile_span.push_back(hi - base + 1);
+            i = j;
+        }
+    }
+    // active point order: tiled (tile order), overflow, gauge-only
+    ctx->pt_idx.clear();
+    for (int k = 0; k < 3; ++k) ctx->pt_idx.insert(ctx->pt_idx.end(), cls[k].begin(), cls[k].end());
+    const int n_ap = (int)ctx->pt_idx.size();
+    const int n_tiled = (int)cls[0].size();
+    // point-major obs in that order
+    std::vector<int> pt_ptr(n_ap + 1, 0);
+    ctx->po_orig.clear();
+    ctx->po_orig.reserve(n_adm);
+    for (int a = 0; a < n_ap; ++a) {
+        const int i = ctx->pt_idx[a];
+        ctx->po_orig.insert(ctx->po_orig.end(), plist.begin() + pptr[i], plist.begin() + pptr[i + 1]);
+        pt_ptr[a + 1] = (int)ctx->po_orig.size();
+    }
+    std::vector<int> po_cam(n_adm), po_ac(n_adm), po_ap(n_adm), ovf_obs;
     std::vector<double> po_uv(2 * (size_t)n_adm), po_dep(n_adm);
     for (int a = 0; a < n_ap; ++a)
         for (int q = pt_ptr[a]; q < pt_ptr[a + 1]; ++q) {
@@ -293,6 +345,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             po_uv[2 * (size_t)q] = p->obs_uv[2 * (size_t)k];
             po_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
             po_dep[q] = p->obs_depth[k];
+            if (a >= n_tiled && po_ac[q] >= 0) ovf_obs.push_back(q);
         }
     // camera-major obs: one segment per camera with admissible obs (gauge included)
     std::vector<int> seg_ptr(1, 0), seg_cam, seg_ac;
@@ -330,6 +383,9 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         const int first = (r < 6 * nac) ? 6 * fc[r / 6] : 0;
         fcol[r / 16] = std::min(fcol[r / 16], first / 16);
     }
+    // band width (in 16-tiles) of the camera part; the last block row is the dense border
+    int band_w = 0;
+    for (int i = 0; i + 1 < nb; ++i) band_w = std::max(band_w, i - fcol[i]);
     std::vector<int> rptr(nb + 1, 0), rows;
     for (int k = 0; k < nb; ++k) {
         for (int i = k + 1; i < nb; ++i)
@@ -363,6 +419,11 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     HIPCHECK(ctx, upload(ctx, B_SEG_AC, seg_ac.data(), seg_ac.size()));
     HIPCHECK(ctx, upload(ctx, B_AC_CAM, ctx->ac_cam.data(), nac));
     HIPCHECK(ctx, upload(ctx, B_FCOL, fcol.data(), nb));
+    HIPCHECK(ctx, upload(ctx, B_TILE_CHUNK, tile_chunk.data(), tile_chunk.size()));
+    HIPCHECK(ctx, upload(ctx, B_TILE_BASE, tile_base.data(), tile_base.size()));
+    HIPCHECK(ctx, upload(ctx, B_TILE_SPAN, tile_span.data(), tile_span.size()));
+    HIPCHECK(ctx, upload(ctx, B_CHUNK_AP, chunk_ap.data(), chunk_ap.size()));
+    HIPCHECK(ctx, upload(ctx, B_OVF_OBS, ovf_obs.data(), ovf_obs.size()));
     HIPCHECK(ctx, upload(ctx, B_RPTR, rptr.data(), nb + 1));
     HIPCHECK(ctx, upload(ctx, B_ROWS, rows.data(), rows.size()));
     const int n_seg = (int)seg_cam.size();
@@ -395,10 +456,17 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     P.co_depth = ctx->buf[B_CO_DEP].as<double>();
     P.seg_ptr = ctx->buf[B_SEG_PTR].as<int>(); P.seg_cam = ctx->buf[B_SEG_CAM].as<int>();
     P.seg_ac = ctx->buf[B_SEG_AC].as<int>(); P.ac_cam = ctx->buf[B_AC_CAM].as<int>();
+    P.tile_chunk = ctx->buf[B_TILE_CHUNK].as<int>(); P.tile_base = ctx->buf[B_TILE_BASE].as<int>();
+    P.tile_span = ctx->buf[B_TILE_SPAN].as<int>(); P.chunk_ap = ctx->buf[B_CHUNK_AP].as<int>();
+    P.ovf_obs = ctx->buf[B_OVF_OBS].as<int>();
+    P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
+    ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
     P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
     P.n = n; P.npad = npad; P.kb = 6 * nac;
     P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
     P.part_stride = part_stride;
+    P.band_w = (nb >= 2 && nb <= 2048 && band_w <= 6) ? std::max(band_w, 1) : 0;
+    if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.band_w = 0;
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
     W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
@@ -436,7 +504,9 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
         kb[K_POINT_PREP] = A * 28 + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
         kf[K_POINT_PREP] = A * 300 + Pn * 200;
-        kb[K_OBS_PAIRS] = A * 36 + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
+        kb[K_SCHUR_TILE] = A * 36 + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
+        kf[K_SCHUR_TILE] = A * 350 + Pn * 13300;
+        kb[K_OBS_PAIRS] = ctx->n_ovf_obs * 36.0;
         kb[K_CHOL] = 2 * env_bytes + 3 * npad * 8.0;
         kf[K_CHOL] = 0;
         for (int k = 0; k < nb; ++k) {

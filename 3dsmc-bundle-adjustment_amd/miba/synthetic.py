@@ -125,7 +125,7 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
                  outlier_frac: float = 0.02, outlier_px: float = 20.0, depth_noise: float = 0.01,
                  rot_noise: float = 0.01, trans_noise: float = 0.01, point_noise: float = 0.02,
                  intr_offset=(2.0, -1.5, 1.0, -0.8), fixed_cam: int = 0, shuffle_obs: bool = False,
-                 bad_depth_frac: float = 0.0) -> ProblemArrays:
+                 bad_depth_frac: float = 0.0, dup_frac: float = 0.0) -> ProblemArrays:
     """Build one synthetic window. ``obs_per_point`` is an int or an inclusive (lo, hi) range."""
     rng = np.random.default_rng(seed)
     if isinstance(obs_per_point, (tuple, list)):
@@ -174,6 +174,14 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
         t0[fixed_cam] = t_wc[fixed_cam]
     cams = np.concatenate([quat_from_rotmat(R0), t0], axis=1)
     pts0 = X + rng.normal(0.0, point_noise, X.shape)
+    if dup_frac > 0:
+        # the same landmark linked to a second keypoint of the same keyframe
+        dup = np.nonzero(rng.random(n_obs) < dup_frac)[0]
+        obs_cam = np.concatenate([obs_cam, obs_cam[dup]])
+        obs_pt = np.concatenate([obs_pt, obs_pt[dup]])
+        uv = np.concatenate([uv, uv[dup] + rng.normal(0.0, 1.0, (len(dup), 2))])
+        depth = np.concatenate([depth, depth[dup] * (1.0 + rng.normal(0.0, depth_noise, len(dup)))])
+        n_obs = len(obs_cam)
     if shuffle_obs:
         perm = rng.permutation(n_obs)
         obs_cam, obs_pt, uv, depth = obs_cam[perm], obs_pt[perm], uv[perm], depth[perm]

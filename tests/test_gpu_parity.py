@@ -30,6 +30,9 @@ CASES = {
     "shuffled_bad_depth": dict(n_cams=12, n_points=200, obs_per_point=(2, 6), seed=3, shuffle_obs=True,
                                bad_depth_frac=0.05),
     "no_gauge_cam_obs": dict(n_cams=8, n_points=120, obs_per_point=(2, 4), seed=4, fixed_cam=3),
+    # points spanning > TILE_WIN cameras and repeated-camera links take the overflow (atomic) Schur path
+    "wide_overflow": dict(n_cams=30, n_points=150, obs_per_point=(6, 16), seed=5, rot_noise=0.005),
+    "dup_obs": dict(n_cams=10, n_points=200, obs_per_point=(2, 5), seed=6, dup_frac=0.05),
 }
 
 
@@ -86,3 +89,17 @@ def test_c2_config_final_cost():
     so = oracle.solve(q)
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
     assert sg["num_iterations"] == so["num_iterations"]
+
+
+@pytest.mark.parametrize("dense", ["0", "1"])
+@pytest.mark.parametrize("case", ["banded", "tum_like", "wide_overflow"])
+def test_band_and_dense_cholesky_agree(case, dense, monkeypatch):
+    """The banded LDS Cholesky and the dense-envelope kernel solve the same step."""
+    from miba.solver import Solver
+    monkeypatch.setenv("MIBA_DENSE_CHOL", dense)
+    p = synthetic.make_problem(**CASES[case])
+    q = p.copy()
+    with Solver(minimizer_progress_to_stdout=0, max_num_iterations=5) as s:
+        sg = s.solve(p)
+    so = oracle.solve(q, oracle.default_options(max_num_iterations=5))
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sg, so)
