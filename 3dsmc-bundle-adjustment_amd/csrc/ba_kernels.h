@@ -28,10 +28,12 @@ enum {
     PART_BS_MCC,
     PART_BS_COST,
     PART_BS_BAD,
+    PART_UPD_XN2,
+    PART_BS_XN2,
     PART_NSLOTS
 };
 // final scalars
-enum { SC_MCC = 0, SC_CAND, SC_SN2, SC_GMAX_PT, SC_BAD, SC_N = 8 };
+enum { SC_MCC = 0, SC_CAND, SC_SN2, SC_GMAX_PT, SC_BAD, SC_XN2, SC_N = 8 };
 // lin record: [0] cost(x), [1] gmax cams+intr, [2..12) Ukk packed (+prior), [12..16) gk (+prior)
 static constexpr int LIN_N = 16;
 
@@ -74,6 +76,23 @@ struct DevProblem {
     int band_w;  // 16x16 tiles below the diagonal in the camera band; <=0 or >6: dense envelope kernel
 };
 
+// Device-resident Levenberg-Marquardt state (Ceres 2.0 TrustRegionMinimizer +
+// LevenbergMarquardtStrategy bookkeeping, owned by k_lm_decide).
+struct LmState {
+    double radius, decrease_factor, x_cost, xnorm2, final_cost, gmax_ci, initial_cost;
+    double msg_a, msg_b;
+    int iter, n_succ, n_unsucc, n_invalid, step_ok, cur, need_lin, done, termination, msg;
+};
+struct LmParams {
+    double min_relative_decrease, max_radius, min_radius, function_tolerance, gradient_tolerance,
+        parameter_tolerance;
+    int max_iter, max_invalid;
+};
+enum LmMsg { MSG_NONE = 0, MSG_MAX_ITER, MSG_GRAD_TOL, MSG_MIN_RADIUS, MSG_PARAM_TOL, MSG_FUNC_TOL, MSG_INVALID,
+             MSG_EVAL_FAIL };
+// per-iteration log row: cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius, accepted
+static constexpr int LOG_W = 8;
+
 struct DevWork {
     double* camdata;
     double* seg_intr;
@@ -90,20 +109,22 @@ struct DevWork {
     int* fcol;
     int* rptr;
     int* rows;
+    LmState* st;
+    double* log;  // [(max_iter + 2) * LOG_W]
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
-    K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_COUNT
+    K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
-    "obs_pairs", "chol", "update_cams", "backsub_eval", "final"};
+    "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {
-    static constexpr int MAXP = 64;
+    static constexpr int MAXP = 160;
     int on = 0;
     int n = 0;
     int id[MAXP];
@@ -116,14 +137,16 @@ struct Prof {
     }
 };
 
-hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int cur, int jacobi, DevWork& W, hipStream_t s,
-                        Prof* pf);
-hipError_t launch_build(const DevProblem& P, const BaConsts& c, int cur, double radius, DevWork& W, hipStream_t s,
-                        Prof* pf);
+// All kernels read cur / radius / done from W.st (device), so an LM iteration is a
+// fixed launch sequence the host can enqueue without reading anything back.
+hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_update(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, int cur, double* res, double* jc, double* jp,
+hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s);
 
 }  // namespace miba

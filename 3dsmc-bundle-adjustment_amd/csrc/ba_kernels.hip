@@ -70,8 +70,10 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
 // One workgroup per camera segment of the camera-major observation list.
 // camdata[ac*CAMDATA + ..]: U upper-packed (21), C (6x4 = 24), g (6)
 // seg_intr[s*SEGINTR + ..]: Ukk upper-packed (10), gk (4), cost (1)
-__global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, int cur, double* __restrict__ camdata,
-                                                  double* __restrict__ seg_intr) {
+__global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
+                                                  double* __restrict__ camdata, double* __restrict__ seg_intr) {
+    if (st->done || (gated && !st->need_lin)) return;
+    const int cur = st->cur;
     __shared__ double lds[4 * 66];
     __shared__ double out[66];
     const int s = blockIdx.x;
@@ -122,8 +124,11 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, int 
 // (OptimizationUtils.cpp:117-125, squared loss), compute the gradient max-norm of
 // cameras + intrinsics: ||x - Plus(x, -g)||_inf (Ceres 2.0 trust_region_minimizer).
 // lin[0] = cost(x), lin[1] = gmax(cams, intr), lin[2..12) = Ukk packed, lin[12..16) = gk
-__global__ __launch_bounds__(TPB) void k_lin_finalize(DevProblem P, BaConsts c, int cur, const double* __restrict__ camdata,
+__global__ __launch_bounds__(TPB) void k_lin_finalize(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
+                                                      const double* __restrict__ camdata,
                                                       const double* __restrict__ seg_intr, double* __restrict__ lin) {
+    if (st->done || (gated && !st->need_lin)) return;
+    const int cur = st->cur;
     __shared__ double lds[4 * SEGINTR];
     __shared__ double out[SEGINTR];
     __shared__ double red[4];
@@ -207,13 +212,16 @@ __device__ __forceinline__ void w_tilde(const double jc[18], const double jp[9],
 // mode 0: column norms only (iteration 0, before the Jacobi scale exists)
 // mode 1: full Schur preparation.
 // pdata[ap*PDATA]: Vinv packed (6: 00 01 02 11 12 22), e (3), Kt (12, [m][i])
-__global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, int cur, int mode, double radius,
+__global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, const LmState* __restrict__ st, int mode,
                                                     const double* __restrict__ scale, double* __restrict__ cnp,
                                                     double* __restrict__ pdata, double* __restrict__ S,
                                                     double* __restrict__ rhs, double* __restrict__ part) {
     __shared__ double lds[4 * 14];
     __shared__ double out[14];
     __shared__ double red[4];
+    if (st->done) return;
+    const int cur = st->cur;
+    const double radius = st->radius;
     const int ap = blockIdx.x * TPB + threadIdx.x;
     double kk[14];
 #pragma unroll
@@ -352,9 +360,11 @@ __global__ void k_scale(DevProblem P, const double* __restrict__ camdata, const 
 // ---------------------------------------------------------------- assembly
 // Writes the camera/intrinsics (F-block) part of the damped, scaled normal
 // equations into the lower triangle of S (row-major, npad stride) and rhs = J~^T f.
-__global__ void k_assemble(DevProblem P, BaConsts c, double radius, const double* __restrict__ camdata,
+__global__ void k_assemble(DevProblem P, BaConsts c, const LmState* __restrict__ st, const double* __restrict__ camdata,
                            const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
                            double* __restrict__ rhs) {
+    if (st->done) return;
+    const double radius = st->radius;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const size_t ld = P.npad;
     const int kb = P.kb;
@@ -389,9 +399,12 @@ __global__ void k_assemble(DevProblem P, BaConsts c, double radius, const double
 
 // Schur scatter for the OVERFLOW points (span > TILE_WIN cameras or repeated
 // cameras): thread per listed observation, global f64 atomics.
-__global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+__global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                   const double* __restrict__ scale,
                                                    const double* __restrict__ pdata, double* __restrict__ S,
                                                    double* __restrict__ rhs) {
+    if (st->done) return;
+    const int cur = st->cur;
     const int t = blockIdx.x * TPB + threadIdx.x;
     if (t >= P.n_ovf_obs) return;
     const int a = P.ovf_obs[t];
@@ -484,7 +497,8 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, int
 //           acc += Z_a Zk^T, Z_a ze
 // and the owner registers are flushed once per tile into S / rhs (f64 atomics:
 // ~span^2*18 adds per tile instead of ~220 per observation).
-__global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+__global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                    const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
                                                     double* __restrict__ rhs) {
     __shared__ double Zs[CHUNK_OBS][18];
@@ -492,6 +506,8 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, in
     __shared__ double ze[CHUNK_PTS][3];
     __shared__ unsigned long long mask[TILE_WIN];
     __shared__ unsigned char oidx[CHUNK_PTS][TILE_WIN];
+    if (st->done) return;
+    const int cur = st->cur;
     const int tile = blockIdx.x;
     const int tid = threadIdx.x;
     const int base = P.tile_base[tile];
@@ -626,9 +642,11 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, in
 // rows[rptr[k]..rptr[k+1]): block rows i > k with fcol[i] <= k.
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(TPB) void k_chol(double* __restrict__ A, int npad, int nb, const int* __restrict__ fcol,
+__global__ __launch_bounds__(TPB) void k_chol(const LmState* __restrict__ st, double* __restrict__ A, int npad, int nb,
+                                              const int* __restrict__ fcol,
                                               const int* __restrict__ rptr, const int* __restrict__ rows,
                                               double* __restrict__ b, int* __restrict__ flag) {
+    if (st->done) return;
     __shared__ double Lkk[16][17];
     __shared__ double red[16][17];
     __shared__ int s_bad;
@@ -801,7 +819,8 @@ struct BandLds {
 static constexpr int BAND_MAX_NB = 2048;                // fcol staged in LDS (nb <= 2048)
 
 // Diagnostic stamps (separate build via STAMP=true, MIBA_CHOL_STAMPS=1): cycles per phase
-// accumulated by thread 0: [0] potrf+fwd, [1] trsm, [2] update, [3] retire/install, [4] tail+backward.
+// accumulated by thread 0: [0] prefetch issue, [1] trsm, [2] update || look-ahead potrf, [3] retire/install,
+// [4] tail+backward.
 __device__ __forceinline__ unsigned long long stamp_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -825,29 +844,33 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 }
 
 // In-register 16x16 Cholesky by one wave: lane r (r < 16; replicated above) holds row r.
-// rdiag[j] = 1 / L_jj. Returns false if not positive definite.
+// Entries above the diagonal are scratch (never consumed; masked at write-back), so the
+// rank-1 updates run unpredicated. rdiag[j] = 1 / L_jj.
 __device__ __forceinline__ void potrf16_regs(double (&a)[16], double* rdiag, int lane, bool& bad) {
     const int r = lane & 15;
+    double my_inv = 0.0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         double djj = bcast(a[j], j);
-        if (!(djj > 0.0) || !isfinite(djj)) { bad = true; djj = 1.0; }
+        const bool ok = (djj > 0.0) && (djj < INFINITY);
+        bad = bad || !ok;
+        djj = ok ? djj : 1.0;
         const double inv = rsqrt_nr(djj);
-        const double lrj = (r == j) ? djj * inv : (r > j ? a[j] * inv : 0.0);
+        const double lrj = a[j] * inv;  // lane j: sqrt(d_jj); lanes r > j: L_rj
         a[j] = lrj;
-        if (lane == j) rdiag[j] = inv;
+        my_inv = (r == j) ? inv : my_inv;
 #pragma unroll
-        for (int k = j + 1; k < 16; ++k) {
-            const double lkj = bcast(lrj, k);
-            if (r >= k) a[k] -= lrj * lkj;
-        }
+        for (int k = j + 1; k < 16; ++k) a[k] -= lrj * bcast(lrj, k);
     }
+    if (lane < 16) rdiag[r] = my_inv;
 }
 
 template <int W, bool STAMP>
-__global__ __launch_bounds__(TPB) void k_chol_band(double* __restrict__ A, int npad, int nb, const int* __restrict__ fcol,
+__global__ __launch_bounds__(TPB) void k_chol_band(const LmState* __restrict__ st, double* __restrict__ A, int npad, int nb,
+                                                   const int* __restrict__ fcol,
                                                    double* __restrict__ b, int* __restrict__ flag,
                                                    unsigned long long* __restrict__ stamps) {
+    if (st->done) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BandLds<W>& L = *reinterpret_cast<BandLds<W>*>(smem);
     int* fc_s = reinterpret_cast<int*>(smem + sizeof(BandLds<W>));
@@ -884,6 +907,29 @@ __global__ __launch_bounds__(TPB) void k_chol_band(double* __restrict__ A, int n
     if (tid < 16) L.blast[tid] = b[(size_t)last * 16 + tid];
     __syncthreads();
     if constexpr (STAMP) t_prev = stamp_now();
+    // wave-0 helper: factor the diagonal tile held in `colk` (rows in registers), write it back,
+    // and run the forward step z = L^-1 z on the rhs block `bz`.
+    auto factor_diag = [&](double* Tk, double* bz) {
+        const int r = lane & 15;
+        double a[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? Tk[r * TLD + j] : 0.0;
+        potrf16_regs(a, L.rdiag, lane, bad);
+        if (lane < 16)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) Tk[r * TLD + j] = (j <= r) ? a[j] : 0.0;
+        double v = bz[r];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const double zm = bcast(v, m) * L.rdiag[m];
+            if (r > m) v -= a[m] * zm;
+            if (r == m) v = zm;
+        }
+        if (lane < 16) bz[r] = v;
+    };
+    // prologue: factor tile (0,0)
+    if (nbb > 0 && wave == 0) factor_diag(L.tiles[0], L.bring[0]);
+    __syncthreads();
     for (int k = 0; k < nbb; ++k) {
         const int sk = k % (W + 1);
         double* colk = L.tiles[sk * TPS];
@@ -899,29 +945,8 @@ __global__ __launch_bounds__(TPB) void k_chol_band(double* __restrict__ A, int n
         }
         if (tid < 16 && kn < nbb) preb = b[(size_t)kn * 16 + tid];
         const int wk = min(W, last - 1 - k);  // band rows k+1..k+wk (fcol <= k), then the border
-        // ---- 1. potrf of tile (k,k) and z_k = L_kk^-1 b_k (wave 0, registers + readlane)
-        if (wave == 0) {
-            const int r = lane & 15;
-            double a[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? colk[r * TLD + j] : 0.0;
-            potrf16_regs(a, L.rdiag, lane, bad);
-            if (lane < 16)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) colk[r * TLD + j] = (j <= r) ? a[j] : 0.0;
-            // forward step of the solve with the fresh factor: z_m = v_m / L_mm, v_r -= L_rm z_m
-            double v = L.bring[sk][r];
-#pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                const double zm = bcast(v, m) * L.rdiag[m];
-                if (r > m) v -= a[m] * zm;
-                if (r == m) v = zm;
-            }
-            if (lane < 16) L.bring[sk][r] = v;
-        }
-        __syncthreads();
         STAMP_AT(0)
-        // ---- 2. TRSM: L_ik = A_ik L_kk^-T (right-looking substitution, thread per row)
+        // ---- 1. TRSM: L_ik = A_ik L_kk^-T (tile (k,k) factored by the previous look-ahead)
         if (tid < (W + 1) * 16) {
             const int bt = (tid >> 4) + 1;  // 1..W+1
             const int r = tid & 15;
@@ -945,63 +970,92 @@ __global__ __launch_bounds__(TPB) void k_chol_band(double* __restrict__ A, int n
         }
         __syncthreads();
         STAMP_AT(1)
-        // ---- 3. trailing update over row pairs (p >= q) of {band rows 1..wk, border}; rhs update
+        // ---- 2. trailing update. Wave 0: look-ahead on block column k+1 (update + factor the
+        //         diagonal tile (k+1,k+1), rhs of row k+1); waves 1..3: every other tile and rhs row.
         {
-            const int nr = wk + 1;  // items: 0..wk-1 band (k+1+idx), wk = border
+            const int nr = wk + 1;  // items: 0..wk-1 band rows k+1+idx, wk = border
             const int npairs = nr * (nr + 1) / 2;
-            constexpr int MAXU = ((W + 2) * (W + 1) / 2 + 3) / 4;
-            d4 acc[MAXU];
-            double* dst[MAXU];
+            const bool la = (wk >= 1);  // look-ahead exists (band row k+1 < last)
             const int rr = lane & 15, kk = lane >> 4;
-#pragma unroll
-            for (int u = 0; u < MAXU; ++u) {
-                acc[u] = d4{0.0, 0.0, 0.0, 0.0};
-                dst[u] = nullptr;
-                const int t = wave + 4 * u;
-                if (t < npairs) {
-                    int p = 0, rem = t;
-                    while (rem > p) { rem -= p + 1; ++p; }
-                    const int q = rem;
-                    const int ip = (p == wk) ? last : k + 1 + p;
-                    const int iq = (q == wk) ? last : k + 1 + q;
-                    if ((ip == last || fc_s[ip] <= k) && (iq == last || fc_s[iq] <= k)) {
-                        const double* Li = L.tiles[sk * TPS + ((p == wk) ? W + 1 : 1 + p)];
-                        const double* Lj = L.tiles[sk * TPS + ((q == wk) ? W + 1 : 1 + q)];
-                        dst[u] = (ip == last && iq == last)
-                                     ? lastdiag
-                                     : (ip == last ? L.tiles[(iq % (W + 1)) * TPS + W + 1]
-                                                   : L.tiles[(iq % (W + 1)) * TPS + (ip - iq)]);
+            auto tile_of = [&](int it) -> double* { return L.tiles[sk * TPS + ((it == wk) ? W + 1 : 1 + it)]; };
+            if (wave == 0) {
+                if (la) {
+                    const int i1 = k + 1;
+                    double* T11 = L.tiles[(i1 % (W + 1)) * TPS];
+                    if (fc_s[i1] <= k) {
+                        const double* Li = tile_of(0);
+                        d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4)
-                            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[rr * TLD + 4 * s4 + kk],
-                                                                          Lj[rr * TLD + 4 * s4 + kk], acc[u], 0, 0, 0);
+                            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[rr * TLD + 4 * s4 + kk], Li[rr * TLD + 4 * s4 + kk],
+                                                                      acc, 0, 0, 0);
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) T11[(kk + 4 * g) * TLD + rr] -= acc[g];
+                        // rhs row k+1
+                        const int r = lane & 15, part = lane >> 4;
+                        double sacc = 0.0;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) sacc += Li[r * TLD + part * 4 + c] * L.bring[sk][part * 4 + c];
+                        sacc += __shfl_xor(sacc, 16);
+                        sacc += __shfl_xor(sacc, 32);
+                        if (lane < 16) L.bring[i1 % (W + 1)][lane] -= sacc;
+                    }
+                    factor_diag(T11, L.bring[i1 % (W + 1)]);
+                }
+            } else {
+                constexpr int MAXU = ((W + 2) * (W + 1) / 2 + 2) / 3;
+                d4 acc[MAXU];
+                double* dst[MAXU];
+#pragma unroll
+                for (int u = 0; u < MAXU; ++u) {
+                    acc[u] = d4{0.0, 0.0, 0.0, 0.0};
+                    dst[u] = nullptr;
+                    const int t = (wave - 1) + 3 * u + (la ? 1 : 0);  // skip pair 0 = (k+1,k+1) under look-ahead
+                    if (t < npairs) {
+                        int p = 0, rem = t;
+                        while (rem > p) { rem -= p + 1; ++p; }
+                        const int q = rem;
+                        const int ip = (p == wk) ? last : k + 1 + p;
+                        const int iq = (q == wk) ? last : k + 1 + q;
+                        if ((ip == last || fc_s[ip] <= k) && (iq == last || fc_s[iq] <= k)) {
+                            const double* Li = tile_of(p);
+                            const double* Lj = tile_of(q);
+                            dst[u] = (ip == last && iq == last)
+                                         ? lastdiag
+                                         : (ip == last ? L.tiles[(iq % (W + 1)) * TPS + W + 1]
+                                                       : L.tiles[(iq % (W + 1)) * TPS + (ip - iq)]);
+#pragma unroll
+                            for (int s4 = 0; s4 < 4; ++s4)
+                                acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[rr * TLD + 4 * s4 + kk],
+                                                                              Lj[rr * TLD + 4 * s4 + kk], acc[u], 0, 0, 0);
+                        }
                     }
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < MAXU; ++u)
-                if (dst[u])
+                for (int u = 0; u < MAXU; ++u)
+                    if (dst[u])
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) dst[u][(kk + 4 * g) * TLD + rr] -= acc[u][g];
-            // rhs: b_i -= L_ik z_k ; one wave per tile row-block (16 lanes x 4 partial sums)
-            for (int it = wave; it < nr; it += 4) {
-                const int i = (it == wk) ? last : k + 1 + it;
-                if (i != last && fc_s[i] > k) continue;
-                const double* Li = L.tiles[sk * TPS + ((it == wk) ? W + 1 : 1 + it)];
-                const int r = lane & 15, part = lane >> 4;
-                double sacc = 0.0;
+                        for (int g = 0; g < 4; ++g) dst[u][(kk + 4 * g) * TLD + rr] -= acc[u][g];
+                // rhs rows other than k+1
+                for (int it = (la ? 1 : 0) + (wave - 1); it < nr; it += 3) {
+                    const int i = (it == wk) ? last : k + 1 + it;
+                    if (i != last && fc_s[i] > k) continue;
+                    const double* Li = tile_of(it);
+                    const int r = lane & 15, part = lane >> 4;
+                    double sacc = 0.0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) sacc += Li[r * TLD + part * 4 + c] * L.bring[sk][part * 4 + c];
-                sacc += __shfl_xor(sacc, 16);
-                sacc += __shfl_xor(sacc, 32);
-                if (lane < 16) {
-                    if (it == wk) L.blast[lane] -= sacc; else L.bring[i % (W + 1)][lane] -= sacc;
+                    for (int c = 0; c < 4; ++c) sacc += Li[r * TLD + part * 4 + c] * L.bring[sk][part * 4 + c];
+                    sacc += __shfl_xor(sacc, 16);
+                    sacc += __shfl_xor(sacc, 32);
+                    if (lane < 16) {
+                        if (it == wk) L.blast[lane] -= sacc; else L.bring[i % (W + 1)][lane] -= sacc;
+                    }
                 }
             }
         }
         __syncthreads();
         STAMP_AT(2)
-        // ---- 4. retire column k to global (L and z), install the prefetched column kn
+        // ---- 3. retire column k to global (L and z), install the prefetched column kn
         for (int bti = 0; bti <= wk; ++bti) {
             const int i = k + bti;
             A[((size_t)i * 16 + er) * ld + (size_t)k * 16 + ec] = L.tiles[sk * TPS + bti][er * TLD + ec];
@@ -1115,12 +1169,14 @@ __global__ __launch_bounds__(TPB) void k_chol_band(double* __restrict__ A, int n
 // ---------------------------------------------------------------- update
 // delta = -s * y over cameras and intrinsics; candidate poses; prior-block model
 // change and candidate prior cost. part[PART_UPD_* * stride + block]
-__global__ void k_update_cams(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+__global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restrict__ st, const double* __restrict__ scale,
                               const double* __restrict__ y, double* __restrict__ delta, double* __restrict__ part) {
-    __shared__ double lds[4 * 3];
-    __shared__ double out[3];
+    __shared__ double lds[4 * 4];
+    __shared__ double out[4];
+    if (st->done) return;
+    const int cur = st->cur;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    double acc[3] = {0.0, 0.0, 0.0};  // sn2, mcc, cand cost
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
     if (t < P.nac) {
         const int cam = P.ac_cam[t];
         double d[6];
@@ -1138,6 +1194,7 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, int cur, const double* _
             xn[j] = tp[j];
             const double df = x[j] - tp[j];
             acc[0] += df * df;
+            acc[3] += tp[j] * tp[j];
         }
     } else if (t == P.nac) {
         const double* K = P.K[cur];
@@ -1154,25 +1211,30 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, int cur, const double* _
             acc[1] += -jd * (fk + jd / 2.0);
             const double fn = c.sw_k * (P.prior[m] - kn);
             acc[2] += 0.5 * fn * fn;
+            acc[3] += kn * kn;
         }
     }
-    block_sum<3>(acc, lds, out);
+    block_sum<4>(acc, lds, out);
     if (threadIdx.x == 0) {
         part[PART_UPD_SN2 * P.part_stride + blockIdx.x] = out[0];
         part[PART_UPD_MCC * P.part_stride + blockIdx.x] = out[1];
         part[PART_UPD_COST * P.part_stride + blockIdx.x] = out[2];
+        part[PART_UPD_XN2 * P.part_stride + blockIdx.x] = out[3];
     }
 }
 
 // Back-substitution y_p = V^-1 (e - sum W^T y_c - Kt^T y_k), delta_p = -s_p y_p,
 // model cost change over the point's observations and the candidate cost.
-__global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, int cur, const double* __restrict__ scale,
+__global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                      const double* __restrict__ scale,
                                                       const double* __restrict__ pdata, const double* __restrict__ y,
                                                       const double* __restrict__ delta, double* __restrict__ part) {
-    __shared__ double lds[4 * 4];
-    __shared__ double out[4];
+    __shared__ double lds[4 * 5];
+    __shared__ double out[5];
+    if (st->done) return;
+    const int cur = st->cur;
     const int ap = blockIdx.x * TPB + threadIdx.x;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cost, bad
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cost, bad, |x_cand|^2
     if (ap < P.n_ap) {
         const int pi = P.pt_idx[ap];
         const double* X = P.pts[cur] + 3 * pi;
@@ -1219,6 +1281,7 @@ __global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, 
             Xn[i] = xn[i];
             const double df = X[i] - xn[i];
             acc[0] += df * df;
+            acc[4] += xn[i] * xn[i];
         }
         const double* dk = delta + P.kb;
         for (int o = o0; o < o1; ++o) {
@@ -1246,45 +1309,50 @@ __global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, 
         }
         if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
     }
-    block_sum<4>(acc, lds, out);
+    block_sum<5>(acc, lds, out);
     if (threadIdx.x == 0) {
         part[PART_BS_SN2 * P.part_stride + blockIdx.x] = out[0];
         part[PART_BS_MCC * P.part_stride + blockIdx.x] = out[1];
         part[PART_BS_COST * P.part_stride + blockIdx.x] = out[2];
         part[PART_BS_BAD * P.part_stride + blockIdx.x] = out[3];
+        part[PART_BS_XN2 * P.part_stride + blockIdx.x] = out[4];
     }
 }
 
 // ---------------------------------------------------------------- final
 // scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]
-__global__ __launch_bounds__(TPB) void k_final(DevProblem P, int nblk_pt, int nblk_upd, int nblk_bs,
-                                               const double* __restrict__ part, const int* __restrict__ chol_flag,
-                                               double* __restrict__ scal) {
-    __shared__ double lds[4 * 3];
-    __shared__ double out[3];
+__global__ __launch_bounds__(TPB) void k_final(DevProblem P, const LmState* __restrict__ st, int nblk_pt, int nblk_upd,
+                                               int nblk_bs, const double* __restrict__ part,
+                                               const int* __restrict__ chol_flag, double* __restrict__ scal) {
+    __shared__ double lds[4 * 4];
+    __shared__ double out[4];
     __shared__ double red[4];
-    double acc[3] = {0.0, 0.0, 0.0};
+    if (st->done) return;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double gm = 0.0, bad = 0.0;
-    const size_t st = P.part_stride;
+    const size_t stp = P.part_stride;
     for (int i = threadIdx.x; i < nblk_upd; i += TPB) {
-        acc[0] += part[PART_UPD_SN2 * st + i];
-        acc[1] += part[PART_UPD_MCC * st + i];
-        acc[2] += part[PART_UPD_COST * st + i];
+        acc[0] += part[PART_UPD_SN2 * stp + i];
+        acc[1] += part[PART_UPD_MCC * stp + i];
+        acc[2] += part[PART_UPD_COST * stp + i];
+        acc[3] += part[PART_UPD_XN2 * stp + i];
     }
     for (int i = threadIdx.x; i < nblk_bs; i += TPB) {
-        acc[0] += part[PART_BS_SN2 * st + i];
-        acc[1] += part[PART_BS_MCC * st + i];
-        acc[2] += part[PART_BS_COST * st + i];
-        bad = fmax(bad, part[PART_BS_BAD * st + i]);
+        acc[0] += part[PART_BS_SN2 * stp + i];
+        acc[1] += part[PART_BS_MCC * stp + i];
+        acc[2] += part[PART_BS_COST * stp + i];
+        acc[3] += part[PART_BS_XN2 * stp + i];
+        bad = fmax(bad, part[PART_BS_BAD * stp + i]);
     }
     for (int i = threadIdx.x; i < nblk_pt; i += TPB) {
-        gm = fmax(gm, part[PART_PT_GMAX * st + i]);
-        bad = fmax(bad, 2.0 * part[PART_PT_BAD * st + i]);
+        gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
+        bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
     }
-    block_sum<3>(acc, lds, out);
+    block_sum<4>(acc, lds, out);
     gm = block_max(gm, red);
     bad = block_max(bad, red);
     if (threadIdx.x == 0) {
+        scal[SC_XN2] = out[3];
         scal[SC_SN2] = out[0];
         scal[SC_MCC] = out[1];
         scal[SC_CAND] = out[2];
@@ -1293,10 +1361,142 @@ __global__ __launch_bounds__(TPB) void k_final(DevProblem P, int nblk_pt, int nb
     }
 }
 
+// ---------------------------------------------------------------- LM control
+// |x|^2 of the active parameter blocks (ambient) -> initial state; called once after
+// the iteration-0 linearisation (lin[0] = cost, lin[1] = gmax of cams+intrinsics).
+__global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* __restrict__ lin,
+                                                    LmState* __restrict__ st, double* __restrict__ log) {
+    __shared__ double lds[4];
+    __shared__ double out[1];
+    const int cur = st->cur;
+    double a[1] = {0.0};
+    for (int t = threadIdx.x; t < P.nac; t += TPB) {
+        const double* x = P.cams[cur] + 7 * P.ac_cam[t];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) a[0] += x[j] * x[j];
+    }
+    for (int t = threadIdx.x; t < P.n_ap; t += TPB) {
+        const double* x = P.pts[cur] + 3 * P.pt_idx[t];
+        a[0] += x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
+    }
+    block_sum<1>(a, lds, out);
+    if (threadIdx.x == 0) {
+        const double* K = P.K[cur];
+        st->xnorm2 = out[0] + K[0] * K[0] + K[1] * K[1] + K[2] * K[2] + K[3] * K[3];
+        st->x_cost = lin[0];
+        st->initial_cost = lin[0];
+        st->final_cost = lin[0];
+        st->gmax_ci = lin[1];
+        log[0] = lin[0];
+        log[1] = 0.0;
+        log[3] = 0.0;
+        log[4] = 0.0;
+        log[5] = st->radius;
+        log[6] = 1.0;
+        if (!isfinite(lin[0])) {
+            st->done = 1;
+            st->termination = 2;  // FAILURE
+            st->msg = MSG_EVAL_FAIL;
+        }
+    }
+}
+
+// One thread: Ceres 2.0 TrustRegionMinimizer::Minimize bookkeeping for the step whose
+// scalars k_final produced (model cost change, candidate cost, |step|, |x_cand|, flags).
+// Same decisions, in the same order, as oracle_solve() (oracle/ba_oracle.c).
+__global__ void k_lm_decide(LmState* __restrict__ st, LmParams prm, const double* __restrict__ lin,
+                            const double* __restrict__ scal, double* __restrict__ log) {
+    if (threadIdx.x != 0) return;
+    LmState S = *st;
+    if (S.done) return;
+    if (S.need_lin) {  // absorb the re-linearisation of the last accepted point
+        S.need_lin = 0;
+        S.x_cost = lin[0];
+        S.gmax_ci = lin[1];
+        log[S.iter * LOG_W + 0] = S.x_cost;
+        if (!isfinite(S.x_cost)) {
+            S.done = 1; S.termination = 2; S.msg = MSG_EVAL_FAIL;
+            *st = S;
+            return;
+        }
+        S.final_cost = fmin(S.final_cost, S.x_cost);
+    }
+    const double gmax = fmax(S.gmax_ci, scal[SC_GMAX_PT]);
+    log[S.iter * LOG_W + 2] = gmax;
+    // FinalizeIterationAndCheckIfMinimizerCanContinue
+    if (S.iter >= prm.max_iter) {
+        S.done = 1; S.termination = 1; S.msg = MSG_MAX_ITER; S.msg_a = S.iter;
+    } else if (S.step_ok && gmax <= prm.gradient_tolerance) {
+        S.done = 1; S.termination = 0; S.msg = MSG_GRAD_TOL; S.msg_a = gmax; S.msg_b = prm.gradient_tolerance;
+    } else if (S.radius <= prm.min_radius) {
+        S.done = 1; S.termination = 0; S.msg = MSG_MIN_RADIUS; S.msg_a = S.radius; S.msg_b = prm.min_radius;
+    }
+    if (S.done) { *st = S; return; }
+    S.iter += 1;
+    double* lg = log + S.iter * LOG_W;
+    const double mcc = scal[SC_MCC];
+    const bool lsf = scal[SC_BAD] >= 2.0;  // linear solver failure (point block or Cholesky not PD)
+    const bool valid = !lsf && isfinite(mcc) && mcc > 0.0;
+    if (!valid) {  // HandleInvalidStep
+        S.n_unsucc += 1;
+        if (++S.n_invalid >= prm.max_invalid) {
+            S.done = 1; S.termination = 2; S.msg = MSG_INVALID; S.msg_a = prm.max_invalid;
+        } else {
+            S.radius /= S.decrease_factor;
+            S.decrease_factor *= 2.0;
+            S.step_ok = 0;
+        }
+        lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
+        *st = S;
+        return;
+    }
+    S.n_invalid = 0;
+    double cand = scal[SC_CAND];
+    if (scal[SC_BAD] >= 1.0 || !isfinite(cand)) cand = DBL_MAX;
+    const double step_norm = sqrt(scal[SC_SN2]);
+    const double xnorm = sqrt(S.xnorm2);
+    const double cost_change = S.x_cost - cand;
+    if (step_norm <= prm.parameter_tolerance * (xnorm + prm.parameter_tolerance)) {
+        S.done = 1; S.termination = 0; S.msg = MSG_PARAM_TOL;
+        S.msg_a = step_norm / (xnorm + prm.parameter_tolerance); S.msg_b = prm.parameter_tolerance;
+    } else if (fabs(cost_change) <= prm.function_tolerance * S.x_cost) {
+        S.done = 1; S.termination = 0; S.msg = MSG_FUNC_TOL;
+        S.msg_a = fabs(cost_change) / S.x_cost; S.msg_b = prm.function_tolerance;
+    }
+    if (S.done) {
+        lg[0] = cand; lg[1] = cost_change; lg[3] = step_norm; lg[4] = 0.0; lg[5] = S.radius; lg[6] = -1.0;
+        *st = S;
+        return;
+    }
+    const double rho = (cand >= DBL_MAX) ? -DBL_MAX : cost_change / mcc;
+    if (rho > prm.min_relative_decrease) {  // HandleSuccessfulStep + LM StepAccepted
+        S.cur ^= 1;
+        S.need_lin = 1;
+        S.xnorm2 = scal[SC_XN2];
+        const double t = 2.0 * rho - 1.0;
+        S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - t * t * t);
+        S.radius = fmin(prm.max_radius, S.radius);
+        S.decrease_factor = 2.0;
+        S.step_ok = 1;
+        S.n_succ += 1;
+        lg[0] = cand; lg[6] = 1.0;  // cost re-evaluated at absorb time
+    } else {  // HandleUnsuccessfulStep + LM StepRejected
+        S.radius /= S.decrease_factor;
+        S.decrease_factor *= 2.0;
+        S.step_ok = 0;
+        S.n_unsucc += 1;
+        S.final_cost = fmin(S.final_cost, cand);
+        lg[0] = cand; lg[6] = 0.0;
+    }
+    lg[1] = cost_change; lg[3] = step_norm; lg[4] = rho; lg[5] = S.radius;
+    *st = S;
+}
+
 // ---------------------------------------------------------------- debug hook
 // Per admissible observation (point-major order) residual + Jacobians, for the parity tests.
-__global__ void k_debug_lin(DevProblem P, BaConsts c, int cur, double* __restrict__ res, double* __restrict__ jcam,
-                            double* __restrict__ jpt, double* __restrict__ jint) {
+__global__ void k_debug_lin(DevProblem P, BaConsts c, const LmState* __restrict__ st, double* __restrict__ res,
+                            double* __restrict__ jcam, double* __restrict__ jpt, double* __restrict__ jint) {
+    const int cur = st->cur;
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= P.n_adm) return;
     const int ap = P.po_ap[a];
@@ -1328,37 +1528,41 @@ static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
         CK(hipGetLastError());              \
     } while (0)
 
-hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf) {
-    if (P.n_seg > 0) PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, cur, W.camdata, W.seg_intr);
-    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, cur, W.camdata, W.seg_intr, W.lin);
+hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
+    if (P.n_seg > 0)
+        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr);
+    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin);
     return hipSuccess;
 }
 
-hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int cur, int jacobi, DevWork& W, hipStream_t s,
-                        Prof* pf) {
+hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf) {
     if (P.n_ap > 0)
-        PL(K_POINT_COLNORM, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, cur, 0, 1.0, W.scale,
-           W.cnp, W.pdata, W.S, W.rhs, W.part);
+        PL(K_POINT_COLNORM, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, W.st, 0, W.scale, W.cnp,
+           W.pdata, W.S, W.rhs, W.part);
     const int nt = 6 * P.nac + 3 * P.n_ap + 4;
     PL(K_SCALE, k_scale, dim3(nblocks(nt, TPB)), dim3(TPB), 0, s, P, W.camdata, W.cnp, W.lin, jacobi, W.scale);
     return hipSuccess;
 }
 
-hipError_t launch_build(const DevProblem& P, const BaConsts& c, int cur, double radius, DevWork& W, hipStream_t s,
-                        Prof* pf) {
+hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
+    PL(K_XNORM, k_xnorm_init, dim3(1), dim3(TPB), 0, s, P, W.lin, W.st, W.log);
+    return hipSuccess;
+}
+
+hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
     if (pf) pf->begin(K_MEMSET_S, s);
     CK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
     CK(hipMemsetAsync(W.chol_flag, 0, sizeof(int), s));
     if (pf) pf->end(s);
-    PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, radius, W.camdata, W.lin, W.scale,
+    PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, W.st, W.camdata, W.lin, W.scale,
        W.S, W.rhs);
     if (P.n_ap > 0)
-        PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, cur, 1, radius, W.scale,
-           W.cnp, W.pdata, W.S, W.rhs, W.part);
+        PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, W.st, 1, W.scale, W.cnp,
+           W.pdata, W.S, W.rhs, W.part);
     if (P.n_tiles > 0)
-        PL(K_SCHUR_TILE, k_schur_tile, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata, W.S, W.rhs);
+        PL(K_SCHUR_TILE, k_schur_tile, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs);
     if (P.n_ovf_obs > 0)
-        PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata,
+        PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata,
            W.S, W.rhs);
     return hipSuccess;
 }
@@ -1378,16 +1582,16 @@ static hipError_t launch_band(const DevProblem& P, DevWork& W, hipStream_t s, Pr
     if (stamp_mode == 1) {
         static unsigned long long* dst = nullptr;
         if (!dst) CK(hipMalloc(&dst, 8 * sizeof(unsigned long long)));
-        PL(K_CHOL, (k_chol_band<BW, true>), dim3(1), dim3(TPB), lds, s, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
+        PL(K_CHOL, (k_chol_band<BW, true>), dim3(1), dim3(TPB), lds, s, W.st, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
            W.chol_flag, dst);
         unsigned long long h[8];
         CK(hipMemcpyAsync(h, dst, sizeof(h[0]) * 5, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
-        fprintf(stderr, "chol_band<%d> nb=%d cycles: potrf %llu trsm %llu update %llu retire %llu backward %llu\n", BW,
+        fprintf(stderr, "chol_band<%d> nb=%d cycles: pre %llu trsm %llu update+lookahead %llu retire %llu backward %llu\n", BW,
                 P.npad / 16, h[0], h[1], h[2], h[3], h[4]);
         return hipSuccess;
     }
-    PL(K_CHOL, (k_chol_band<BW, false>), dim3(1), dim3(TPB), lds, s, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
+    PL(K_CHOL, (k_chol_band<BW, false>), dim3(1), dim3(TPB), lds, s, W.st, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
        W.chol_flag, (unsigned long long*)nullptr);
     return hipSuccess;
 }
@@ -1402,27 +1606,32 @@ hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* p
         case 6: return launch_band<6>(P, W, s, pf);
         default: break;
     }
-    PL(K_CHOL, k_chol, dim3(1), dim3(TPB), 0, s, W.S, P.npad, P.npad / 16, W.fcol, W.rptr, W.rows, W.rhs,
+    PL(K_CHOL, k_chol, dim3(1), dim3(TPB), 0, s, W.st, W.S, P.npad, P.npad / 16, W.fcol, W.rptr, W.rows, W.rhs,
        W.chol_flag);
     return hipSuccess;
 }
 
-hipError_t launch_update(const DevProblem& P, const BaConsts& c, int cur, DevWork& W, hipStream_t s, Prof* pf) {
+hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
     const int nb_upd = nblocks(P.nac + 1, TPB);
-    PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, cur, W.scale, W.rhs, W.delta, W.part);
+    PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.rhs, W.delta, W.part);
     const int nb_bs = nblocks(P.n_ap, TPB);
     if (P.n_ap > 0)
-        PL(K_BACKSUB_EVAL, k_backsub_eval, dim3(nb_bs), dim3(TPB), 0, s, P, c, cur, W.scale, W.pdata, W.rhs, W.delta,
+        PL(K_BACKSUB_EVAL, k_backsub_eval, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part);
-    PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0, nb_upd,
+    PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, W.st, P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0, nb_upd,
        P.n_ap > 0 ? nb_bs : 0, W.part, W.chol_flag, W.scal);
     return hipSuccess;
 }
 
-hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, int cur, double* res, double* jc, double* jp,
+hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf) {
+    PL(K_DECIDE, k_lm_decide, dim3(1), dim3(64), 0, s, W.st, prm, W.lin, W.scal, W.log);
+    return hipSuccess;
+}
+
+hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s) {
     if (P.n_adm > 0)
-        hipLaunchKernelGGL(k_debug_lin, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, cur, res, jc, jp, jk);
+        hipLaunchKernelGGL(k_debug_lin, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, W.st, res, jc, jp, jk);
     return hipGetLastError();
 }
 

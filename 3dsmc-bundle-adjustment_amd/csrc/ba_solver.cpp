@@ -57,7 +57,7 @@ enum BufId {
     B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_FCOL, B_RPTR, B_ROWS, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3,
     B_COUNT
 };
@@ -441,6 +441,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
     HIPCHECK(ctx, ctx->buf[B_SCAL].ensure(sizeof(double) * SC_N));
     HIPCHECK(ctx, ctx->buf[B_FLAG].ensure(sizeof(int) * 4));
+    HIPCHECK(ctx, ctx->buf[B_STATE].ensure(sizeof(LmState)));
+    HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (std::max(o.max_num_iterations, 0) + 2)));
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * part_stride, s));
 
     DevProblem& P = ctx->P;
@@ -475,6 +477,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     W.delta = ctx->buf[B_DELTA].as<double>(); W.part = ctx->buf[B_PART].as<double>();
     W.scal = ctx->buf[B_SCAL].as<double>(); W.chol_flag = ctx->buf[B_FLAG].as<int>();
     W.fcol = ctx->buf[B_FCOL].as<int>(); W.rptr = ctx->buf[B_RPTR].as<int>(); W.rows = ctx->buf[B_ROWS].as<int>();
+    W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
     BaConsts& C = ctx->C;
     const double N = (double)n_adm;
     C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
@@ -519,6 +522,30 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
     }
     return BA_OK;
+}
+
+// Fresh LM state (Ceres IterationZero): radius = initial_trust_region_radius.
+static LmState fresh_state(const ba_options& o, double radius) {
+    LmState st{};
+    st.radius = radius;
+    st.decrease_factor = 2.0;
+    st.n_succ = 1;  // iteration 0 counts as successful (Ceres convention)
+    st.step_ok = 1;
+    st.termination = -1;
+    return st;
+}
+
+static void format_message(const LmState& S, char* out, size_t n) {
+    switch (S.msg) {
+        case MSG_MAX_ITER: std::snprintf(out, n, "Maximum number of iterations reached. Number of iterations: %d.", (int)S.msg_a); break;
+        case MSG_GRAD_TOL: std::snprintf(out, n, "Gradient tolerance reached. Gradient max norm: %e <= %e", S.msg_a, S.msg_b); break;
+        case MSG_MIN_RADIUS: std::snprintf(out, n, "Minimum trust region radius reached. Trust region radius: %e <= %e", S.msg_a, S.msg_b); break;
+        case MSG_PARAM_TOL: std::snprintf(out, n, "Parameter tolerance reached. Relative step_norm: %e <= %e.", S.msg_a, S.msg_b); break;
+        case MSG_FUNC_TOL: std::snprintf(out, n, "Function tolerance reached. |cost_change|/cost: %e <= %e", S.msg_a, S.msg_b); break;
+        case MSG_INVALID: std::snprintf(out, n, "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d", (int)S.msg_a); break;
+        case MSG_EVAL_FAIL: std::snprintf(out, n, "Residual and Jacobian evaluation failed."); break;
+        default: std::snprintf(out, n, "unknown"); break;
+    }
 }
 
 static void print_header() {
@@ -577,6 +604,12 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     HIPCHECK(ctx, hipMemcpyAsync(P.pts[1], ctx->buf[B_PTS_INIT].p, sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToDevice, s));
     HIPCHECK(ctx, hipMemcpyAsync(P.K[0], ctx->buf[B_K_INIT].p, sizeof(double) * 4, hipMemcpyDeviceToDevice, s));
     HIPCHECK(ctx, hipMemcpyAsync(P.K[1], ctx->buf[B_K_INIT].p, sizeof(double) * 4, hipMemcpyDeviceToDevice, s));
+    const int max_iter = std::max(o.max_num_iterations, 0);
+    HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (max_iter + 2)));
+    W.log = ctx->buf[B_LOG].as<double>();
+    static thread_local LmState h_state;  // host staging (outlives the async copies)
+    h_state = fresh_state(o, o.initial_trust_region_radius);
+    HIPCHECK(ctx, hipMemcpyAsync(W.st, &h_state, sizeof(LmState), hipMemcpyHostToDevice, s));
     sum->num_obs_admissible = P.n_adm;
     sum->num_active_cams = P.nac;
     sum->num_active_points = P.n_ap;
@@ -584,168 +617,64 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     HIPCHECK(ctx, hipStreamSynchronize(s));
     const double tl0 = now_ms();
     sum->time_setup_ms = tl0 - t0;
+    double kms0[K_COUNT];
+    std::memcpy(kms0, ctx->k_ms, sizeof(kms0));
 
-    int cur = 0;
-    double lin_h[LIN_N], scal_h[SC_N];
-    // IterationZero: evaluate cost, gradient, Jacobian column norms -> Jacobi scale
-    HIPCHECK(ctx, launch_linearize(P, C, cur, W, s, pf));
-    HIPCHECK(ctx, launch_scale(P, C, cur, o.jacobi_scaling, W, s, pf));
-    HIPCHECK(ctx, hipMemcpyAsync(lin_h, W.lin, sizeof(lin_h), hipMemcpyDeviceToHost, s));
-    HIPCHECK(ctx, hipStreamSynchronize(s));
-    flush_prof(ctx);
-    double x_cost = lin_h[0];
-    sum->initial_cost = x_cost;
-    if (!std::isfinite(x_cost)) {
-        sum->termination_type = BA_FAILURE;
-        sum->final_cost = x_cost;
-        std::snprintf(sum->message, sizeof(sum->message), "Residual and Jacobian evaluation failed.");
-        sum->time_total_ms = now_ms() - t0;
-        return BA_OK;
-    }
-    double gmax_ci = lin_h[1];
-    double final_cost = x_cost;
-    double radius = o.initial_trust_region_radius;
-    double decrease_factor = 2.0;
-    int iter = 0, n_succ = 1, n_unsucc = 0, n_invalid = 0;
-    bool step_ok = true;
-    double xnorm2 = -1.0;  // ambient |x|^2 of active blocks (computed lazily on host)
-    const bool progress = o.minimizer_progress_to_stdout != 0;
-    double t_lin = 0, t_build = 0, t_fac = 0, t_upd = 0;
-    bool linearized_this_iter = true;  // iteration-0 linearisation precedes the first step
+    LmParams prm;
+    prm.min_relative_decrease = o.min_relative_decrease;
+    prm.max_radius = o.max_trust_region_radius;
+    prm.min_radius = o.min_trust_region_radius;
+    prm.function_tolerance = o.function_tolerance;
+    prm.gradient_tolerance = o.gradient_tolerance;
+    prm.parameter_tolerance = o.parameter_tolerance;
+    prm.max_iter = max_iter;
+    prm.max_invalid = o.max_num_consecutive_invalid_steps;
 
-    // host mirror of the active parameters for |x| (parameter tolerance)
-    auto compute_xnorm2 = [&](int which) -> double {
-        std::vector<double> cams(7 * (size_t)p->n_cams), pts(3 * (size_t)p->n_points), K(4);
-        hipMemcpyAsync(cams.data(), P.cams[which], sizeof(double) * cams.size(), hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(pts.data(), P.pts[which], sizeof(double) * pts.size(), hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(K.data(), P.K[which], sizeof(double) * 4, hipMemcpyDeviceToHost, s);
-        hipStreamSynchronize(s);
-        double acc = 0;
-        for (int c : ctx->ac_cam)
-            for (int j = 0; j < 7; ++j) acc += cams[7 * (size_t)c + j] * cams[7 * (size_t)c + j];
-        for (int i : ctx->pt_idx)
-            for (int j = 0; j < 3; ++j) acc += pts[3 * (size_t)i + j] * pts[3 * (size_t)i + j];
-        for (int j = 0; j < 4; ++j) acc += K[j] * K[j];
-        return acc;
-    };
-    xnorm2 = compute_xnorm2(cur);
-    if (progress) { print_header(); print_row(0, x_cost, 0, gmax_ci, 0, 0, radius, 0, now_ms() - tl0); }
-    double gmax_pt = 0.0;
+    // IterationZero: cost, gradient, column norms -> Jacobi scale, |x|
+    HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
+    HIPCHECK(ctx, launch_scale(P, C, o.jacobi_scaling, W, s, pf));
+    HIPCHECK(ctx, launch_init_state(P, W, s, pf));
+    // LM iterations: fixed launch sequence, device-side decisions; the host only polls
+    // the state once per batch. Iterations enqueued after termination are no-ops.
+    int launched = 0;
+    int batch = 2;
+    LmState& S = h_state;
     for (;;) {
-        if (iter >= o.max_num_iterations) {
-            sum->termination_type = BA_NO_CONVERGENCE;
-            std::snprintf(sum->message, sizeof(sum->message),
-                          "Maximum number of iterations reached. Number of iterations: %d.", iter);
-            break;
+        for (int i = 0; i < batch && launched <= max_iter + 1; ++i, ++launched) {
+            HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
+            HIPCHECK(ctx, launch_build(P, C, W, s, pf));
+            HIPCHECK(ctx, launch_factor(P, W, s, pf));
+            HIPCHECK(ctx, launch_update(P, C, W, s, pf));
+            HIPCHECK(ctx, launch_decide(P, prm, W, s, pf));
         }
-        if (radius <= o.min_trust_region_radius) {
-            sum->termination_type = BA_CONVERGENCE;
-            std::snprintf(sum->message, sizeof(sum->message), "Minimum trust region radius reached. Trust region radius: %e <= %e", radius, o.min_trust_region_radius);
-            break;
-        }
-        const double ti0 = now_ms();
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[1], s));
-        HIPCHECK(ctx, launch_build(P, C, cur, radius, W, s, pf));
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[2], s));
-        HIPCHECK(ctx, launch_factor(P, W, s, pf));
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[3], s));
-        HIPCHECK(ctx, launch_update(P, C, cur, W, s, pf));
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[4], s));
-        HIPCHECK(ctx, hipMemcpyAsync(scal_h, W.scal, sizeof(scal_h), hipMemcpyDeviceToHost, s));
+        HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
         HIPCHECK(ctx, hipStreamSynchronize(s));
         flush_prof(ctx);
-        float ms;
-        if (linearized_this_iter && iter > 0) { hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]); t_lin += ms; }
-        hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]); t_build += ms;
-        hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]); t_fac += ms;
-        hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]); t_upd += ms;
-        gmax_pt = scal_h[SC_GMAX_PT];
-        const double gmax = std::max(gmax_ci, gmax_pt);
-        // FinalizeIteration (of the previous iteration): gradient tolerance
-        if (step_ok && gmax <= o.gradient_tolerance) {
-            sum->termination_type = BA_CONVERGENCE;
-            std::snprintf(sum->message, sizeof(sum->message), "Gradient tolerance reached. Gradient max norm: %e <= %e", gmax, o.gradient_tolerance);
-            break;
-        }
-        ++iter;
-        linearized_this_iter = false;
-        const double mcc = scal_h[SC_MCC];
-        const bool lsf = scal_h[SC_BAD] >= 2.0;  // point V not PD or Cholesky failure
-        const bool valid = !lsf && std::isfinite(mcc) && mcc > 0.0;
-        if (!valid) {
-            if (++n_invalid >= o.max_num_consecutive_invalid_steps) {
-                sum->termination_type = BA_FAILURE;
-                std::snprintf(sum->message, sizeof(sum->message),
-                              "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d",
-                              o.max_num_consecutive_invalid_steps);
-                ++n_unsucc;
-                break;
-            }
-            radius /= decrease_factor;
-            decrease_factor *= 2.0;
-            step_ok = false;
-            ++n_unsucc;
-            if (progress) print_row(iter, x_cost, 0, gmax, 0, 0, radius, now_ms() - ti0, now_ms() - tl0);
-            continue;
-        }
-        n_invalid = 0;
-        double cand = scal_h[SC_CAND];
-        if (scal_h[SC_BAD] >= 1.0 || !std::isfinite(cand)) cand = DBL_MAX;
-        const double step_norm = std::sqrt(scal_h[SC_SN2]);
-        const double xnorm = std::sqrt(xnorm2);
-        if (step_norm <= o.parameter_tolerance * (xnorm + o.parameter_tolerance)) {
-            sum->termination_type = BA_CONVERGENCE;
-            std::snprintf(sum->message, sizeof(sum->message), "Parameter tolerance reached. Relative step_norm: %e <= %e.",
-                          step_norm / (xnorm + o.parameter_tolerance), o.parameter_tolerance);
-            break;
-        }
-        const double cost_change = x_cost - cand;
-        if (std::fabs(cost_change) <= o.function_tolerance * x_cost) {
-            sum->termination_type = BA_CONVERGENCE;
-            std::snprintf(sum->message, sizeof(sum->message), "Function tolerance reached. |cost_change|/cost: %e <= %e",
-                          std::fabs(cost_change) / x_cost, o.function_tolerance);
-            break;
-        }
-        const double rho = (cand >= DBL_MAX) ? -DBL_MAX : (x_cost - cand) / mcc;
-        if (rho > o.min_relative_decrease) {
-            // HandleSuccessfulStep: x = candidate, re-linearise
-            cur ^= 1;
-            HIPCHECK(ctx, hipEventRecord(ctx->ev[0], s));
-            HIPCHECK(ctx, launch_linearize(P, C, cur, W, s, pf));
-            HIPCHECK(ctx, hipMemcpyAsync(lin_h, W.lin, sizeof(lin_h), hipMemcpyDeviceToHost, s));
-            HIPCHECK(ctx, hipStreamSynchronize(s));
-            flush_prof(ctx);
-            linearized_this_iter = true;
-            const double ncost = lin_h[0];
-            if (!std::isfinite(ncost)) {
-                sum->termination_type = BA_FAILURE;
-                std::snprintf(sum->message, sizeof(sum->message), "Residual and Jacobian evaluation failed.");
-                break;
-            }
-            x_cost = ncost;
-            gmax_ci = lin_h[1];
-            xnorm2 = compute_xnorm2(cur);
-            radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3));
-            radius = std::min(o.max_trust_region_radius, radius);
-            decrease_factor = 2.0;
-            step_ok = true;
-            ++n_succ;
-            final_cost = std::min(final_cost, x_cost);
-            if (progress) print_row(iter, x_cost, cost_change, gmax, step_norm, rho, radius, now_ms() - ti0, now_ms() - tl0);
-        } else {
-            radius /= decrease_factor;
-            decrease_factor *= 2.0;
-            step_ok = false;
-            ++n_unsucc;
-            final_cost = std::min(final_cost, cand);
-            if (progress) print_row(iter, cand, cost_change, gmax, step_norm, rho, radius, now_ms() - ti0, now_ms() - tl0);
+        if (S.done || launched > max_iter + 1) break;
+        batch = std::min(batch * 2, 8);
+    }
+    if (!S.done) {  // cannot happen (max_iter bounds the loop); report defensively
+        ctx->err = "LM loop did not terminate";
+        return BA_E_INTERNAL;
+    }
+    sum->initial_cost = S.initial_cost;
+    sum->final_cost = S.final_cost;
+    sum->num_successful_steps = S.n_succ;
+    sum->num_unsuccessful_steps = S.n_unsucc;
+    sum->num_iterations = S.iter;
+    sum->termination_type = S.termination;
+    format_message(S, sum->message, sizeof(sum->message));
+    if (o.minimizer_progress_to_stdout) {
+        std::vector<double> lg((size_t)LOG_W * (S.iter + 1));
+        HIPCHECK(ctx, hipMemcpy(lg.data(), W.log, sizeof(double) * lg.size(), hipMemcpyDeviceToHost));
+        print_header();
+        for (int it = 0; it <= S.iter; ++it) {
+            const double* r = &lg[(size_t)it * LOG_W];
+            print_row(it, r[0], r[1], r[2], r[3], r[4], r[5], 0.0, 0.0);
         }
     }
-    sum->final_cost = final_cost;
-    sum->num_successful_steps = n_succ;
-    sum->num_unsuccessful_steps = n_unsucc;
-    sum->num_iterations = iter;
     // copy the best (= last accepted) parameters back in place
+    const int cur = S.cur;
     HIPCHECK(ctx, hipMemcpyAsync(p->cams, P.cams[cur], sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipMemcpyAsync(p->points, P.pts[cur], sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipMemcpyAsync(p->intr, P.K[cur], sizeof(double) * 4, hipMemcpyDeviceToHost, s));
@@ -753,10 +682,11 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     const double t1 = now_ms();
     sum->time_lm_ms = t1 - tl0;
     sum->time_total_ms = t1 - t0;
-    sum->time_linearize_ms = t_lin;
-    sum->time_schur_ms = t_build;
-    sum->time_factor_ms = t_fac;
-    sum->time_update_ms = t_upd;
+    auto dk = [&](int k) { return ctx->k_ms[k] - kms0[k]; };
+    sum->time_linearize_ms = dk(K_CAM_SIDE) + dk(K_LIN_FINALIZE) + dk(K_POINT_COLNORM) + dk(K_SCALE);
+    sum->time_schur_ms = dk(K_MEMSET_S) + dk(K_ASSEMBLE) + dk(K_POINT_PREP) + dk(K_SCHUR_TILE) + dk(K_OBS_PAIRS);
+    sum->time_factor_ms = dk(K_CHOL);
+    sum->time_update_ms = dk(K_UPDATE_CAMS) + dk(K_BACKSUB_EVAL) + dk(K_FINAL) + dk(K_DECIDE);
     return BA_OK;
 }
 
@@ -773,8 +703,11 @@ extern "C" int32_t ba_debug_linearize(ba_context* ctx, const ba_problem* p, doub
     HIPCHECK(ctx, ctx->buf[B_DBG1].ensure(sizeof(double) * 18 * na));
     HIPCHECK(ctx, ctx->buf[B_DBG2].ensure(sizeof(double) * 9 * na));
     HIPCHECK(ctx, ctx->buf[B_DBG3].ensure(sizeof(double) * 8 * na));
+    static thread_local LmState h_st;
+    h_st = fresh_state(ctx->opts, ctx->opts.initial_trust_region_radius);
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->W.st, &h_st, sizeof(LmState), hipMemcpyHostToDevice, s));
     HIPCHECK(ctx, launch_linearize(P, ctx->C, 0, ctx->W, s, nullptr));
-    HIPCHECK(ctx, launch_debug_lin(P, ctx->C, 0, ctx->buf[B_DBG0].as<double>(), ctx->buf[B_DBG1].as<double>(),
+    HIPCHECK(ctx, launch_debug_lin(P, ctx->C, ctx->W, ctx->buf[B_DBG0].as<double>(), ctx->buf[B_DBG1].as<double>(),
                                    ctx->buf[B_DBG2].as<double>(), ctx->buf[B_DBG3].as<double>(), s));
     std::vector<double> r(3 * na), jc(18 * na), jp(9 * na), jk(8 * na);
     double lin_h[LIN_N];
@@ -811,9 +744,12 @@ extern "C" int32_t ba_debug_reduced_system(ba_context* ctx, const ba_problem* p,
     if (n_out) *n_out = P.n;
     if (!S || !rhs) return BA_OK;
     if (radius <= 0) radius = ctx->opts.initial_trust_region_radius;
+    static thread_local LmState h_st;
+    h_st = fresh_state(ctx->opts, radius);
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->W.st, &h_st, sizeof(LmState), hipMemcpyHostToDevice, s));
     HIPCHECK(ctx, launch_linearize(P, ctx->C, 0, ctx->W, s, nullptr));
-    HIPCHECK(ctx, launch_scale(P, ctx->C, 0, ctx->opts.jacobi_scaling, ctx->W, s, nullptr));
-    HIPCHECK(ctx, launch_build(P, ctx->C, 0, radius, ctx->W, s, nullptr));
+    HIPCHECK(ctx, launch_scale(P, ctx->C, ctx->opts.jacobi_scaling, ctx->W, s, nullptr));
+    HIPCHECK(ctx, launch_build(P, ctx->C, ctx->W, s, nullptr));
     std::vector<double> Sp((size_t)P.npad * P.npad);
     HIPCHECK(ctx, hipMemcpyAsync(Sp.data(), ctx->W.S, sizeof(double) * Sp.size(), hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipMemcpyAsync(rhs, ctx->W.rhs, sizeof(double) * P.n, hipMemcpyDeviceToHost, s));
