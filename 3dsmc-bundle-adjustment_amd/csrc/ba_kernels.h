@@ -74,7 +74,25 @@ struct DevProblem {
     int off_pt, off_k;  // scale-vector offsets
     int part_stride;
     int band_w;  // 16x16 tiles below the diagonal in the camera band; <=0 or >6: dense envelope kernel
+    int cam_band;  // max over active cameras of (camera - first co-visible camera)
+    int solver;    // 0 dense envelope, 1 band, 2 block cyclic reduction
 };
+
+// Block cyclic reduction workspace (ba_bcr.hip): nblk blocks of BCR_CAMS cameras (64 dofs).
+static constexpr int BCR_CAMS = 10;
+// Block cyclic reduction workspace, per 64-dof block i (see ba_bcr.hip):
+//   Cf   Cholesky factor of the block at its elimination      64x64
+//   XL   Cf^-1 A[i][i-s]   XR  Cf^-1 A[i][i+s]                 64x64 each
+//   UL   XL^T XL  (Schur contribution to the left survivor)    64x64 (lower tiles)
+//   UR   XR^T XR  (to the right survivor)                      64x64 (lower tiles)
+//   F    -XR^T XL (fill coupling right survivor -> left one)   64x64
+//   x    Cf^-1 R_i, Y solution, rL = XL^T x, rR = XR^T x        64x8 each
+//   rd   1 / diag(Cf)                                          64
+struct BcrWork {
+    double *Cf, *XL, *XR, *UL, *UR, *F, *x, *Y, *rL, *rR, *rd;
+    int nblk, levels;
+};
+static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)6 * 64 * 64 + 4 * 64 * 8 + 64;
 
 // Device-resident Levenberg-Marquardt state (Ceres 2.0 TrustRegionMinimizer +
 // LevenbergMarquardtStrategy bookkeeping, owned by k_lm_decide).
@@ -111,6 +129,7 @@ struct DevWork {
     int* rows;
     LmState* st;
     double* log;  // [(max_iter + 2) * LOG_W]
+    BcrWork bcr;
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
@@ -146,6 +165,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
 hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s);
 

@@ -1597,7 +1597,8 @@ static hipError_t launch_band(const DevProblem& P, DevWork& W, hipStream_t s, Pr
 }
 
 hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
-    switch (P.band_w) {
+    if (P.solver == 2) return launch_bcr(P, W, W.bcr, s, pf);
+    if (P.solver == 1) switch (P.band_w) {
         case 1: return launch_band<1>(P, W, s, pf);
         case 2: return launch_band<2>(P, W, s, pf);
         case 3: return launch_band<3>(P, W, s, pf);

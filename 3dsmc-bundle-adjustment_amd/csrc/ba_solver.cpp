@@ -57,7 +57,7 @@ enum BufId {
     B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3,
     B_COUNT
 };
@@ -383,6 +383,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         const int first = (r < 6 * nac) ? 6 * fc[r / 6] : 0;
         fcol[r / 16] = std::min(fcol[r / 16], first / 16);
     }
+    int cam_band = 0;
+    for (int a = 0; a < nac; ++a) cam_band = std::max(cam_band, a - fc[a]);
     // band width (in 16-tiles) of the camera part; the last block row is the dense border
     int band_w = 0;
     for (int i = 0; i + 1 < nb; ++i) band_w = std::max(band_w, i - fcol[i]);
@@ -468,7 +470,40 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
     P.part_stride = part_stride;
     P.band_w = (nb >= 2 && nb <= 2048 && band_w <= 6) ? std::max(band_w, 1) : 0;
-    if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.band_w = 0;
+    P.cam_band = cam_band;
+    // reduced-system solver: block cyclic reduction when the camera band fits a 64-dof block
+    // and there are >= 2 blocks; else the banded LDS Cholesky; else the dense envelope kernel.
+    const int bcr_nblk = (nac + BCR_CAMS - 1) / BCR_CAMS;
+    P.solver = (cam_band < BCR_CAMS && bcr_nblk >= 2) ? 2 : (P.band_w > 0 ? 1 : 0);
+    if (const char* e = std::getenv("MIBA_SOLVER")) {
+        if (!std::strcmp(e, "dense")) P.solver = 0;
+        else if (!std::strcmp(e, "band") && P.band_w > 0) P.solver = 1;
+        else if (!std::strcmp(e, "bcr") && cam_band < BCR_CAMS && bcr_nblk >= 2) P.solver = 2;
+    }
+    if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
+    if (P.solver == 2) {
+        const size_t bytes = sizeof(double) * BCR_BLOCK_DOUBLES * bcr_nblk;
+        HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
+        // upper tiles of UL/UR are never written and must read as zero
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
+        double* base = ctx->buf[B_BCR].as<double>();
+        BcrWork& Bw = ctx->W.bcr;
+        Bw.nblk = bcr_nblk;
+        Bw.levels = 0;
+        while ((1 << Bw.levels) < bcr_nblk) ++Bw.levels;
+        const size_t b64 = (size_t)64 * 64 * bcr_nblk, b8 = (size_t)64 * 8 * bcr_nblk;
+        Bw.Cf = base;
+        Bw.XL = Bw.Cf + b64;
+        Bw.XR = Bw.XL + b64;
+        Bw.UL = Bw.XR + b64;
+        Bw.UR = Bw.UL + b64;
+        Bw.F = Bw.UR + b64;
+        Bw.x = Bw.F + b64;
+        Bw.Y = Bw.x + b8;
+        Bw.rL = Bw.Y + b8;
+        Bw.rR = Bw.rL + b8;
+        Bw.rd = Bw.rR + b8;
+    }
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
     W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
@@ -614,6 +649,8 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     sum->num_active_cams = P.nac;
     sum->num_active_points = P.n_ap;
     sum->reduced_system_size = P.n;
+    sum->linear_solver = P.solver;
+    sum->camera_band = P.cam_band;
     HIPCHECK(ctx, hipStreamSynchronize(s));
     const double tl0 = now_ms();
     sum->time_setup_ms = tl0 - t0;

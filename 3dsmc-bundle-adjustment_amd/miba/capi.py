@@ -90,6 +90,8 @@ class BaSummary(C.Structure):
         ("num_active_cams", C.c_int32),
         ("num_active_points", C.c_int32),
         ("reduced_system_size", C.c_int32),
+        ("linear_solver", C.c_int32),
+        ("camera_band", C.c_int32),
         ("time_setup_ms", C.c_double),
         ("time_lm_ms", C.c_double),
         ("time_linearize_ms", C.c_double),

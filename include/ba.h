@@ -106,6 +106,11 @@ typedef struct ba_problem {
 } ba_problem;
 
 /* Result summary (subset of ceres::Solver::Summary + per-phase device timings). */
+/* ba_summary.linear_solver */
+#define BA_LS_DENSE 0 /* dense-envelope LDS Cholesky */
+#define BA_LS_BAND 1  /* banded LDS Cholesky (6x6 block band <= 6) */
+#define BA_LS_BCR 2   /* block cyclic reduction over 64-dof camera blocks */
+
 typedef struct ba_summary {
     double initial_cost;
     double final_cost;
@@ -117,6 +122,8 @@ typedef struct ba_summary {
     int32_t num_active_cams;
     int32_t num_active_points;
     int32_t reduced_system_size;    /* 6*active_cams + 4 */
+    int32_t linear_solver;          /* reduced-system solver used: BA_LS_DENSE / BA_LS_BAND / BA_LS_BCR */
+    int32_t camera_band;            /* max |cam_a - cam_b| over coupled active cameras */
     double time_setup_ms;           /* host prep + H2D + structure build */
     double time_lm_ms;              /* LM loop wall time (device work + host control) */
     double time_linearize_ms;       /* device: camera-side / point-side linearisation */

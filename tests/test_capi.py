@@ -48,13 +48,32 @@ def test_api_version(L):
     assert b"gfx950" in L.ba_build_info()
 
 
-def test_struct_layout():
-    # ba_options: 4 doubles, 2 int32, 7 doubles, 2 int32, 3 doubles, 2 int32, 6 int32
-    assert C.sizeof(BaOptions) == 4 * 8 + 8 + 7 * 8 + 8 + 3 * 8 + 8 + 24
-    from miba.capi import BaKernelStat
-    assert C.sizeof(BaKernelStat) == 32 + 8 + 3 * 8
-    assert C.sizeof(BaProblem) == 16 + 8 * 8
-    assert C.sizeof(BaSummary) == 8 * 2 + 4 * 8 + 8 * 7 + 160
+def _c_layout(struct_name, fields):
+    """sizeof + offsetof of every field, from the real header compiled by gcc."""
+    import subprocess
+    import tempfile
+    lines = [f'printf("%zu\\n", sizeof({struct_name}));']
+    lines += [f'printf("%zu\\n", offsetof({struct_name}, {f}));' for f in fields]
+    src = "#include <stddef.h>\n#include <stdio.h>\n#include \"ba.h\"\nint main(void){" + "".join(lines) + "return 0;}\n"
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "l")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        out = [int(x) for x in subprocess.check_output([exe]).split()]
+    return out[0], out[1:]
+
+
+@pytest.mark.parametrize("cls,cname", [(BaOptions, "ba_options"), (BaProblem, "ba_problem"),
+                                       (BaSummary, "ba_summary"), ("BaKernelStat", "ba_kernel_stat")])
+def test_struct_layout_matches_header(cls, cname):
+    if isinstance(cls, str):
+        from miba import capi
+        cls = getattr(capi, cls)
+    names = [n for n, _ in cls._fields_]
+    size, offs = _c_layout(cname, names)
+    assert C.sizeof(cls) == size
+    assert [getattr(cls, n).offset for n in names] == offs
 
 
 def test_no_device_fails_loudly(L):

@@ -91,15 +91,34 @@ def test_c2_config_final_cost():
     assert sg["num_iterations"] == so["num_iterations"]
 
 
-@pytest.mark.parametrize("dense", ["0", "1"])
-@pytest.mark.parametrize("case", ["banded", "tum_like", "wide_overflow"])
-def test_band_and_dense_cholesky_agree(case, dense, monkeypatch):
-    """The banded LDS Cholesky and the dense-envelope kernel solve the same step."""
+LS = {"dense": 0, "band": 1, "bcr": 2}
+
+
+@pytest.mark.parametrize("ls", sorted(LS))
+@pytest.mark.parametrize("case", ["banded", "tum_like", "shuffled_bad_depth", "wide_overflow"])
+def test_linear_solvers_agree(case, ls, monkeypatch):
+    """Dense-envelope Cholesky, banded Cholesky and block cyclic reduction solve the same
+    reduced camera system: 5 LM iterations match the oracle to 1e-9 whichever runs."""
     from miba.solver import Solver
-    monkeypatch.setenv("MIBA_DENSE_CHOL", dense)
+    monkeypatch.setenv("MIBA_SOLVER", ls)
     p = synthetic.make_problem(**CASES[case])
     q = p.copy()
     with Solver(minimizer_progress_to_stdout=0, max_num_iterations=5) as s:
         sg = s.solve(p)
     so = oracle.solve(q, oracle.default_options(max_num_iterations=5))
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sg, so)
+    assert sg["num_iterations"] == so["num_iterations"]
+    eligible = {"dense": True, "band": sg["camera_band"] <= 6,
+                "bcr": sg["camera_band"] < 10 and sg["num_active_cams"] - 1 > 10}
+    if eligible[ls]:
+        assert sg["linear_solver"] == LS[ls], sg
+
+
+@pytest.mark.parametrize("config", ["C2", "C4"])
+def test_bcr_selected_on_long_windows(config):
+    """Long sliding windows (camera band < 10) take the BCR path by default."""
+    from miba.solver import Solver
+    p = synthetic.make_config(config)
+    with Solver(minimizer_progress_to_stdout=0, max_num_iterations=2) as s:
+        sg = s.solve(p)
+    assert sg["linear_solver"] == LS["bcr"], sg
