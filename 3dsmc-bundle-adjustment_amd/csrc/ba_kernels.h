@@ -14,7 +14,7 @@ static constexpr int SEGINTR = 15;
 static constexpr int PDATA = 21;
 // tiled Schur reduction geometry
 static constexpr int TILE_WIN = 12;    // cameras per tile window
-static constexpr int CHUNK_PTS = 64;   // points per chunk (one 64-bit mask word)
+static constexpr int CHUNK_PTS = 32;   // points per Schur chunk (K = 3 * CHUNK_PTS of the MFMA product)
 static constexpr int CHUNK_OBS = 256;  // observations per chunk (one per thread)
 
 // partial-sum slots (each slot holds part_stride doubles, one per producing block)
@@ -30,6 +30,7 @@ enum {
     PART_BS_BAD,
     PART_UPD_XN2,
     PART_BS_XN2,
+    PART_INIT_XN2,
     PART_NSLOTS
 };
 // final scalars
@@ -49,6 +50,7 @@ struct DevProblem {
     const double2* po_uv;  // pixel
     const double* po_depth;
     const int* po_ap;      // active point index
+    const int* po_pt;      // point index (= pt_idx[po_ap])
     const int* pt_ptr;     // [n_ap+1]
     const int* pt_idx;     // active point -> point index
     // admissible observations grouped by camera (camera-major)

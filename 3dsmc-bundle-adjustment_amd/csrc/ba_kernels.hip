@@ -486,58 +486,124 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, con
     }
 }
 
-// Schur reduction over the TILED points (the common, banded case).
-// One workgroup per tile: a run of points (sorted by first camera) whose active
-// cameras all lie in the window [base, base+span), span <= TILE_WIN. The tile
-// is processed in chunks of <= CHUNK_PTS points / <= CHUNK_OBS observations:
-//   phase A (thread per obs): recompute J, W~ = s_c Jc^T Jp s_p, Z = W~ G^T -> LDS;
-//           (thread per point): Zk = K~ G^T, ze = G e~ -> LDS; camera->points bitmasks
-//   phase B (thread per owner slot, registers): pair half-blocks (ca<=cb, rows 3h..3h+2)
-//           acc += sum_{p in mask[ca]&mask[cb]} Z_a Z_b^T ; border/rhs slots
-//           acc += Z_a Zk^T, Z_a ze
-// and the owner registers are flushed once per tile into S / rhs (f64 atomics:
-// ~span^2*18 adds per tile instead of ~220 per observation).
+// Schur reduction over the TILED points (the common, banded case), on the f64 matrix cores.
+// One workgroup per tile: a run of points (sorted by first camera) whose active cameras
+// all lie in the window [base, base+span), span <= TILE_WIN. For a chunk of <= CHUNK_PTS
+// points the tile's Schur term is a small dense product: with M' the (6 span + 5) x 3 npts
+// matrix whose column (p, j) holds, for every camera c observing p, the rows
+// 6c..6c+5 = Z_(p,c)[:, j] (Z = W~ G^T, zero where c does not observe p), then the
+// 4 rows Zk = K~ G^T and one row ze = G e~,
+//     S_cc -= M'_c M'_c^T,  S_kc -= M'_k M'_c^T,  rhs_c -= M'_c ze.
+// Phase A (thread per observation / per point) writes M' k-major into LDS; phase B: each
+// wave owns up to 4 of the (<= 15) lower 16x16 tiles of M' M'^T and runs 4 independent
+// v_mfma_f64_16x16x4 chains over K = 3 npts, accumulating across chunks in registers.
+// The tile is flushed into S / rhs once (f64 atomics, lower triangle). The intrinsics-
+// intrinsics terms stay in k_point_prep, which also covers the overflow points.
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+typedef double d4 __attribute__((ext_vector_type(4)));
+static constexpr int SCH_K = 3 * CHUNK_PTS;   // K extent of one chunk
+static constexpr int SCH_LDM = 80;            // rows of M' (6 * TILE_WIN + 5 <= 80)
+static_assert(6 * TILE_WIN + 5 <= SCH_LDM, "M' rows exceed 5 MFMA tiles");
+static_assert(CHUNK_OBS <= TPB, "phase A: one observation per thread");
+
+template <bool STAMP>
 __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
-                                                    double* __restrict__ rhs) {
-    __shared__ double Zs[CHUNK_OBS][18];
-    __shared__ double Zk[CHUNK_PTS][12];
-    __shared__ double ze[CHUNK_PTS][3];
-    __shared__ unsigned long long mask[TILE_WIN];
-    __shared__ unsigned char oidx[CHUNK_PTS][TILE_WIN];
+                                                    double* __restrict__ rhs, unsigned long long* __restrict__ stamps) {
+    __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     if (st->done) return;
+    unsigned long long t_prev = 0, st_acc[4] = {0, 0, 0, 0};
+#define SCH_STAMP(k)                                          \
+    do {                                                      \
+        if constexpr (STAMP) {                                \
+            if (threadIdx.x == 0) {                           \
+                const unsigned long long t_ = stamp_now();    \
+                st_acc[k] += t_ - t_prev;                     \
+                t_prev = t_;                                  \
+            }                                                 \
+        }                                                     \
+    } while (0)
+    if constexpr (STAMP) if (threadIdx.x == 0) t_prev = stamp_now();
     const int cur = st->cur;
     const int tile = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rr = lane & 15, kq = lane >> 4;
     const int base = P.tile_base[tile];
     const int span = P.tile_span[tile];
-    const int npair = span * (span + 1);  // half-block slots
-    const int nslot = npair + span;       // + border/rhs slots
-    // owner slot decode
-    int ca = -1, cb = -1, h = 0;
-    const bool pair_slot = tid < npair;
-    if (pair_slot) {
-        int pi = tid >> 1;
-        h = tid & 1;
-        int r = 0;
-        while (pi >= span - r) { pi -= span - r; ++r; }
-        ca = r;
-        cb = r + pi;
-    } else if (tid < nslot) {
-        ca = tid - npair;
-    }
-    double acc[30];
+    const int kr = 6 * span, er = kr + 4;     // intrinsics rows, rhs row of M'
+    const int nrt = (er + 1 + 15) >> 4;        // 16-row tiles of M'
+    const int ntl = nrt * (nrt + 1) / 2;       // lower tiles of M' M'^T
+    // lower tiles in reverse row-major order, 4 consecutive per wave (operand rows shared
+    // within a wave); slots past ntl duplicate tile (0,0) and are never flushed
+    int tib[4], tjb[4];
+    bool tok[4];
 #pragma unroll
-    for (int i = 0; i < 30; ++i) acc[i] = 0.0;
+    for (int q = 0; q < 4; ++q) {
+        const int u = 4 * wave + q;
+        tok[q] = u < ntl;
+        int t = tok[q] ? ntl - 1 - u : 0, ib = 0;
+        while (t > ib) { t -= ib + 1; ++ib; }
+        tib[q] = ib;
+        tjb[q] = t;
+    }
+    d4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
     const double* K = P.K[cur];
-    for (int ch = P.tile_chunk[tile]; ch < P.tile_chunk[tile + 1]; ++ch) {
-        const int apb = P.chunk_ap[ch], ape = P.chunk_ap[ch + 1];
-        const int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
-        if (tid < TILE_WIN) mask[tid] = 0ull;
-        __syncthreads();
-        // ---- phase A
+    // Software pipeline over the tile's chunks: the next chunk's bounds and level-1
+    // observation records are loaded before this chunk's MFMAs, its level-2 operands
+    // (pose, point, scales, G) right after them, so phase A starts with its data resident.
+    const int ch_end = P.tile_chunk[tile + 1];
+    int ch = P.tile_chunk[tile];
+    int apb = P.chunk_ap[ch], ape = P.chunk_ap[ch + 1];
+    int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
+    const int n_last = P.n_adm - 1;
+    // level 1: observation record of this thread
+    int r_ac, r_ap, r_cam, r_pt;
+    double2 r_uv;
+    double r_dep;
+    auto load_rec = [&](int qq) {
+        const int qc = qq < n_last ? qq : n_last;
+        r_ac = P.po_ac[qc]; r_ap = P.po_ap[qc]; r_cam = P.po_cam[qc]; r_pt = P.po_pt[qc];
+        r_uv = P.po_uv[qc]; r_dep = P.po_depth[qc];
+    };
+    // level 2: operands of the observation
+    double o_pose[7], o_X[3], o_sc[6], o_sp[3], o_G[6];
+    bool o_ok = false;
+    auto load_ops = [&](bool ok) {
+        o_ok = ok;
+        const int ac = ok ? r_ac : 0, ap = ok ? r_ap : 0;
+        const double* pose = P.cams[cur] + 7 * (ok ? r_cam : 0);
+        const double* X = P.pts[cur] + 3 * (ok ? r_pt : 0);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) o_pose[k] = pose[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o_X[k] = X[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o_sc[k] = scale[6 * ac + k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o_sp[k] = scale[P.off_pt + 3 * ap + k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o_G[k] = pdata[(size_t)ap * PDATA + k];
+    };
+    load_rec(ob + tid);
+    load_ops(ob + tid < oe && r_ac >= 0);
+    for (;;) {
         const int npts = ape - apb;
+        {
+            double2* M2 = reinterpret_cast<double2*>(Mt);
+            for (int e = tid; e < SCH_K * SCH_LDM / 2; e += TPB) M2[e] = double2{0.0, 0.0};
+        }
+        __syncthreads();
+        SCH_STAMP(0);
+        // ---- phase A
         if (tid < npts) {
             const double* pd = pdata + (size_t)(apb + tid) * PDATA;
             double G[6], Ks[12], es[3], zk[12], z3[3];
@@ -549,90 +615,94 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             for (int i = 0; i < 12; ++i) Ks[i] = pd[9 + i];
             zk_ze(G, Ks, es, zk, z3);
 #pragma unroll
-            for (int i = 0; i < 12; ++i) Zk[tid][i] = zk[i];
+            for (int j = 0; j < 3; ++j) {
+                double* col = Mt + (3 * tid + j) * SCH_LDM;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) ze[tid][i] = z3[i];
+                for (int m = 0; m < 4; ++m) col[kr + m] = zk[m * 3 + j];
+                col[er] = z3[j];
+            }
         }
-        const int q = ob + tid;
-        if (q < oe) {
-            const int ac = P.po_ac[q];
-            if (ac >= 0) {
-                const int ap = P.po_ap[q];
-                const int pl = ap - apb;
-                const double2 uv = P.po_uv[q];
-                ObsEval ev;
-                double jc[18], jp[9], jk[8];
-                lin_obs(c, P.cams[cur] + 7 * P.po_cam[q], P.pts[cur] + 3 * P.pt_idx[ap], K, uv.x, uv.y, P.po_depth[q],
-                        ev, jc, jp, jk);
-                double W[18];
-                w_tilde(jc, jp, scale + 6 * ac, scale + P.off_pt + 3 * ap, W);
-                const double* G = pdata + (size_t)ap * PDATA;
-                const double g00 = G[0], g10 = G[1], g11 = G[2], g20 = G[3], g21 = G[4], g22 = G[5];
+        if (o_ok) {
+            const int pl = r_ap - apb;
+            ObsEval ev;
+            double jc[18], jp[9], jk[8];
+            lin_obs(c, o_pose, o_X, K, r_uv.x, r_uv.y, r_dep, ev, jc, jp, jk);
+            double W[18];
+            w_tilde(jc, jp, o_sc, o_sp, W);
+            const double g00 = o_G[0], g10 = o_G[1], g11 = o_G[2], g20 = o_G[3], g21 = o_G[4], g22 = o_G[5];
+            double* c0 = Mt + (3 * pl) * SCH_LDM + 6 * (r_ac - base);
 #pragma unroll
-                for (int d = 0; d < 6; ++d) {
-                    Zs[tid][d * 3 + 0] = W[d * 3 + 0] * g00;
-                    Zs[tid][d * 3 + 1] = W[d * 3 + 0] * g10 + W[d * 3 + 1] * g11;
-                    Zs[tid][d * 3 + 2] = W[d * 3 + 0] * g20 + W[d * 3 + 1] * g21 + W[d * 3 + 2] * g22;
-                }
-                const int lc = ac - base;
-                oidx[pl][lc] = (unsigned char)tid;
-                atomicOr(&mask[lc], 1ull << pl);
+            for (int d = 0; d < 6; ++d) {
+                c0[d] = W[d * 3 + 0] * g00;
+                c0[SCH_LDM + d] = W[d * 3 + 0] * g10 + W[d * 3 + 1] * g11;
+                c0[2 * SCH_LDM + d] = W[d * 3 + 0] * g20 + W[d * 3 + 1] * g21 + W[d * 3 + 2] * g22;
             }
         }
         __syncthreads();
-        // ---- phase B
-        if (pair_slot) {
-            unsigned long long m = mask[ca] & mask[cb];
-            while (m) {
-                const int p = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const double* za = Zs[oidx[p][ca]] + 9 * h;  // rows 3h..3h+2 of Z_a
-                const double* zb = Zs[oidx[p][cb]];
+        SCH_STAMP(1);
+        // ---- prefetch: next chunk bounds + level-1 records
+        const bool more = ch + 1 < ch_end;
+        int ape_n = ape;
+        if (more) {
+            ape_n = P.chunk_ap[ch + 2];
+            load_rec(oe + tid);
+        }
+        // ---- phase B: acc[t] += M'[16 ib..][k] M'[16 jb..][k]^T over the chunk's K
+        const int ksteps = (3 * npts + 3) >> 2;
+        {
+            const double* row = Mt + kq * SCH_LDM + rr;
+            double a[4], b[4];
 #pragma unroll
-                for (int r = 0; r < 3; ++r) {
-                    const double a0 = za[r * 3 + 0], a1 = za[r * 3 + 1], a2 = za[r * 3 + 2];
+            for (int t = 0; t < 4; ++t) { a[t] = row[16 * tib[t]]; b[t] = row[16 * tjb[t]]; }
+            for (int s4 = 0; s4 < ksteps; ++s4) {
+                double an[4], bn[4];
+                const double* nrow = row + (s4 + 1 < ksteps ? 4 * SCH_LDM : 0);
 #pragma unroll
-                    for (int e = 0; e < 6; ++e) acc[r * 6 + e] += a0 * zb[e * 3 + 0] + a1 * zb[e * 3 + 1] + a2 * zb[e * 3 + 2];
-                }
-            }
-        } else if (ca >= 0) {
-            unsigned long long m = mask[ca];
-            while (m) {
-                const int p = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const double* za = Zs[oidx[p][ca]];
+                for (int t = 0; t < 4; ++t) { an[t] = nrow[16 * tib[t]]; bn[t] = nrow[16 * tjb[t]]; }
 #pragma unroll
-                for (int r = 0; r < 6; ++r) {
-                    const double a0 = za[r * 3 + 0], a1 = za[r * 3 + 1], a2 = za[r * 3 + 2];
+                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
 #pragma unroll
-                    for (int mm = 0; mm < 4; ++mm)
-                        acc[r * 4 + mm] += a0 * Zk[p][mm * 3 + 0] + a1 * Zk[p][mm * 3 + 1] + a2 * Zk[p][mm * 3 + 2];
-                    acc[24 + r] += a0 * ze[p][0] + a1 * ze[p][1] + a2 * ze[p][2];
-                }
+                for (int t = 0; t < 4; ++t) { a[t] = an[t]; b[t] = bn[t]; }
+                row = nrow;
             }
         }
+        if (!more) break;
+        // ---- prefetch: level-2 operands of the next chunk
+        const int oe_n = P.pt_ptr[ape_n];
+        load_ops(oe + tid < oe_n && r_ac >= 0);
+        ++ch;
+        apb = ape; ape = ape_n;
+        ob = oe; oe = oe_n;
         __syncthreads();
+        SCH_STAMP(2);
     }
-    // ---- flush (lower triangle of S, row-major npad)
+    __syncthreads();
+    SCH_STAMP(2);
+    // ---- flush (lower triangle of S, row-major npad); C/D layout row = kq + 4g, col = rr
     const size_t ld = P.npad;
-    if (pair_slot) {
-        const int gca = 6 * (base + ca), gcb = 6 * (base + cb);
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+    for (int t = 0; t < 4; ++t) {
+        if (!tok[t]) continue;
+        const int r2 = 16 * tjb[t] + rr;
+        if (r2 >= kr) continue;  // column must be a camera dof
+        const int g2 = 6 * base + r2;
 #pragma unroll
-            for (int e = 0; e < 6; ++e) {
-                const int row = gcb + e, col = gca + 3 * h + r;
-                if (row >= col) atomicAdd(&S[(size_t)row * ld + col], -acc[r * 6 + e]);
-            }
-    } else if (ca >= 0) {
-        const int g = 6 * (base + ca);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-#pragma unroll
-            for (int mm = 0; mm < 4; ++mm) atomicAdd(&S[(size_t)(P.kb + mm) * ld + g + r], -acc[r * 4 + mm]);
-            atomicAdd(&rhs[g + r], -acc[24 + r]);
+        for (int g = 0; g < 4; ++g) {
+            const int r1 = 16 * tib[t] + kq + 4 * g;
+            if (r1 < r2 || r1 > er) continue;
+            const double v = -acc[t][g];
+            if (r1 < kr) atomicAdd(&S[(size_t)(6 * base + r1) * ld + g2], v);
+            else if (r1 < er) atomicAdd(&S[(size_t)(P.kb + r1 - kr) * ld + g2], v);
+            else atomicAdd(&rhs[g2], v);
         }
     }
+    if constexpr (STAMP) {
+        __syncthreads();
+        SCH_STAMP(3);
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 4; ++k) stamps[(size_t)blockIdx.x * 4 + k] = st_acc[k];
+    }
+#undef SCH_STAMP
 }
 
 // ---------------------------------------------------------------- Cholesky
@@ -640,7 +710,6 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 // (lower triangle, row-major), then L z = b, L^T y = z (y overwrites b).
 // One workgroup (4 waves). fcol[i]: first non-zero 16-block column of block row i;
 // rows[rptr[k]..rptr[k+1]): block rows i > k with fcol[i] <= k.
-typedef double d4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(TPB) void k_chol(const LmState* __restrict__ st, double* __restrict__ A, int npad, int nb,
                                               const int* __restrict__ fcol,
@@ -821,13 +890,6 @@ static constexpr int BAND_MAX_NB = 2048;                // fcol staged in LDS (n
 // Diagnostic stamps (separate build via STAMP=true, MIBA_CHOL_STAMPS=1): cycles per phase
 // accumulated by thread 0: [0] prefetch issue, [1] trsm, [2] update || look-ahead potrf, [3] retire/install,
 // [4] tail+backward.
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
 // uniform broadcast of lane `l`'s double (v_readlane, no LDS round trip)
 __device__ __forceinline__ double bcast(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);
@@ -1364,21 +1426,36 @@ __global__ __launch_bounds__(TPB) void k_final(DevProblem P, const LmState* __re
 // ---------------------------------------------------------------- LM control
 // |x|^2 of the active parameter blocks (ambient) -> initial state; called once after
 // the iteration-0 linearisation (lin[0] = cost, lin[1] = gmax of cams+intrinsics).
-__global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* __restrict__ lin,
-                                                    LmState* __restrict__ st, double* __restrict__ log) {
+// |x|^2 at the start of a solve: per-block partial sums over the active cameras / points,
+// then one block reduces the partials (fixed order) and initialises the LM state.
+__global__ __launch_bounds__(TPB) void k_xnorm_part(DevProblem P, const LmState* __restrict__ st,
+                                                    double* __restrict__ part) {
     __shared__ double lds[4];
     __shared__ double out[1];
     const int cur = st->cur;
     double a[1] = {0.0};
-    for (int t = threadIdx.x; t < P.nac; t += TPB) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    if (t < P.nac) {
         const double* x = P.cams[cur] + 7 * P.ac_cam[t];
 #pragma unroll
         for (int j = 0; j < 7; ++j) a[0] += x[j] * x[j];
     }
-    for (int t = threadIdx.x; t < P.n_ap; t += TPB) {
+    if (t < P.n_ap) {
         const double* x = P.pts[cur] + 3 * P.pt_idx[t];
         a[0] += x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
     }
+    block_sum<1>(a, lds, out);
+    if (threadIdx.x == 0) part[PART_INIT_XN2 * P.part_stride + blockIdx.x] = out[0];
+}
+
+__global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* __restrict__ lin,
+                                                    LmState* __restrict__ st, double* __restrict__ log,
+                                                    const double* __restrict__ part, int nparts) {
+    __shared__ double lds[4];
+    __shared__ double out[1];
+    const int cur = st->cur;
+    double a[1] = {0.0};
+    for (int t = threadIdx.x; t < nparts; t += TPB) a[0] += part[PART_INIT_XN2 * P.part_stride + t];
     block_sum<1>(a, lds, out);
     if (threadIdx.x == 0) {
         const double* K = P.K[cur];
@@ -1545,7 +1622,9 @@ hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevW
 }
 
 hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
-    PL(K_XNORM, k_xnorm_init, dim3(1), dim3(TPB), 0, s, P, W.lin, W.st, W.log);
+    const int nparts = nblocks(std::max(P.nac, P.n_ap), TPB);
+    PL(K_XNORM, k_xnorm_part, dim3(nparts), dim3(TPB), 0, s, P, W.st, W.part);
+    PL(K_XNORM, k_xnorm_init, dim3(1), dim3(TPB), 0, s, P, W.lin, W.st, W.log, W.part, nparts);
     return hipSuccess;
 }
 
@@ -1560,7 +1639,38 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
         PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, W.st, 1, W.scale, W.cnp,
            W.pdata, W.S, W.rhs, W.part);
     if (P.n_tiles > 0)
-        PL(K_SCHUR_TILE, k_schur_tile, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs);
+    {
+        static int smode = -1;
+        static unsigned long long* sst = nullptr;
+        static int scap = 0;
+        if (smode < 0) {
+            const char* e = getenv("MIBA_SCHUR_STAMPS");
+            smode = (e && e[0] == '1') ? 1 : 0;
+        }
+        if (smode == 1) {
+            if (scap < P.n_tiles) {
+                if (sst) CK(hipFree(sst));
+                CK(hipMalloc(&sst, sizeof(unsigned long long) * 4 * P.n_tiles));
+                scap = P.n_tiles;
+            }
+            PL(K_SCHUR_TILE, k_schur_tile<true>, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
+               sst);
+            std::vector<unsigned long long> h((size_t)4 * P.n_tiles);
+            CK(hipMemcpyAsync(h.data(), sst, sizeof(h[0]) * h.size(), hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            double sum[4] = {0, 0, 0, 0}, mx = 0;
+            for (int t = 0; t < P.n_tiles; ++t) {
+                double tot = 0;
+                for (int k = 0; k < 4; ++k) { sum[k] += (double)h[4 * t + k]; tot += (double)h[4 * t + k]; }
+                mx = std::max(mx, tot);
+            }
+            fprintf(stderr, "schur_tile %d tiles, mean cycles/tile: zero %.0f phaseA %.0f phaseB %.0f flush %.0f | max total %.0f\n",
+                    P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
+        } else {
+            PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
+               W.rhs, (unsigned long long*)nullptr);
+        }
+    }
     if (P.n_ovf_obs > 0)
         PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata,
            W.S, W.rhs);

@@ -54,7 +54,7 @@ struct DevBuf {
 
 enum BufId {
     B_CAMS0, B_CAMS1, B_PTS0, B_PTS1, B_K0, B_K1, B_PRIOR,
-    B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PT_PTR, B_PT_IDX,
+    B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PO_PT, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
     B_FCOL, B_RPTR, B_ROWS, B_BCR, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
@@ -334,7 +334,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         ctx->po_orig.insert(ctx->po_orig.end(), plist.begin() + pptr[i], plist.begin() + pptr[i + 1]);
         pt_ptr[a + 1] = (int)ctx->po_orig.size();
     }
-    std::vector<int> po_cam(n_adm), po_ac(n_adm), po_ap(n_adm), ovf_obs;
+    std::vector<int> po_cam(n_adm), po_ac(n_adm), po_ap(n_adm), po_pt(n_adm), ovf_obs;
     std::vector<double> po_uv(2 * (size_t)n_adm), po_dep(n_adm);
     for (int a = 0; a < n_ap; ++a)
         for (int q = pt_ptr[a]; q < pt_ptr[a + 1]; ++q) {
@@ -342,6 +342,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             po_cam[q] = p->obs_cam[k];
             po_ac[q] = cam_ac[p->obs_cam[k]];
             po_ap[q] = a;
+            po_pt[q] = ctx->pt_idx[a];
             po_uv[2 * (size_t)q] = p->obs_uv[2 * (size_t)k];
             po_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
             po_dep[q] = p->obs_depth[k];
@@ -411,6 +412,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     HIPCHECK(ctx, upload(ctx, B_PO_UV, po_uv.data(), 2 * (size_t)n_adm));
     HIPCHECK(ctx, upload(ctx, B_PO_DEP, po_dep.data(), n_adm));
     HIPCHECK(ctx, upload(ctx, B_PO_AP, po_ap.data(), n_adm));
+    HIPCHECK(ctx, upload(ctx, B_PO_PT, po_pt.data(), n_adm));
     HIPCHECK(ctx, upload(ctx, B_PT_PTR, pt_ptr.data(), n_ap + 1));
     HIPCHECK(ctx, upload(ctx, B_PT_IDX, ctx->pt_idx.data(), n_ap));
     HIPCHECK(ctx, upload(ctx, B_CO_PT, co_pt.data(), n_adm));
@@ -454,7 +456,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     P.prior = ctx->buf[B_PRIOR].as<double>();
     P.po_cam = ctx->buf[B_PO_CAM].as<int>(); P.po_ac = ctx->buf[B_PO_AC].as<int>();
     P.po_uv = ctx->buf[B_PO_UV].as<double2>(); P.po_depth = ctx->buf[B_PO_DEP].as<double>();
-    P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.pt_ptr = ctx->buf[B_PT_PTR].as<int>();
+    P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.po_pt = ctx->buf[B_PO_PT].as<int>();
+    P.pt_ptr = ctx->buf[B_PT_PTR].as<int>();
     P.pt_idx = ctx->buf[B_PT_IDX].as<int>();
     P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
     P.co_depth = ctx->buf[B_CO_DEP].as<double>();

@@ -1,8 +1,10 @@
-"""Diagnostic: per-phase cycle stamps of the BCR kernels on a config (MIBA_BCR_STAMPS=1)."""
+"""Diagnostic: per-phase cycle stamps of the hand-written kernels on a synthetic config.
+
+usage: MIBA_BCR_STAMPS=1 | MIBA_SCHUR_STAMPS=1 | MIBA_CHOL_STAMPS=1  python tools/kernel_stamps.py [C4] [iters]
+The stamped kernel variants print their phase breakdown to stderr on every launch."""
 import os
 import sys
 
-os.environ["MIBA_BCR_STAMPS"] = "1"
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "3dsmc-bundle-adjustment_amd"))
 from miba import synthetic  # noqa: E402
 from miba.solver import Solver  # noqa: E402
