@@ -6,39 +6,45 @@
 // border B (6nac x 4) and corner C (4x4):
 //     S = [A  B; B^T C],  A y_a + B y_k = b_a,  B^T y_a + C y_k = b_k.
 // We solve A [u | V] = [b_a | B] (5 right-hand sides) by odd-even block elimination.
-// At level m (stride s = 2^m) every block i with i % 2s == s is eliminated in parallel,
-// one workgroup each (k_bcr_elim):
-//   - its diagonal block D_i, rhs R_i and couplings A[i][i-s], A[i][i+s] are assembled:
-//     level 0 reads them straight from S; deeper levels subtract the Schur contributions
-//     that blocks eliminated at levels l < m left for it (UR of i-2^l, UL of i+2^l) and
-//     take the fill couplings F of i -+ 2^(m-1);
-//   - Cf = chol(D_i) (LDS, MFMA trailing updates), [XL | XR | x] = Cf^-1 [A_l | A_r | R];
-//   - it emits its own contributions for the survivors, all from LDS operands:
-//       UL = XL^T XL, rL = XL^T x  -> left survivor i-s
-//       UR = XR^T XR, rR = XR^T x  -> right survivor i+s
-//       F  = -XR^T XL              -> new coupling A[i+s][i-s]
-//     Survivors sum these in a fixed order when they are eliminated (deterministic, no
-//     atomics, no separate update pass).
-// Block 0 is factored last (the root); back-substitution runs the levels in reverse
-// (k_bcr_back: y_i = Cf^-T (x_i - XL y_{i-s} - XR y_{i+s})). Finally the 4x4 border system
-// C' = C - B^T V, b' = b_k - B^T u gives y_k and y_a = u - V y_k (k_bcr_border).
-// Sequential depth: (levels + 1) block factorizations instead of the n = 6*nac + 4 pivots
-// of the band Cholesky; exact elimination, only the rounding order differs.
+// Level m (stride s = 2^m) eliminates every block i with i % 2s == s:
+//   k_bcr_elim  (critical path, one workgroup per block) assembles D_i, R_i and the
+//               couplings A[i][i-s], A[i][i+s] in ONE load round, then factors
+//               Cf = chol(D_i) fused with the forward solve X = Cf^-1 [A_l | A_r | R_i].
+//               Level 0 reads S directly; level m >= 1 subtracts the level m-1 Schur
+//               contributions of its neighbours i -+ s/2 from Dacc_i, which already holds
+//               all earlier levels: extra "accumulator" workgroups of the same launch fold
+//               level m-1 into Dacc_j of every block j that survives level m.
+//   k_bcr_contrib (11 workgroups per eliminated block, MFMA operands straight from L2)
+//               emits UL = XL^T XL, UR = XR^T XR, F = -XR^T XL, rL = XL^T x, rR = XR^T x.
+// Block 0 is the root (factor + solve). Back-substitution runs the levels in reverse
+// (k_bcr_back: y_i = Cf^-T (x_i - XL y_{i-s} - XR y_{i+s}), plus the border partial
+// B_i^T y_i). k_bcr_border sums the partials in block order, solves the 4x4 system
+// C' y_k = b' (C' = C - B^T V, b' = b_k - B^T u) and writes y_a = u - V y_k.
+// All sums run in a fixed order (deterministic, no atomics). Sequential depth:
+// (levels + 1) block factorizations instead of the n = 6*nac + 4 pivots of the band
+// Cholesky; exact elimination, only the rounding order differs.
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
 
 #include "ba_device.h"
 #include "ba_kernels.h"
 
 namespace miba {
 
-static constexpr int TPB_B = 512;        // 8 waves per block workgroup
-static constexpr int NWB = TPB_B / 64;
+static constexpr int TPB_E = 512;        // elimination workgroup: 8 waves
+static constexpr int NWE = TPB_E / 64;
+static constexpr int TPB_C = 256;        // contrib / back workgroups: 4 waves
 static constexpr int BB = 64;            // block size (dofs)
 static constexpr int BLD = 66;           // LDS row stride of 64x64 blocks
 static constexpr int RC = 8;             // rhs columns: u, V(4), 3 pad
-static constexpr int LDX = 2 * BB + RC;  // [XL | XR | x]
+static constexpr int XW = 2 * BB + RC;   // [XL | XR | x] width (global and LDS stride)
 static constexpr int G_DOF = 6 * BCR_CAMS;
 static constexpr int BSZ = BB * BB;
+static constexpr int XSZ = BB * XW;
+static constexpr int RSZ = BB * RC;
+static constexpr int NCONTRIB_WG = 11;  // 44 contribution tiles / 4 waves
 typedef double d4b __attribute__((ext_vector_type(4)));
 
 // Diagnostic phase stamps (MIBA_BCR_STAMPS=1 launches the STAMP=true variants).
@@ -49,12 +55,12 @@ __device__ __forceinline__ unsigned long long bcr_stamp() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
-#define BCR_STAMP(k)                                                             \
-    do {                                                                         \
-        if constexpr (STAMP) {                                                   \
-            __syncthreads();                                                     \
-            if (threadIdx.x == 0) stamps[(m * 64 + blockIdx.x % 64) * 8 + (k)] = bcr_stamp(); \
-        }                                                                        \
+#define BCR_STAMP(slot, k)                                                                       \
+    do {                                                                                         \
+        if constexpr (STAMP) {                                                                   \
+            __syncthreads();                                                                     \
+            if (threadIdx.x == 0 && blockIdx.x == 0) stamps[(slot) * 8 + (k)] = bcr_stamp();     \
+        }                                                                                        \
     } while (0)
 
 __device__ __forceinline__ double bcast_b(double v, int l) {
@@ -63,11 +69,12 @@ __device__ __forceinline__ double bcast_b(double v, int l) {
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
     return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ double rsqrt_nr_b(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    y = y * (1.5 - 0.5 * x * y * y);
-    y = y * (1.5 - 0.5 * x * y * y);
-    return y;
+// 1/sqrt(x): v_rsq_f64 (~2^-24) + one Newton step in FMA form (rel. error ~4e-15,
+// measured by tools/rsq_f64_check.hip) — three dependent f64 ops on the pivot path.
+__device__ __forceinline__ double rsqrt_1nr(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = __builtin_fma(-x * y, y, 1.0);
+    return __builtin_fma(0.5 * y, e, y);
 }
 
 // 16x16 Cholesky of the tile at T (LDS, stride ld) by one wave; rdiag[16] = 1/L_jj.
@@ -83,7 +90,7 @@ __device__ __forceinline__ void potrf16_tile(double* T, int ld, double* rdiag, i
         const bool ok = (djj > 0.0) && (djj < INFINITY);
         bad = bad || !ok;
         djj = ok ? djj : 1.0;
-        const double inv = rsqrt_nr_b(djj);
+        const double inv = rsqrt_1nr(djj);
         const double lrj = a[j] * inv;
         a[j] = lrj;
         my_inv = (r == j) ? inv : my_inv;
@@ -97,100 +104,107 @@ __device__ __forceinline__ void potrf16_tile(double* T, int ld, double* rdiag, i
     }
 }
 
-// In-LDS Cholesky of a 64x64 SPD block (lower triangle of T, stride BLD), whole workgroup.
-__device__ void potrf64(double* T, double* rdiag64, bool& bad) {
+// Forward substitution of a 16-vector against the 16x16 lower tile Lkk:
+// v[m] = (v[m] - sum_{j<m} L[m][j] v[j]) / L[m][m]. Serves both panel rows
+// (l = a L^-T) and right-hand-side columns (z = L^-1 b).
+__device__ __forceinline__ void fwd16(double v[16], const double* Lkk, const double* rd) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        v[m] *= rd[m];
+#pragma unroll
+        for (int j = m + 1; j < 16; ++j) v[j] -= Lkk[j * BLD + m] * v[m];
+    }
+}
+
+// In-LDS Cholesky of the 64x64 SPD block T (lower, stride BLD) fused with the forward
+// solve X <- L^-1 X of ncol right-hand columns (X stride XW): per 16-column panel,
+// (1) wave 0 factors the diagonal tile, (2) the panel rows below it and the X columns
+// run their 16-step substitution in the same phase, (3) the trailing updates of T and
+// of X share one MFMA phase.
+__device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, bool& bad) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rr = lane & 15, kk = lane >> 4;
+    const int ncb = (ncol + 15) >> 4;
     for (int kb = 0; kb < 4; ++kb) {
         double* Tkk = T + (16 * kb) * BLD + 16 * kb;
+        const double* rd = rdiag64 + 16 * kb;
         if (wave == 0) potrf16_tile(Tkk, BLD, rdiag64 + 16 * kb, lane, bad);
         __syncthreads();
-        const int nrow = 64 - 16 * (kb + 1);
+        const int nrow = 48 - 16 * kb;
         if (tid < nrow) {
-            const int r = 16 * (kb + 1) + tid;
-            double x[16];
+            double* row = T + (16 * (kb + 1) + tid) * BLD + 16 * kb;
+            double v[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) x[j] = T[r * BLD + 16 * kb + j];
+            for (int j = 0; j < 16; ++j) v[j] = row[j];
+            fwd16(v, Tkk, rd);
 #pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                x[m] *= rdiag64[16 * kb + m];
+            for (int j = 0; j < 16; ++j) row[j] = v[j];
+        } else if (tid < nrow + ncol) {
+            double* col = X + (16 * kb) * XW + (tid - nrow);
+            double v[16];
 #pragma unroll
-                for (int j = m + 1; j < 16; ++j) x[j] -= x[m] * Tkk[j * BLD + m];
-            }
+            for (int j = 0; j < 16; ++j) v[j] = col[j * XW];
+            fwd16(v, Tkk, rd);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) T[r * BLD + 16 * kb + j] = x[j];
+            for (int j = 0; j < 16; ++j) col[j * XW] = v[j];
         }
         __syncthreads();
+        // trailing: T tiles (i, j), kb < j <= i, then X tiles (i > kb, cb)
         const int nt = 3 - kb;
         const int npairs = nt * (nt + 1) / 2;
-        for (int t = wave; t < npairs; t += NWB) {
-            int p = 0, rem = t;
-            while (rem > p) { rem -= p + 1; ++p; }
-            const int i = kb + 1 + p, j = kb + 1 + rem;
-            const double* Li = T + (16 * i) * BLD + 16 * kb;
-            const double* Lj = T + (16 * j) * BLD + 16 * kb;
-            d4b acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[rr * BLD + 4 * s4 + kk], Lj[rr * BLD + 4 * s4 + kk], acc, 0, 0, 0);
-            double* C = T + (16 * i) * BLD + 16 * j;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) C[(kk + 4 * g) * BLD + rr] -= acc[g];
-        }
-        __syncthreads();
-    }
-}
-
-// X <- L^-1 X, L 64x64 lower (LDS, stride BLD), X 64 x ncol (LDS, stride ldx).
-__device__ void trsm_lower64(const double* L, const double* rdiag64, double* X, int ldx, int ncol) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int rr = lane & 15, kk = lane >> 4;
-    for (int kb = 0; kb < 4; ++kb) {
-        const double* Lkk = L + (16 * kb) * BLD + 16 * kb;
-        for (int c = tid; c < ncol; c += TPB_B) {
-            double x[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) x[j] = X[(16 * kb + j) * ldx + c];
-#pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                x[m] *= rdiag64[16 * kb + m];
-#pragma unroll
-                for (int j = m + 1; j < 16; ++j) x[j] -= Lkk[j * BLD + m] * x[m];
+        const int ntile = npairs + nt * ncb;
+        for (int t = wave; t < ntile; t += NWE) {
+            const double *Ap, *Bp;
+            double* C;
+            int ldb, ldc;
+            bool colok = true;
+            if (t < npairs) {
+                int p = 0, rem = t;
+                while (rem > p) { rem -= p + 1; ++p; }
+                const int i = kb + 1 + p, j = kb + 1 + rem;
+                Ap = T + (16 * i + rr) * BLD + 16 * kb;  // L[i][kb] row rr
+                Bp = T + (16 * j + rr) * BLD + 16 * kb;  // L[j][kb] row rr  (B = L[j][kb]^T)
+                C = T + (16 * i) * BLD + 16 * j;
+                ldb = 1;
+                ldc = BLD;
+            } else {
+                const int u = t - npairs, i = kb + 1 + u / ncb, cb = u % ncb;
+                Ap = T + (16 * i + rr) * BLD + 16 * kb;
+                Bp = X + (16 * kb) * XW + 16 * cb + rr;  // X[kb rows][cols]
+                C = X + (16 * i) * XW + 16 * cb;
+                ldb = XW;
+                ldc = XW;
+                colok = 16 * cb + rr < ncol;
             }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) X[(16 * kb + j) * ldx + c] = x[j];
-        }
-        __syncthreads();
-        const int ncb = (ncol + 15) / 16;
-        const int ntile = (3 - kb) * ncb;
-        for (int t = wave; t < ntile; t += NWB) {
-            const int i = kb + 1 + t / ncb, cb = t % ncb;
-            const double* A = L + (16 * i) * BLD + 16 * kb;
-            d4b acc = {0.0, 0.0, 0.0, 0.0};
-            const int col = 16 * cb + rr;
+            double av[4], bv[4];
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
-                const double bv = (col < ncol) ? X[(16 * kb + 4 * s4 + kk) * ldx + col] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[rr * BLD + 4 * s4 + kk], bv, acc, 0, 0, 0);
+                av[s4] = Ap[4 * s4 + kk];
+                bv[s4] = colok ? Bp[(4 * s4 + kk) * ldb] : 0.0;
             }
-            if (col < ncol)
+            d4b acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int g = 0; g < 4; ++g) X[(16 * i + kk + 4 * g) * ldx + col] -= acc[g];
+            for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+            if (colok)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) C[(kk + 4 * g) * ldc + rr] -= acc[g];
         }
         __syncthreads();
     }
 }
 
-// X <- L^-T X (backward), L 64x64 lower in LDS, X (64 x ncol) in LDS.
+// X <- L^-T X (backward), L 64x64 lower in LDS (stride BLD), X 64 x ncol (LDS, stride ldx).
 __device__ void trsm_lower64_t(const double* L, const double* rdiag64, double* X, int ldx, int ncol) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rr = lane & 15, kk = lane >> 4;
+    const int nw = blockDim.x >> 6;
     for (int kb = 3; kb >= 0; --kb) {
         const double* Lkk = L + (16 * kb) * BLD + 16 * kb;
-        for (int c = tid; c < ncol; c += TPB_B) {
+        if (tid < ncol) {
+            double* col = X + (16 * kb) * ldx + tid;
             double x[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) x[j] = X[(16 * kb + j) * ldx + c];
+            for (int j = 0; j < 16; ++j) x[j] = col[j * ldx];
 #pragma unroll
             for (int m = 15; m >= 0; --m) {
                 x[m] *= rdiag64[16 * kb + m];
@@ -198,22 +212,24 @@ __device__ void trsm_lower64_t(const double* L, const double* rdiag64, double* X
                 for (int j = 0; j < m; ++j) x[j] -= Lkk[m * BLD + j] * x[m];  // (L^T)[j][m] = L[m][j]
             }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) X[(16 * kb + j) * ldx + c] = x[j];
+            for (int j = 0; j < 16; ++j) col[j * ldx] = x[j];
         }
         __syncthreads();
         const int ncb = (ncol + 15) / 16;
         const int ntile = kb * ncb;
-        for (int t = wave; t < ntile; t += NWB) {
+        for (int t = wave; t < ntile; t += nw) {
             const int i = t / ncb, cb = t % ncb;
             const double* A = L + (16 * kb) * BLD + 16 * i;  // L[kb][i]; operand (L^T)[r][k] = L[kb][i][k][r]
-            d4b acc = {0.0, 0.0, 0.0, 0.0};
             const int col = 16 * cb + rr;
+            double av[4], bv[4];
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
-                const double av = A[(4 * s4 + kk) * BLD + rr];
-                const double bv = (col < ncol) ? X[(16 * kb + 4 * s4 + kk) * ldx + col] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                av[s4] = A[(4 * s4 + kk) * BLD + rr];
+                bv[s4] = (col < ncol) ? X[(16 * kb + 4 * s4 + kk) * ldx + col] : 0.0;
             }
+            d4b acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
             if (col < ncol)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) X[(16 * i + kk + 4 * g) * ldx + col] -= acc[g];
@@ -222,316 +238,362 @@ __device__ void trsm_lower64_t(const double* L, const double* rdiag64, double* X
     }
 }
 
-// 64x64 block copy global -> LDS with every load issued before any LDS store
-// (one round trip per block instead of one per element row).
-template <bool TRANS>
-__device__ __forceinline__ void stage64(double* dst, int ldd, const double* __restrict__ src) {
-    double v[BSZ / TPB_B];
-#pragma unroll
-    for (int q = 0; q < BSZ / TPB_B; ++q) v[q] = src[threadIdx.x + TPB_B * q];
-#pragma unroll
-    for (int q = 0; q < BSZ / TPB_B; ++q) {
-        const int e = threadIdx.x + TPB_B * q, r = e >> 6, c = e & 63;
-        if (TRANS) dst[c * ldd + r] = v[q];
-        else dst[r * ldd + c] = v[q];
-    }
+// Y <- L^-T Y for the 8 right-hand columns of Y (LDS, 64 x RC), L = Cf (LDS, stride BLD,
+// upper triangle zero), rd = 1/diag(L). Lane-per-row layout: waves 0..3 each own columns
+// (w, w+4); lane r holds row r. Step R = 63..0 finalises row R (y_R = x_R / L_RR) and
+// broadcasts x_R by v_readlane; rows r < R subtract (L[R][r] / L_RR) x_R. The row
+// L[R][*] is one conflict-free LDS read, issued a step ahead; no barriers inside.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ void zero64(double* dst, int ldd) {
+__device__ void trsm_t_lanes(const double* L, const double* rd, double* Y) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave < 4) {
+        double x0 = Y[lane * RC + wave], x1 = Y[lane * RC + wave + 4];
+        double lr = L[63 * BLD + lane] * rd[63];
 #pragma unroll
-    for (int q = 0; q < BSZ / TPB_B; ++q) {
-        const int e = threadIdx.x + TPB_B * q;
-        dst[(e >> 6) * ldd + (e & 63)] = 0.0;
+        for (int R = 63; R >= 0; --R) {
+            const double lt = lane < R ? lr : 0.0;
+            if (R > 0) lr = L[(R - 1) * BLD + lane] * rd[R - 1];  // prefetch the next row
+            const double xr0 = readlane_d(x0, R), xr1 = readlane_d(x1, R);
+            x0 = __builtin_fma(-lt, xr0, x0);
+            x1 = __builtin_fma(-lt, xr1, x1);
+        }
+        const double rdl = rd[lane];
+        Y[lane * RC + wave] = x0 * rdl;
+        Y[lane * RC + wave + 4] = x1 * rdl;
     }
+    __syncthreads();
 }
-__device__ __forceinline__ void store64(double* __restrict__ dst, const double* src, int lds_) {
+
+// Border rows B_i (4 x 60, S rows kb..kb+3 at the block's columns) -> LDS Bl[4][BB]
+// (zero past the last dof); one element per thread, issued with the block's other loads.
+__device__ __forceinline__ double border_load(const DevProblem& P, const double* __restrict__ S, int i, int e) {
+    const int m = e >> 6, r = e & 63;
+    const int b0 = i * G_DOF, nd = 6 * P.nac;
+    return (e < 4 * BB && r < G_DOF && b0 + r < nd) ? S[(size_t)(P.kb + m) * P.npad + b0 + r] : 0.0;
+}
+// Border partial B_i^T Y_i (4 x 5) from Bl (LDS) and Y (LDS, stride RC): 80 threads
+// = 20 outputs x 4 row quarters, then a fixed-order 4-term sum.
+__device__ __forceinline__ void border_partial(const double* Bl, const double* Yl, double* red, int i,
+                                               double* __restrict__ Bp) {
+    const int t = threadIdx.x;
+    if (t < 80) {
+        const int q = t >> 2, part = t & 3, m = q / 5, c = q % 5;
+        double acc = 0.0;
 #pragma unroll
-    for (int q = 0; q < BSZ / TPB_B; ++q) {
-        const int e = threadIdx.x + TPB_B * q;
-        dst[e] = src[(e >> 6) * lds_ + (e & 63)];
+        for (int r = 16 * part; r < 16 * part + 16; ++r) acc += Bl[m * BB + r] * Yl[r * RC + c];
+        red[t] = acc;
     }
+    __syncthreads();
+    if (t < 20) Bp[(size_t)i * 32 + t] = ((red[4 * t] + red[4 * t + 1]) + red[4 * t + 2]) + red[4 * t + 3];
 }
 
 struct ElimLds {
-    double T[BB * BLD];   // D_i -> Cf
-    double X[BB * LDX];   // [A_l | A_r | R] -> [XL | XR | x]
+    double T[BB * BLD];  // D_i -> Cf
+    double X[BB * XW];   // [A_l | A_r | R] -> [XL | XR | x]
     double rdiag[BB];
+    double Bl[4 * BB];   // root: border rows
+    double red[80];
 };
 
-// ---- level-m elimination of the blocks i = s + 2s*b (s = 2^m); m == levels: root (block 0).
+// ---- launch m: eliminate the blocks of level m (workgroups [0, nel)) and fold the level
+// m-1 contributions into the accumulators of the level-m survivors (workgroups [nel, ...)).
+// m == levels: the root (block 0; one workgroup).
 template <bool STAMP>
-__global__ __launch_bounds__(TPB_B) void k_bcr_elim(const LmState* __restrict__ st, DevProblem P,
+__global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ st, DevProblem P,
                                                     const double* __restrict__ S, const double* __restrict__ rhs,
-                                                    BcrWork Bw, int m, int* __restrict__ flag,
+                                                    BcrWork Bw, int m, int nel, int* __restrict__ flag,
                                                     unsigned long long* __restrict__ stamps) {
     if (st->done) return;
-    BCR_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ElimLds& L = *reinterpret_cast<ElimLds*>(smem);
     const int nblk = Bw.nblk;
     const bool root = m >= Bw.levels;
-    const int s = 1 << m;
+    const int s = 1 << m, h = s >> 1;
+    const int tid = threadIdx.x;
+    const size_t ld = P.npad;
+    const int nd = 6 * P.nac;
+    constexpr int NQ = BSZ / TPB_E;  // 64x64 elements per thread
+    BCR_STAMP(m, 0);
+    if (!root && (int)blockIdx.x >= nel) {
+        // accumulator for survivor j (m >= 1): Dacc_j = base - UR_{j-h} - UL_{j+h}
+        const int j = ((int)blockIdx.x - nel) << (m + 1);
+        if (j >= nblk) return;
+        const int a = j - h, b = j + h;
+        const int b0 = j * G_DOF;
+        double v[NQ], ua[NQ], ub[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+            const bool ok = c <= r && r < G_DOF && b0 + r < nd;
+            v[q] = m >= 2 ? Bw.Dacc[(size_t)j * BSZ + e] : (ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0));
+            ua[q] = a >= 0 ? Bw.UR[(size_t)a * BSZ + e] : 0.0;
+            ub[q] = b < nblk ? Bw.UL[(size_t)b * BSZ + e] : 0.0;
+        }
+        const int r = tid >> 3, c = tid & 7, gr = b0 + r;
+        double rv = 0.0;
+        if (m >= 2) rv = Bw.Racc[(size_t)j * RSZ + tid];
+        else if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
+        const double ra = a >= 0 ? Bw.rR[(size_t)a * RSZ + tid] : 0.0;
+        const double rb = b < nblk ? Bw.rL[(size_t)b * RSZ + tid] : 0.0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) Bw.Dacc[(size_t)j * BSZ + tid + TPB_E * q] = (v[q] - ua[q]) - ub[q];
+        Bw.Racc[(size_t)j * RSZ + tid] = (rv - ra) - rb;
+        return;
+    }
     const int i = root ? 0 : s + 2 * s * (int)blockIdx.x;
     if (i >= nblk) return;
     const bool has_r = !root && i + s < nblk;
-    const size_t ld = P.npad;
-    const int nd = 6 * P.nac;
     const int b0 = i * G_DOF;
-    const int tid = threadIdx.x;
-
-    // D_i: lower triangle of S (identity on pad / missing dofs) minus pending contributions
+    const int a = i - h, b = i + h;  // level m-1 neighbours (m >= 1)
+    // ---- one load round: D, R, contributions, couplings
     {
-        double v[BSZ / TPB_B];
+        double v[NQ], ua[NQ], ub[NQ], al[NQ], ar[NQ];
 #pragma unroll
-        for (int q = 0; q < BSZ / TPB_B; ++q) {
-            const int e = tid + TPB_B * q, r = e >> 6, c = e & 63;
-            const int gr = b0 + r;
-            const bool ok = c <= r && r < G_DOF && gr < nd;
-            v[q] = ok ? S[(size_t)gr * ld + b0 + c] : (r == c ? 1.0 : 0.0);
-        }
-        for (int l = 0; l < m; ++l) {
-            const int a = i - (1 << l), b = i + (1 << l);
-            const double* pa = Bw.UR + (size_t)(a >= 0 ? a : 0) * BSZ;
-            const double* pb = Bw.UL + (size_t)(b < nblk ? b : 0) * BSZ;
-            double ua[BSZ / TPB_B], ub[BSZ / TPB_B];
-#pragma unroll
-            for (int q = 0; q < BSZ / TPB_B; ++q) {
-                ua[q] = a >= 0 ? pa[tid + TPB_B * q] : 0.0;
-                ub[q] = b < nblk ? pb[tid + TPB_B * q] : 0.0;
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+            const bool ok = c <= r && r < G_DOF && b0 + r < nd;
+            v[q] = m >= 2 ? Bw.Dacc[(size_t)i * BSZ + e] : (ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0));
+            ua[q] = (m >= 1 && a >= 0) ? Bw.UR[(size_t)a * BSZ + e] : 0.0;
+            ub[q] = (m >= 1 && b < nblk) ? Bw.UL[(size_t)b * BSZ + e] : 0.0;
+            if (root) {
+                al[q] = ar[q] = 0.0;
+            } else if (m == 0) {
+                const bool okl = r < G_DOF && b0 + r < nd && c < G_DOF;
+                al[q] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
+                const int b1 = b0 + G_DOF;  // element (r, c) of A[i+1][i] -> A[i][i+1][c][r]
+                const bool okr = has_r && r < G_DOF && b1 + r < nd && c < G_DOF;
+                ar[q] = okr ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
+            } else {
+                al[q] = Bw.F[(size_t)(i - h) * BSZ + e];
+                ar[q] = has_r ? Bw.F[(size_t)(i + h) * BSZ + e] : 0.0;
             }
-#pragma unroll
-            for (int q = 0; q < BSZ / TPB_B; ++q) v[q] = (v[q] - ua[q]) - ub[q];
         }
-#pragma unroll
-        for (int q = 0; q < BSZ / TPB_B; ++q) {
-            const int e = tid + TPB_B * q;
-            L.T[(e >> 6) * BLD + (e & 63)] = v[q];
-        }
-    }
-    // R_i = [b_a | B] rows of block i (one element per thread)
-    {
         const int r = tid >> 3, c = tid & 7, gr = b0 + r;
-        double v = 0.0;
-        if (r < G_DOF && gr < nd) {
-            if (c == 0) v = rhs[gr];
-            else if (c <= 4) v = S[(size_t)(P.kb + c - 1) * ld + gr];
-        }
-        for (int l = 0; l < m; ++l) {
-            const int a = i - (1 << l), b = i + (1 << l);
-            const double va = a >= 0 ? Bw.rR[(size_t)a * BB * RC + tid] : 0.0;
-            const double vb = b < nblk ? Bw.rL[(size_t)b * BB * RC + tid] : 0.0;
-            v = (v - va) - vb;
-        }
-        L.X[r * LDX + 2 * BB + c] = v;
-    }
-    if (!root) {
-        // left coupling A[i][i-s]
-        if (m == 0) {
+        double rv = 0.0;
+        if (m >= 2) rv = Bw.Racc[(size_t)i * RSZ + tid];
+        else if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
+        const double ra = (m >= 1 && a >= 0) ? Bw.rR[(size_t)a * RSZ + tid] : 0.0;
+        const double rb = (m >= 1 && b < nblk) ? Bw.rL[(size_t)b * RSZ + tid] : 0.0;
 #pragma unroll
-            for (int q = 0; q < BSZ / TPB_B; ++q) {
-                const int e = tid + TPB_B * q, r = e >> 6, c = e & 63;
-                const int gr = b0 + r;
-                const bool ok = r < G_DOF && gr < nd && c < G_DOF;
-                L.X[r * LDX + c] = ok ? S[(size_t)gr * ld + b0 - G_DOF + c] : 0.0;
-            }
-        } else {
-            stage64<false>(L.X, LDX, Bw.F + (size_t)(i - s / 2) * BSZ);
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, rr_ = e >> 6, cc = e & 63;
+            L.T[rr_ * BLD + cc] = (v[q] - ua[q]) - ub[q];
+            L.X[rr_ * XW + cc] = al[q];
+            L.X[cc * XW + BB + rr_] = ar[q];  // A[i][i+s] = (A[i+s][i])^T
         }
-        // right coupling A[i][i+s] = A[i+s][i]^T
-        if (!has_r) {
-            zero64(L.X + BB, LDX);
-        } else if (m == 0) {
-            const int b1 = b0 + G_DOF;
-#pragma unroll
-            for (int q = 0; q < BSZ / TPB_B; ++q) {
-                const int e = tid + TPB_B * q, r = e >> 6, c = e & 63;
-                const bool ok = r < G_DOF && b1 + r < nd && c < G_DOF;
-                L.X[c * LDX + BB + r] = ok ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
-            }
-        } else {
-            stage64<true>(L.X + BB, LDX, Bw.F + (size_t)(i + s / 2) * BSZ);
-        }
+        L.X[r * XW + 2 * BB + c] = (rv - ra) - rb;
+        if (root && tid < 4 * BB) L.Bl[tid] = border_load(P, S, 0, tid);
     }
     __syncthreads();
-    BCR_STAMP(1);
+    BCR_STAMP(m, 1);
     bool bad = false;
-    potrf64(L.T, L.rdiag, bad);
+    potrf64_fwd(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad);
     if (bad) *flag = 1;
-    BCR_STAMP(2);
+    BCR_STAMP(m, 2);
     if (root) {
-        trsm_lower64(L.T, L.rdiag, L.X + 2 * BB, LDX, RC);
-        trsm_lower64_t(L.T, L.rdiag, L.X + 2 * BB, LDX, RC);
+        // compact the 8 solved columns (stride RC) next to the factor, backward solve
+        double* Yl = L.X;  // rows of X are consumed: reuse its head as Y_0 (stride RC)
         const int r = tid >> 3, c = tid & 7;
-        Bw.Y[tid] = L.X[r * LDX + 2 * BB + c];
+        const double z = L.X[r * XW + 2 * BB + c];
+        __syncthreads();
+        Yl[tid] = z;
+        __syncthreads();
+        trsm_t_lanes(L.T, L.rdiag, Yl);
+        Bw.Y[tid] = Yl[tid];
+        if (tid < 4) Bw.bk[tid] = rhs[P.kb + tid];
+        if (tid >= 4 && tid < 14) {
+            int q = tid - 4, mm = 0;
+            while (q > mm) { q -= mm + 1; ++mm; }
+            Bw.bk[tid] = S[(size_t)(P.kb + mm) * ld + P.kb + q];  // (mm, q), q <= mm
+        }
+        __syncthreads();
+        border_partial(L.Bl, Yl, L.red, 0, Bw.Bp);
+        BCR_STAMP(m, 3);
         return;
     }
-    trsm_lower64(L.T, L.rdiag, L.X, LDX, LDX);
-    BCR_STAMP(3);
-    // factor and solved blocks for the back-substitution
-    store64(Bw.Cf + (size_t)i * BSZ, L.T, BLD);
-    store64(Bw.XL + (size_t)i * BSZ, L.X, LDX);
-    if (has_r) store64(Bw.XR + (size_t)i * BSZ, L.X + BB, LDX);
-    {
-        const int r = tid >> 3, c = tid & 7;
-        Bw.x[(size_t)i * BB * RC + tid] = L.X[r * LDX + 2 * BB + c];
-    }
-    if (tid < BB) Bw.rd[(size_t)i * BB + tid] = L.rdiag[tid];
-    BCR_STAMP(4);
-    // Schur contributions for the survivors (operands in LDS):
-    //   t in [0,10) UL lower tiles, [10,20) UR lower tiles, [20,36) F, [36,40) rL, [40,44) rR
-    const int lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
-    for (int t = wave; t < 44; t += NWB) {
-        int ib, cb, aoff, boff;
-        double* dst;
-        int ldd = BB;
-        double sign = 1.0;
-        bool rhs_tile = false;
-        if (t < 20) {
-            if (t >= 10 && !has_r) continue;
-            int p = 0, rem = t % 10;
-            while (rem > p) { rem -= p + 1; ++p; }
-            ib = p; cb = rem;
-            aoff = boff = (t < 10) ? 0 : BB;
-            dst = (t < 10 ? Bw.UL : Bw.UR) + (size_t)i * BSZ;
-        } else if (t < 36) {
-            if (!has_r) continue;
-            ib = (t - 20) >> 2; cb = (t - 20) & 3;
-            aoff = BB; boff = 0; sign = -1.0;
-            dst = Bw.F + (size_t)i * BSZ;
-        } else {
-            if (t >= 40 && !has_r) continue;
-            ib = (t - 36) & 3; cb = 0;
-            aoff = (t < 40) ? 0 : BB; boff = 2 * BB;
-            dst = (t < 40 ? Bw.rL : Bw.rR) + (size_t)i * BB * RC;
-            ldd = RC;
-            rhs_tile = true;
-        }
-        const bool bcol_ok = !rhs_tile || rr < RC;
-        d4b acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int s4 = 0; s4 < 16; ++s4) {
-            const double* row = L.X + (4 * s4 + kk) * LDX;
-            const double bv = bcol_ok ? row[boff + 16 * cb + rr] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(row[aoff + 16 * ib + rr], bv, acc, 0, 0, 0);
-        }
-        if (bcol_ok)
+    // ---- store factor and solved blocks
 #pragma unroll
-            for (int g = 0; g < 4; ++g) dst[(size_t)(16 * ib + kk + 4 * g) * ldd + 16 * cb + rr] = sign * acc[g];
+    for (int q = 0; q < NQ; ++q) {
+        const int e = tid + TPB_E * q;
+        Bw.Cf[(size_t)i * BSZ + e] = L.T[(e >> 6) * BLD + (e & 63)];
     }
-    BCR_STAMP(5);
+    for (int e = tid; e < XSZ; e += TPB_E) Bw.X[(size_t)i * XSZ + e] = L.X[e];
+    if (tid < BB) Bw.rd[(size_t)i * BB + tid] = L.rdiag[tid];
+    BCR_STAMP(m, 3);
+}
+
+// ---- Schur contributions of the blocks eliminated at level m: 44 tiles per block,
+// one per wave, MFMA operands loaded straight from X (L2-resident):
+//   t in [0,10) UL lower tiles, [10,20) UR lower tiles, [20,36) F, [36,40) rL, [40,44) rR
+__global__ __launch_bounds__(TPB_C) void k_bcr_contrib(const LmState* __restrict__ st, BcrWork Bw, int m) {
+    if (st->done) return;
+    const int s = 1 << m;
+    const int bi = (int)blockIdx.x / NCONTRIB_WG, r = (int)blockIdx.x % NCONTRIB_WG;
+    const int i = s + 2 * s * bi;
+    const int nblk = Bw.nblk;
+    if (i >= nblk) return;
+    const bool has_r = i + s < nblk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, rr = lane & 15, kq = lane >> 4;
+    const int t = 4 * r + wave;
+    int ib, cb, aoff, boff, ldd = BB;
+    double* dst;
+    double sign = 1.0;
+    bool rhs_tile = false;
+    if (t < 20) {
+        if (t >= 10 && !has_r) return;
+        int p = 0, rem = t % 10;
+        while (rem > p) { rem -= p + 1; ++p; }
+        ib = p; cb = rem;
+        aoff = boff = (t < 10) ? 0 : BB;
+        dst = (t < 10 ? Bw.UL : Bw.UR) + (size_t)i * BSZ;
+    } else if (t < 36) {
+        if (!has_r) return;
+        ib = (t - 20) >> 2; cb = (t - 20) & 3;
+        aoff = BB; boff = 0; sign = -1.0;
+        dst = Bw.F + (size_t)i * BSZ;
+    } else {
+        if (t >= 40 && !has_r) return;
+        ib = (t - 36) & 3; cb = 0;
+        aoff = (t < 40) ? 0 : BB; boff = 2 * BB;
+        dst = (t < 40 ? Bw.rL : Bw.rR) + (size_t)i * RSZ;
+        ldd = RC;
+        rhs_tile = true;
+    }
+    const bool bcol_ok = !rhs_tile || rr < RC;
+    const double* X = Bw.X + (size_t)i * XSZ;
+    double av[16], bv[16];
+#pragma unroll
+    for (int s4 = 0; s4 < 16; ++s4) {
+        const double* row = X + (4 * s4 + kq) * XW;
+        av[s4] = row[aoff + 16 * ib + rr];
+        bv[s4] = bcol_ok ? row[boff + 16 * cb + rr] : 0.0;
+    }
+    d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s4 = 0; s4 < 16; s4 += 2) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4 + 1], bv[s4 + 1], acc1, 0, 0, 0);
+    }
+    if (bcol_ok)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dst[(size_t)(16 * ib + kq + 4 * g) * ldd + 16 * cb + rr] = sign * (acc0[g] + acc1[g]);
 }
 
 struct BackLds {
-    double T[BB * BLD];   // Cf_i
-    double U1[BB * BLD];  // XL_i
-    double U2[BB * BLD];  // XR_i
-    double t[BB * RC], yl[BB * RC], yr[BB * RC];
+    double T[BB * BLD];  // Cf_i
+    double t[RSZ], yl[RSZ], yr[RSZ];
     double rdiag[BB];
+    double Bl[4 * BB];   // border rows of the block
+    double red[80];
 };
 
 // ---- back-substitution for the blocks eliminated at level m:
-// y_i = Cf_i^-T (x_i - XL_i y_{i-s} - XR_i y_{i+s})
+// y_i = Cf_i^-T (x_i - XL_i y_{i-s} - XR_i y_{i+s});  plus the border partial B_i^T y_i.
 template <bool STAMP>
-__global__ __launch_bounds__(TPB_B) void k_bcr_back(const LmState* __restrict__ st, BcrWork Bw, int m,
+__global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ st, DevProblem P,
+                                                    const double* __restrict__ S, BcrWork Bw, int m,
                                                     unsigned long long* __restrict__ stamps) {
     if (st->done) return;
-    BCR_STAMP(6);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BackLds& L = *reinterpret_cast<BackLds*>(smem);
     const int s = 1 << m;
     const int i = s + 2 * s * (int)blockIdx.x;
     const int nblk = Bw.nblk;
     if (i >= nblk) return;
+    BCR_STAMP(16 + m, 0);
     const bool has_r = i + s < nblk;
-    const int tid = threadIdx.x;
-    stage64<false>(L.T, BLD, Bw.Cf + (size_t)i * BSZ);
-    stage64<false>(L.U1, BLD, Bw.XL + (size_t)i * BSZ);
-    if (has_r) stage64<false>(L.U2, BLD, Bw.XR + (size_t)i * BSZ);
-    {
-        const double xv = Bw.x[(size_t)i * BB * RC + tid];
-        const double yl = Bw.Y[(size_t)(i - s) * BB * RC + tid];
-        const double yr = has_r ? Bw.Y[(size_t)(i + s) * BB * RC + tid] : 0.0;
-        L.t[tid] = xv;
-        L.yl[tid] = yl;
-        L.yr[tid] = yr;
-        if (tid < BB) L.rdiag[tid] = Bw.rd[(size_t)i * BB + tid];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kq = lane >> 4;
+    constexpr int NQ = BSZ / TPB_C;
+    const double* X = Bw.X + (size_t)i * XSZ;
+    // ---- one load round: Cf, x, y_{i-s}, y_{i+s}, and the MFMA A-operands XL / XR
+    double cf[NQ], xv[2], ylv[2], yrv[2], al[16], ar[16];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) cf[q] = Bw.Cf[(size_t)i * BSZ + tid + TPB_C * q];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = tid + TPB_C * q, r = e >> 3, c = e & 7;
+        xv[q] = X[r * XW + 2 * BB + c];
+        ylv[q] = Bw.Y[(size_t)(i - s) * RSZ + e];
+        yrv[q] = has_r ? Bw.Y[(size_t)(i + s) * RSZ + e] : 0.0;
     }
+#pragma unroll
+    for (int s4 = 0; s4 < 16; ++s4) {
+        const double* row = X + (16 * wave + rr) * XW + 4 * s4 + kq;  // XL[16w + rr][4 s4 + kq]
+        al[s4] = row[0];
+        ar[s4] = has_r ? row[BB] : 0.0;
+    }
+    const double rdv = tid < BB ? Bw.rd[(size_t)i * BB + tid] : 0.0;
+    const double blv = border_load(P, S, i, tid);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = tid + TPB_C * q;
+        L.T[(e >> 6) * BLD + (e & 63)] = cf[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = tid + TPB_C * q;
+        L.t[e] = xv[q];
+        L.yl[e] = ylv[q];
+        L.yr[e] = yrv[q];
+    }
+    if (tid < BB) L.rdiag[tid] = rdv;
+    L.Bl[tid] = blv;
     __syncthreads();
-    const int lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
-    if (wave < 4) {
-        d4b acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
+    BCR_STAMP(16 + m, 1);
+    // t -= XL y_l + XR y_r  (wave w: rows 16w..16w+15)
+    {
+        d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
         for (int s4 = 0; s4 < 16; ++s4) {
-            const double bv = rr < RC ? L.yl[(4 * s4 + kk) * RC + rr] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(L.U1[(16 * wave + rr) * BLD + 4 * s4 + kk], bv, acc, 0, 0, 0);
-        }
-        if (has_r) {
-#pragma unroll 4
-            for (int s4 = 0; s4 < 16; ++s4) {
-                const double bv = rr < RC ? L.yr[(4 * s4 + kk) * RC + rr] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(L.U2[(16 * wave + rr) * BLD + 4 * s4 + kk], bv, acc, 0, 0, 0);
-            }
+            const double bl = rr < RC ? L.yl[(4 * s4 + kq) * RC + rr] : 0.0;
+            const double br = rr < RC ? L.yr[(4 * s4 + kq) * RC + rr] : 0.0;
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bl, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s4], br, acc1, 0, 0, 0);
         }
         if (rr < RC)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) L.t[(16 * wave + kk + 4 * g) * RC + rr] -= acc[g];
+            for (int g = 0; g < 4; ++g) L.t[(16 * wave + kq + 4 * g) * RC + rr] -= acc0[g] + acc1[g];
     }
     __syncthreads();
-    BCR_STAMP(7);
-    trsm_lower64_t(L.T, L.rdiag, L.t, RC, RC);
-    Bw.Y[(size_t)i * BB * RC + tid] = L.t[tid];
-    if constexpr (STAMP) {
-        __syncthreads();
-        if (threadIdx.x == 0) stamps[(m * 64 + blockIdx.x % 64) * 8 + 6] = bcr_stamp() - stamps[(m * 64 + blockIdx.x % 64) * 8 + 6];
-        if (threadIdx.x == 0) stamps[(m * 64 + blockIdx.x % 64) * 8 + 7] = bcr_stamp() - stamps[(m * 64 + blockIdx.x % 64) * 8 + 7];
-    }
+    BCR_STAMP(16 + m, 2);
+    trsm_t_lanes(L.T, L.rdiag, L.t);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) Bw.Y[(size_t)i * RSZ + tid + TPB_C * q] = L.t[tid + TPB_C * q];
+    border_partial(L.Bl, L.t, L.red, i, Bw.Bp);
+    BCR_STAMP(16 + m, 3);
 }
 
-// ---- border: C' = S_kk - B^T V, b' = b_k - B^T u ; y_k = C'^-1 b' ; y_a = u - V y_k -> rhs (dense)
-static constexpr int TPB_BD = 256;
+// ---- border: every workgroup sums the border partials in block order and solves the
+// 4x4 system C' y_k = b' (C' = S_kk - B^T V, b' = b_k - B^T u); workgroup i then writes
+// y_a = u - V y_k for the rows of block i into rhs (workgroup 0 also y_k).
+static constexpr int TPB_BD = 64;
 __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict__ st, DevProblem P,
-                                                      const double* __restrict__ S, double* __restrict__ rhs,
-                                                      BcrWork Bw, int* __restrict__ flag) {
+                                                       double* __restrict__ rhs, BcrWork Bw, int* __restrict__ flag) {
     if (st->done) return;
-    __shared__ double red[TPB_BD][20];
+    __shared__ double red[20];
     __shared__ double yk[4];
-    const size_t ld = P.npad;
-    const int nd = 6 * P.nac;
-    const int kb = P.kb;
-    double acc[20];
-#pragma unroll
-    for (int q = 0; q < 20; ++q) acc[q] = 0.0;
-    for (int g = threadIdx.x; g < nd; g += TPB_BD) {
-        const int blk = g / G_DOF, r = g % G_DOF;
-        const double* y = Bw.Y + ((size_t)blk * BB + r) * RC;
-        double bm[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) bm[m] = S[(size_t)(kb + m) * ld + g];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-#pragma unroll
-            for (int l = 0; l < 4; ++l) acc[m * 4 + l] += bm[m] * y[1 + l];  // (B^T V)[m][l]
-            acc[16 + m] += bm[m] * y[0];                                    // (B^T u)[m]
-        }
+    const int tid = threadIdx.x;
+    if (tid < 20) {
+        double acc = 0.0;
+        for (int b = 0; b < Bw.nblk; ++b) acc += Bw.Bp[(size_t)b * 32 + tid];
+        red[tid] = acc;
     }
-#pragma unroll
-    for (int q = 0; q < 20; ++q) red[threadIdx.x][q] = acc[q];
     __syncthreads();
-    for (int w = TPB_BD / 2; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w)
-#pragma unroll
-            for (int q = 0; q < 20; ++q) red[threadIdx.x][q] += red[threadIdx.x + w][q];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         double Cm[16], bp[4];
-        for (int m = 0; m < 4; ++m) {
-            for (int l = 0; l < 4; ++l) {
-                const double s_ml = (m >= l) ? S[(size_t)(kb + m) * ld + kb + l] : S[(size_t)(kb + l) * ld + kb + m];
-                Cm[m * 4 + l] = s_ml - red[0][m * 4 + l];
+        int q = 0;
+        for (int mm = 0; mm < 4; ++mm)
+            for (int l = 0; l <= mm; ++l, ++q) {
+                const double v = Bw.bk[4 + q];
+                Cm[mm * 4 + l] = v - red[mm * 5 + 1 + l];
+                Cm[l * 4 + mm] = v - red[l * 5 + 1 + mm];
             }
-            bp[m] = rhs[kb + m] - red[0][16 + m];
-        }
-        // 4x4 Cholesky solve
+        for (int mm = 0; mm < 4; ++mm) bp[mm] = Bw.bk[mm] - red[mm * 5];
         bool bad = false;
         double Lm[16] = {0};
         for (int j = 0; j < 4; ++j) {
@@ -539,33 +601,34 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
             for (int k = 0; k < j; ++k) d -= Lm[j * 4 + k] * Lm[j * 4 + k];
             if (!(d > 0.0)) { bad = true; d = 1.0; }
             Lm[j * 4 + j] = sqrt(d);
-            for (int i = j + 1; i < 4; ++i) {
-                double v = Cm[i * 4 + j];
-                for (int k = 0; k < j; ++k) v -= Lm[i * 4 + k] * Lm[j * 4 + k];
-                Lm[i * 4 + j] = v / Lm[j * 4 + j];
+            for (int r = j + 1; r < 4; ++r) {
+                double v = Cm[r * 4 + j];
+                for (int k = 0; k < j; ++k) v -= Lm[r * 4 + k] * Lm[j * 4 + k];
+                Lm[r * 4 + j] = v / Lm[j * 4 + j];
             }
         }
         double z[4];
-        for (int i = 0; i < 4; ++i) {
-            double v = bp[i];
-            for (int k = 0; k < i; ++k) v -= Lm[i * 4 + k] * z[k];
-            z[i] = v / Lm[i * 4 + i];
+        for (int r = 0; r < 4; ++r) {
+            double v = bp[r];
+            for (int k = 0; k < r; ++k) v -= Lm[r * 4 + k] * z[k];
+            z[r] = v / Lm[r * 4 + r];
         }
-        for (int i = 3; i >= 0; --i) {
-            double v = z[i];
-            for (int k = i + 1; k < 4; ++k) v -= Lm[k * 4 + i] * z[k];
-            z[i] = v / Lm[i * 4 + i];
+        for (int r = 3; r >= 0; --r) {
+            double v = z[r];
+            for (int k = r + 1; k < 4; ++k) v -= Lm[k * 4 + r] * z[k];
+            z[r] = v / Lm[r * 4 + r];
         }
-        for (int m = 0; m < 4; ++m) yk[m] = z[m];
-        if (bad) *flag = 1;
+        for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
+        if (bad && blockIdx.x == 0) *flag = 1;
     }
     __syncthreads();
-    for (int g = threadIdx.x; g < nd; g += TPB_BD) {
-        const int blk = g / G_DOF, r = g % G_DOF;
-        const double* y = Bw.Y + ((size_t)blk * BB + r) * RC;
-        rhs[g] = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
+    const int i = blockIdx.x;
+    const int b0 = i * G_DOF, nd = 6 * P.nac;
+    if (tid < G_DOF && b0 + tid < nd) {
+        const double* y = Bw.Y + (size_t)i * RSZ + tid * RC;
+        rhs[b0 + tid] = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
     }
-    if (threadIdx.x < 4) rhs[kb + threadIdx.x] = yk[threadIdx.x];
+    if (i == 0 && tid < 4) rhs[P.kb + tid] = yk[tid];
 }
 
 #define CKB(x)                            \
@@ -574,27 +637,33 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
         if (e_ != hipSuccess) return e_;  \
     } while (0)
 
+static inline int n_elim(int nblk, int m) {
+    const int s = 1 << m;
+    return (nblk - s + 2 * s - 1) / (2 * s);
+}
+
 template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps) {
     const int nblk = Bw.nblk;
     for (int m = 0; m < Bw.levels; ++m) {
-        const int st = 1 << m;
-        const int nel = (nblk - st + 2 * st - 1) / (2 * st);
-        hipLaunchKernelGGL(k_bcr_elim<STAMP>, dim3(nel), dim3(TPB_B), sizeof(ElimLds), s, W.st, P, W.S, W.rhs, Bw, m,
-                           W.chol_flag, stamps);
+        const int nel = n_elim(nblk, m);
+        const int nacc = m >= 1 ? (nblk + (2 << m) - 1) / (2 << m) : 0;
+        hipLaunchKernelGGL(k_bcr_elim<STAMP>, dim3(nel + nacc), dim3(TPB_E), sizeof(ElimLds), s, W.st, P, W.S, W.rhs,
+                           Bw, m, nel, W.chol_flag, stamps);
+        CKB(hipGetLastError());
+        hipLaunchKernelGGL(k_bcr_contrib, dim3(nel * NCONTRIB_WG), dim3(TPB_C), 0, s, W.st, Bw, m);
         CKB(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_bcr_elim<STAMP>, dim3(1), dim3(TPB_B), sizeof(ElimLds), s, W.st, P, W.S, W.rhs, Bw, Bw.levels,
-                       W.chol_flag, stamps);
+    hipLaunchKernelGGL(k_bcr_elim<STAMP>, dim3(1), dim3(TPB_E), sizeof(ElimLds), s, W.st, P, W.S, W.rhs, Bw, Bw.levels,
+                       1, W.chol_flag, stamps);
     CKB(hipGetLastError());
     for (int m = Bw.levels - 1; m >= 0; --m) {
-        const int st = 1 << m;
-        const int nel = (nblk - st + 2 * st - 1) / (2 * st);
-        hipLaunchKernelGGL(k_bcr_back<STAMP>, dim3(nel), dim3(TPB_B), sizeof(BackLds), s, W.st, Bw, m, stamps);
+        hipLaunchKernelGGL(k_bcr_back<STAMP>, dim3(n_elim(nblk, m)), dim3(TPB_C), sizeof(BackLds), s, W.st, P, W.S, Bw,
+                           m, stamps);
         CKB(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_bcr_border, dim3(1), dim3(TPB_BD), 0, s, W.st, P, W.S, W.rhs, Bw, W.chol_flag);
+    hipLaunchKernelGGL(k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
     CKB(hipGetLastError());
     return hipSuccess;
 }
@@ -609,21 +678,22 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         const char* e = getenv("MIBA_BCR_STAMPS");
-        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * 16 * 64 * 8));
+        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * 32 * 8));
         attr = true;
     }
     if (pf) pf->begin(K_CHOL, s);
     if (stamps) {
-        CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 16 * 64 * 8, s));
+        CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 32 * 8, s));
         CKB(launch_bcr_t<true>(P, W, Bw, s, stamps));
-        static unsigned long long h[16 * 64 * 8];
+        static unsigned long long h[32 * 8];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
         for (int m = 0; m <= Bw.levels; ++m) {
-            const unsigned long long* q = h + (size_t)m * 64 * 8;
-            if (!q[0]) continue;
-            fprintf(stderr, "bcr level %d blk0 cycles: load %llu potrf %llu trsm %llu store %llu contrib %llu | back %llu (trsm %llu)\n", m,
-                    q[1] - q[0], q[2] - q[1], q[3] - q[2], q[4] - q[3], q[5] ? q[5] - q[4] : 0ull, q[6], q[7]);
+            const unsigned long long* q = h + (size_t)m * 8;
+            const unsigned long long* b = h + (size_t)(16 + m) * 8;
+            fprintf(stderr, "bcr level %d blk0 cycles: elim load %llu factor+fwd %llu store %llu | back load %llu gemv %llu trsm+store %llu\n",
+                    m, q[1] - q[0], q[2] - q[1], q[3] - q[2], b[0] ? b[1] - b[0] : 0ull, b[0] ? b[2] - b[1] : 0ull,
+                    b[0] ? b[3] - b[2] : 0ull);
         }
     } else {
         CKB(launch_bcr_t<false>(P, W, Bw, s, nullptr));

@@ -80,21 +80,26 @@ struct DevProblem {
     int solver;    // 0 dense envelope, 1 band, 2 block cyclic reduction
 };
 
-// Block cyclic reduction workspace (ba_bcr.hip): nblk blocks of BCR_CAMS cameras (64 dofs).
+// Block cyclic reduction (ba_bcr.hip): nblk blocks of BCR_CAMS cameras (64 dofs).
 static constexpr int BCR_CAMS = 10;
-// Block cyclic reduction workspace, per 64-dof block i (see ba_bcr.hip):
-//   Cf   Cholesky factor of the block at its elimination      64x64
-//   XL   Cf^-1 A[i][i-s]   XR  Cf^-1 A[i][i+s]                 64x64 each
-//   UL   XL^T XL  (Schur contribution to the left survivor)    64x64 (lower tiles)
-//   UR   XR^T XR  (to the right survivor)                      64x64 (lower tiles)
-//   F    -XR^T XL (fill coupling right survivor -> left one)   64x64
-//   x    Cf^-1 R_i, Y solution, rL = XL^T x, rR = XR^T x        64x8 each
-//   rd   1 / diag(Cf)                                          64
+// Block cyclic reduction workspace, per 64-dof block i:
+//   Cf   Cholesky factor of the block at its elimination                  64x64
+//   X    [XL | XR | x] = Cf^-1 [A[i][i-s] | A[i][i+s] | R_i]              64x136
+//   UL   XL^T XL  (Schur contribution to the left survivor, lower tiles) 64x64
+//   UR   XR^T XR  (to the right survivor, lower tiles)                    64x64
+//   F    -XR^T XL (fill coupling right survivor -> left one)              64x64
+//   rL   XL^T x, rR = XR^T x                                              64x8 each
+//   Dacc, Racc  survivor's diagonal block / rhs with the contributions of
+//               all levels <= its elimination level - 2 folded in         64x64, 64x8
+//   Y    solution rows [u | V]                                            64x8
+//   Bp   border partial B_i^T Y_i (4x5)                                   32
+//   rd   1 / diag(Cf)                                                     64
+// plus one global slot: bk = [b_k (4) | S_kk lower (10)].
 struct BcrWork {
-    double *Cf, *XL, *XR, *UL, *UR, *F, *x, *Y, *rL, *rR, *rd;
+    double *Cf, *X, *UL, *UR, *F, *rL, *rR, *Dacc, *Racc, *Y, *Bp, *rd, *bk;
     int nblk, levels;
 };
-static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)6 * 64 * 64 + 4 * 64 * 8 + 64;
+static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)5 * 64 * 64 + 64 * 136 + 4 * 64 * 8 + 32 + 64;
 
 // Device-resident Levenberg-Marquardt state (Ceres 2.0 TrustRegionMinimizer +
 // LevenbergMarquardtStrategy bookkeeping, owned by k_lm_decide).

@@ -485,7 +485,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     }
     if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
     if (P.solver == 2) {
-        const size_t bytes = sizeof(double) * BCR_BLOCK_DOUBLES * bcr_nblk;
+        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
         // upper tiles of UL/UR are never written and must read as zero
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
@@ -496,16 +496,18 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         while ((1 << Bw.levels) < bcr_nblk) ++Bw.levels;
         const size_t b64 = (size_t)64 * 64 * bcr_nblk, b8 = (size_t)64 * 8 * bcr_nblk;
         Bw.Cf = base;
-        Bw.XL = Bw.Cf + b64;
-        Bw.XR = Bw.XL + b64;
-        Bw.UL = Bw.XR + b64;
+        Bw.X = Bw.Cf + b64;
+        Bw.UL = Bw.X + (size_t)64 * 136 * bcr_nblk;
         Bw.UR = Bw.UL + b64;
         Bw.F = Bw.UR + b64;
-        Bw.x = Bw.F + b64;
-        Bw.Y = Bw.x + b8;
-        Bw.rL = Bw.Y + b8;
+        Bw.Dacc = Bw.F + b64;
+        Bw.rL = Bw.Dacc + b64;
         Bw.rR = Bw.rL + b8;
-        Bw.rd = Bw.rR + b8;
+        Bw.Racc = Bw.rR + b8;
+        Bw.Y = Bw.Racc + b8;
+        Bw.Bp = Bw.Y + b8;
+        Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
+        Bw.bk = Bw.rd + (size_t)64 * bcr_nblk;
     }
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
