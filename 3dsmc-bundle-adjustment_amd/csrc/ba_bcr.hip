@@ -121,8 +121,20 @@ __device__ __forceinline__ void fwd16(double v[16], const double* Lkk, const dou
 // (1) wave 0 factors the diagonal tile, (2) the panel rows below it and the X columns
 // run their 16-step substitution in the same phase, (3) the trailing updates of T and
 // of X share one MFMA phase.
-__device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, bool& bad) {
+template <bool STAMP = false>
+__device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, bool& bad,
+                            unsigned long long* pst = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long tp = 0;
+    if constexpr (STAMP) if (tid == 0 && pst) tp = bcr_stamp();
+#define PF_STAMP(k)                                                        \
+    do {                                                                   \
+        if constexpr (STAMP) if (tid == 0 && pst) {                        \
+            const unsigned long long t_ = bcr_stamp();                     \
+            pst[k] += t_ - tp;                                             \
+            tp = t_;                                                       \
+        }                                                                  \
+    } while (0)
     const int rr = lane & 15, kk = lane >> 4;
     const int ncb = (ncol + 15) >> 4;
     for (int kb = 0; kb < 4; ++kb) {
@@ -130,6 +142,7 @@ __device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, boo
         const double* rd = rdiag64 + 16 * kb;
         if (wave == 0) potrf16_tile(Tkk, BLD, rdiag64 + 16 * kb, lane, bad);
         __syncthreads();
+        PF_STAMP(0);
         const int nrow = 48 - 16 * kb;
         if (tid < nrow) {
             double* row = T + (16 * (kb + 1) + tid) * BLD + 16 * kb;
@@ -149,6 +162,7 @@ __device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, boo
             for (int j = 0; j < 16; ++j) col[j * XW] = v[j];
         }
         __syncthreads();
+        PF_STAMP(1);
         // trailing: T tiles (i, j), kb < j <= i, then X tiles (i > kb, cb)
         const int nt = 3 - kb;
         const int npairs = nt * (nt + 1) / 2;
@@ -190,7 +204,9 @@ __device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, boo
                 for (int g = 0; g < 4; ++g) C[(kk + 4 * g) * ldc + rr] -= acc[g];
         }
         __syncthreads();
+        PF_STAMP(2);
     }
+#undef PF_STAMP
 }
 
 // X <- L^-T X (backward), L 64x64 lower in LDS (stride BLD), X 64 x ncol (LDS, stride ldx).
@@ -392,7 +408,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
     __syncthreads();
     BCR_STAMP(m, 1);
     bool bad = false;
-    potrf64_fwd(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad);
+    potrf64_fwd<STAMP>(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad,
+                       STAMP && blockIdx.x == 0 ? stamps + 8 * 24 + 4 * m : nullptr);
     if (bad) *flag = 1;
     BCR_STAMP(m, 2);
     if (root) {
@@ -642,29 +659,31 @@ static inline int n_elim(int nblk, int m) {
     return (nblk - s + 2 * s - 1) / (2 * s);
 }
 
+#define BPL(kid, ...)                     \
+    do {                                  \
+        if (pf) pf->begin(kid, s);        \
+        hipLaunchKernelGGL(__VA_ARGS__);  \
+        if (pf) pf->end(s);               \
+        CKB(hipGetLastError());           \
+    } while (0)
+
 template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
-                               unsigned long long* stamps) {
+                               unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
     for (int m = 0; m < Bw.levels; ++m) {
         const int nel = n_elim(nblk, m);
         const int nacc = m >= 1 ? (nblk + (2 << m) - 1) / (2 << m) : 0;
-        hipLaunchKernelGGL(k_bcr_elim<STAMP>, dim3(nel + nacc), dim3(TPB_E), sizeof(ElimLds), s, W.st, P, W.S, W.rhs,
-                           Bw, m, nel, W.chol_flag, stamps);
-        CKB(hipGetLastError());
-        hipLaunchKernelGGL(k_bcr_contrib, dim3(nel * NCONTRIB_WG), dim3(TPB_C), 0, s, W.st, Bw, m);
-        CKB(hipGetLastError());
+        BPL(K_BCR_ELIM, k_bcr_elim<STAMP>, dim3(nel + nacc), dim3(TPB_E), sizeof(ElimLds), s, W.st, P, W.S, W.rhs, Bw, m,
+            nel, W.chol_flag, stamps);
+        BPL(K_BCR_CONTRIB, k_bcr_contrib, dim3(nel * NCONTRIB_WG), dim3(TPB_C), 0, s, W.st, Bw, m);
     }
-    hipLaunchKernelGGL(k_bcr_elim<STAMP>, dim3(1), dim3(TPB_E), sizeof(ElimLds), s, W.st, P, W.S, W.rhs, Bw, Bw.levels,
-                       1, W.chol_flag, stamps);
-    CKB(hipGetLastError());
-    for (int m = Bw.levels - 1; m >= 0; --m) {
-        hipLaunchKernelGGL(k_bcr_back<STAMP>, dim3(n_elim(nblk, m)), dim3(TPB_C), sizeof(BackLds), s, W.st, P, W.S, Bw,
-                           m, stamps);
-        CKB(hipGetLastError());
-    }
-    hipLaunchKernelGGL(k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
-    CKB(hipGetLastError());
+    BPL(K_BCR_ELIM, k_bcr_elim<STAMP>, dim3(1), dim3(TPB_E), sizeof(ElimLds), s, W.st, P, W.S, W.rhs, Bw, Bw.levels, 1,
+        W.chol_flag, stamps);
+    for (int m = Bw.levels - 1; m >= 0; --m)
+        BPL(K_BCR_BACK, k_bcr_back<STAMP>, dim3(n_elim(nblk, m)), dim3(TPB_C), sizeof(BackLds), s, W.st, P, W.S, Bw, m,
+            stamps);
+    BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
     return hipSuccess;
 }
 
@@ -678,27 +697,26 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         const char* e = getenv("MIBA_BCR_STAMPS");
-        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * 32 * 8));
+        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * 32 * 8 * 2));
         attr = true;
     }
-    if (pf) pf->begin(K_CHOL, s);
     if (stamps) {
-        CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 32 * 8, s));
-        CKB(launch_bcr_t<true>(P, W, Bw, s, stamps));
-        static unsigned long long h[32 * 8];
+        CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 32 * 8 * 2, s));
+        CKB(launch_bcr_t<true>(P, W, Bw, s, stamps, nullptr));
+        static unsigned long long h[32 * 8 * 2];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
         for (int m = 0; m <= Bw.levels; ++m) {
             const unsigned long long* q = h + (size_t)m * 8;
             const unsigned long long* b = h + (size_t)(16 + m) * 8;
-            fprintf(stderr, "bcr level %d blk0 cycles: elim load %llu factor+fwd %llu store %llu | back load %llu gemv %llu trsm+store %llu\n",
-                    m, q[1] - q[0], q[2] - q[1], q[3] - q[2], b[0] ? b[1] - b[0] : 0ull, b[0] ? b[2] - b[1] : 0ull,
-                    b[0] ? b[3] - b[2] : 0ull);
+            const unsigned long long* f = h + 8 * 24 + 4 * m;
+            fprintf(stderr, "bcr level %d blk0 cycles: elim load %llu factor+fwd %llu [potrf16 %llu fwd16 %llu trailing %llu] store %llu | back load %llu gemv %llu trsm+store %llu\n",
+                    m, q[1] - q[0], q[2] - q[1], f[0], f[1], f[2], q[3] - q[2], b[0] ? b[1] - b[0] : 0ull,
+                    b[0] ? b[2] - b[1] : 0ull, b[0] ? b[3] - b[2] : 0ull);
         }
     } else {
-        CKB(launch_bcr_t<false>(P, W, Bw, s, nullptr));
+        CKB(launch_bcr_t<false>(P, W, Bw, s, nullptr, pf));
     }
-    if (pf) pf->end(s);
     return hipSuccess;
 }
 

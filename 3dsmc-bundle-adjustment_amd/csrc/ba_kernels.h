@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "ba_comm.h"
 #include "ba_device.h"
 
 namespace miba {
@@ -78,6 +79,7 @@ struct DevProblem {
     int band_w;  // 16x16 tiles below the diagonal in the camera band; <=0 or >6: dense envelope kernel
     int cam_band;  // max over active cameras of (camera - first co-visible camera)
     int solver;    // 0 dense envelope, 1 band, 2 block cyclic reduction
+    int rank, nranks;  // landmark shard of this context (ba_comm_init); rank 0 adds the camera/intrinsics terms
 };
 
 // Block cyclic reduction (ba_bcr.hip): nblk blocks of BCR_CAMS cameras (64 dofs).
@@ -137,29 +139,45 @@ struct DevWork {
     LmState* st;
     double* log;  // [(max_iter + 2) * LOG_W]
     BcrWork bcr;
+    // landmark sharding (nranks > 1): this rank's camera-side partials, the packed envelope
+    // of S (+ rhs) before / after the all-reduce, and the step-scalar exchange buffer
+    Comm comm;
+    double* camdata_loc;   // [nac * CAMDATA + 16]; == camdata when unsharded
+    const int2* env_tile;  // (block row, block col) of every 16x16 envelope tile of S
+    int n_env;
+    double* env_loc;       // [n_env * 256 + npad]
+    double* env_glob;
+    double* red;           // [32]: 0..3 local sums, 4..5 local maxima, 6..9 replicated sums, 10 chol flag,
+                           //       16..19 global sums, 20..21 global maxima
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
-    K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_COUNT
+    K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
-    "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm"};
+    "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
+    "bcr_back", "bcr_border", "comm"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {
-    static constexpr int MAXP = 160;
+    static constexpr int MAXP = 640;
     int on = 0;
     int n = 0;
     int id[MAXP];
     hipEvent_t ev[2 * MAXP];
+    unsigned mask = 0;  // bit k: record kernel id k (0 = every kernel)
+    bool open_ = false;
     void begin(int k, hipStream_t s) {
-        if (on && n < MAXP) { (void)hipEventRecord(ev[2 * n], s); id[n] = k; }
+        open_ = on && n < MAXP && (mask == 0 || ((mask >> k) & 1u));
+        if (open_) { (void)hipEventRecord(ev[2 * n], s); id[n] = k; }
     }
     void end(hipStream_t s) {
-        if (on && n < MAXP) { (void)hipEventRecord(ev[2 * n + 1], s); ++n; }
+        if (open_) { (void)hipEventRecord(ev[2 * n + 1], s); ++n; }
+        open_ = false;
     }
 };
 

@@ -124,22 +124,35 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
 // (OptimizationUtils.cpp:117-125, squared loss), compute the gradient max-norm of
 // cameras + intrinsics: ||x - Plus(x, -g)||_inf (Ceres 2.0 trust_region_minimizer).
 // lin[0] = cost(x), lin[1] = gmax(cams, intr), lin[2..12) = Ukk packed, lin[12..16) = gk
+// mode 0: unsharded. mode 1 (sharded, before the all-reduce): only the fixed-order sum of
+// this rank's segment partials -> linpart[0..SEGINTR). mode 2 (after the all-reduce): the
+// summed partials are read from linpart and the rest runs as in mode 0.
 __global__ __launch_bounds__(TPB) void k_lin_finalize(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
                                                       const double* __restrict__ camdata,
-                                                      const double* __restrict__ seg_intr, double* __restrict__ lin) {
+                                                      const double* __restrict__ seg_intr, double* __restrict__ lin,
+                                                      int mode, double* __restrict__ linpart) {
     if (st->done || (gated && !st->need_lin)) return;
     const int cur = st->cur;
     __shared__ double lds[4 * SEGINTR];
     __shared__ double out[SEGINTR];
     __shared__ double red[4];
-    double acc[SEGINTR];
+    if (mode == 2) {
+        if (threadIdx.x < SEGINTR) out[threadIdx.x] = linpart[threadIdx.x];
+        __syncthreads();
+    } else {
+        double acc[SEGINTR];
 #pragma unroll
-    for (int i = 0; i < SEGINTR; ++i) acc[i] = 0.0;
-    // fixed-order: each thread sums a strided subset; block_sum order is fixed too
-    for (int s = threadIdx.x; s < P.n_seg; s += TPB)
+        for (int i = 0; i < SEGINTR; ++i) acc[i] = 0.0;
+        // fixed-order: each thread sums a strided subset; block_sum order is fixed too
+        for (int s = threadIdx.x; s < P.n_seg; s += TPB)
 #pragma unroll
-        for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)s * SEGINTR + i];
-    block_sum<SEGINTR>(acc, lds, out);
+            for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)s * SEGINTR + i];
+        block_sum<SEGINTR>(acc, lds, out);
+        if (mode == 1) {
+            if (threadIdx.x < SEGINTR) linpart[threadIdx.x] = out[threadIdx.x];
+            return;
+        }
+    }
     const double* K = P.K[cur];
     double gm = 0.0;
     for (int ac = threadIdx.x; ac < P.nac; ac += TPB) {
@@ -1423,6 +1436,82 @@ __global__ __launch_bounds__(TPB) void k_final(DevProblem P, const LmState* __re
     }
 }
 
+// ---------------------------------------------------------------- landmark sharding
+// Zero n doubles (gated: only when the window is re-linearised).
+__global__ void k_zero_gated(const LmState* __restrict__ st, int gated, double* __restrict__ p, size_t n) {
+    if (st->done || (gated && !st->need_lin)) return;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = 0.0;
+}
+// Envelope of S (its 16x16 tiles) + rhs <-> one contiguous buffer for the all-reduce.
+// unpack == 0: S, rhs -> buf; unpack == 1: buf -> S, rhs.
+__global__ __launch_bounds__(TPB) void k_env_pack(const LmState* __restrict__ st, const int2* __restrict__ tiles, int n_env,
+                                                  int npad, double* __restrict__ S, double* __restrict__ rhs,
+                                                  double* __restrict__ buf, int unpack) {
+    if (st->done) return;
+    const int t = blockIdx.x;
+    if (t < n_env) {
+        const int2 ij = tiles[t];
+        const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;
+        double* sp = S + (size_t)(16 * ij.x + r) * npad + 16 * ij.y + cc;
+        double* bp = buf + (size_t)t * 256 + threadIdx.x;
+        if (unpack) *sp = *bp; else *bp = *sp;
+    } else {
+        for (int i = threadIdx.x; i < npad; i += TPB) {
+            double* bp = buf + (size_t)n_env * 256 + i;
+            if (unpack) rhs[i] = *bp; else *bp = rhs[i];
+        }
+    }
+}
+// Sharded k_final: this rank's point-side sums / maxima and the (replicated) camera-side
+// sums go to red[] for the all-reduce; k_combine assembles scal[] from the reduced values.
+__global__ __launch_bounds__(TPB) void k_final_shard(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
+                                                     int nblk_upd, int nblk_bs, const double* __restrict__ part,
+                                                     const int* __restrict__ chol_flag, double* __restrict__ red) {
+    __shared__ double lds[4 * 8];
+    __shared__ double out[8];
+    __shared__ double rl[4];
+    if (st->done) return;
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // 0..3 local, 4..7 replicated
+    double gm = 0.0, bad = 0.0;
+    const size_t stp = P.part_stride;
+    for (int i = threadIdx.x; i < nblk_upd; i += TPB) {
+        acc[4] += part[PART_UPD_SN2 * stp + i];
+        acc[5] += part[PART_UPD_MCC * stp + i];
+        acc[6] += part[PART_UPD_COST * stp + i];
+        acc[7] += part[PART_UPD_XN2 * stp + i];
+    }
+    for (int i = threadIdx.x; i < nblk_bs; i += TPB) {
+        acc[0] += part[PART_BS_SN2 * stp + i];
+        acc[1] += part[PART_BS_MCC * stp + i];
+        acc[2] += part[PART_BS_COST * stp + i];
+        acc[3] += part[PART_BS_XN2 * stp + i];
+        bad = fmax(bad, part[PART_BS_BAD * stp + i]);
+    }
+    for (int i = threadIdx.x; i < nblk_pt; i += TPB) {
+        gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
+        bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
+    }
+    block_sum<8>(acc, lds, out);
+    gm = block_max(gm, rl);
+    bad = block_max(bad, rl);
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 4; ++i) red[i] = out[i];
+        red[4] = gm;
+        red[5] = bad;
+        for (int i = 0; i < 4; ++i) red[6 + i] = out[4 + i];
+        red[10] = *chol_flag ? 4.0 : 0.0;
+    }
+}
+__global__ void k_combine(const LmState* __restrict__ st, const double* __restrict__ red, double* __restrict__ scal) {
+    if (st->done || threadIdx.x != 0) return;
+    scal[SC_SN2] = red[16 + 0] + red[6];
+    scal[SC_MCC] = red[16 + 1] + red[7];
+    scal[SC_CAND] = red[16 + 2] + red[8];
+    scal[SC_XN2] = red[16 + 3] + red[9];
+    scal[SC_GMAX_PT] = red[20];
+    scal[SC_BAD] = red[21] + red[10];
+}
+
 // ---------------------------------------------------------------- LM control
 // |x|^2 of the active parameter blocks (ambient) -> initial state; called once after
 // the iteration-0 linearisation (lin[0] = cost, lin[1] = gmax of cams+intrinsics).
@@ -1435,7 +1524,7 @@ __global__ __launch_bounds__(TPB) void k_xnorm_part(DevProblem P, const LmState*
     const int cur = st->cur;
     double a[1] = {0.0};
     const int t = blockIdx.x * TPB + threadIdx.x;
-    if (t < P.nac) {
+    if (t < P.nac && P.rank == 0) {  // cameras are replicated: counted once
         const double* x = P.cams[cur] + 7 * P.ac_cam[t];
 #pragma unroll
         for (int j = 0; j < 7; ++j) a[0] += x[j] * x[j];
@@ -1459,7 +1548,7 @@ __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* 
     block_sum<1>(a, lds, out);
     if (threadIdx.x == 0) {
         const double* K = P.K[cur];
-        st->xnorm2 = out[0] + K[0] * K[0] + K[1] * K[1] + K[2] * K[2] + K[3] * K[3];
+        st->xnorm2 = out[0] + (P.rank == 0 ? K[0] * K[0] + K[1] * K[1] + K[2] * K[2] + K[3] * K[3] : 0.0);
         st->x_cost = lin[0];
         st->initial_cost = lin[0];
         st->final_cost = lin[0];
@@ -1605,10 +1694,34 @@ static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
         CK(hipGetLastError());              \
     } while (0)
 
+// all-reduce on the solver stream, timed as K_COMM
+#define COMM(send, recv, n, t, op)                                             \
+    do {                                                                        \
+        if (pf) pf->begin(K_COMM, s);                                           \
+        CK(comm_allreduce(W.comm, (send), (recv), (n), (t), (op), s));          \
+        if (pf) pf->end(s);                                                     \
+    } while (0)
+
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
+    if (!W.comm.on()) {
+        if (P.n_seg > 0)
+            PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr);
+        PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin, 0,
+           (double*)nullptr);
+        return hipSuccess;
+    }
+    // sharded: this rank's camera-side partials -> camdata_loc (cameras without local
+    // observations stay zero), one all-reduce of [camdata | intrinsics partials], finalize
+    const size_t ncd = (size_t)P.nac * CAMDATA;
+    PL(K_CAM_SIDE, k_zero_gated, dim3(nblocks((int)std::min<size_t>(ncd, 1 << 20), TPB)), dim3(TPB), 0, s, W.st, gated,
+       W.camdata_loc, ncd);
     if (P.n_seg > 0)
-        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr);
-    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin);
+        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_loc, W.seg_intr);
+    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_loc, W.seg_intr, W.lin, 1,
+       W.camdata_loc + ncd);
+    COMM(W.camdata_loc, W.camdata, ncd + SEGINTR, COMM_F64, COMM_SUM);
+    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin, 2,
+       W.camdata + ncd);
     return hipSuccess;
 }
 
@@ -1625,6 +1738,7 @@ hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Pro
     const int nparts = nblocks(std::max(P.nac, P.n_ap), TPB);
     PL(K_XNORM, k_xnorm_part, dim3(nparts), dim3(TPB), 0, s, P, W.st, W.part);
     PL(K_XNORM, k_xnorm_init, dim3(1), dim3(TPB), 0, s, P, W.lin, W.st, W.log, W.part, nparts);
+    if (W.comm.on()) COMM(&W.st->xnorm2, &W.st->xnorm2, 1, COMM_F64, COMM_SUM);  // points of all shards
     return hipSuccess;
 }
 
@@ -1633,8 +1747,12 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     CK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
     CK(hipMemsetAsync(W.chol_flag, 0, sizeof(int), s));
     if (pf) pf->end(s);
-    PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, W.st, W.camdata, W.lin, W.scale,
-       W.S, W.rhs);
+    if (P.rank == 0) {  // camera / intrinsics blocks, LM diagonal, pad: once over the shards
+        PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, W.st, W.camdata, W.lin, W.scale,
+           W.S, W.rhs);
+    } else {
+        CK(hipMemsetAsync(W.rhs, 0, sizeof(double) * P.npad, s));
+    }
     if (P.n_ap > 0)
         PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, W.st, 1, W.scale, W.cnp,
            W.pdata, W.S, W.rhs, W.part);
@@ -1674,6 +1792,14 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     if (P.n_ovf_obs > 0)
         PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata,
            W.S, W.rhs);
+    if (W.comm.on()) {  // S = sum over the landmark shards: envelope tiles + rhs
+        const size_t ne = (size_t)W.n_env * 256 + P.npad;
+        PL(K_COMM, k_env_pack, dim3(W.n_env + 1), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs,
+           W.env_loc, 0);
+        COMM(W.env_loc, W.env_glob, ne, COMM_F64, COMM_SUM);
+        PL(K_COMM, k_env_pack, dim3(W.n_env + 1), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs,
+           W.env_glob, 1);
+    }
     return hipSuccess;
 }
 
@@ -1729,8 +1855,17 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hip
     if (P.n_ap > 0)
         PL(K_BACKSUB_EVAL, k_backsub_eval, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part);
-    PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, W.st, P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0, nb_upd,
-       P.n_ap > 0 ? nb_bs : 0, W.part, W.chol_flag, W.scal);
+    const int nb_pt = P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0;
+    if (!W.comm.on()) {
+        PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
+           W.chol_flag, W.scal);
+        return hipSuccess;
+    }
+    PL(K_FINAL, k_final_shard, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
+       W.chol_flag, W.red);
+    COMM(W.red, W.red + 16, 4, COMM_F64, COMM_SUM);
+    COMM(W.red + 4, W.red + 20, 2, COMM_F64, COMM_MAX);
+    PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal);
     return hipSuccess;
 }
 

@@ -57,7 +57,7 @@ enum BufId {
     B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PO_PT, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_ENV_GLOB, B_RED, B_PREP, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3,
     B_COUNT
 };
@@ -80,6 +80,7 @@ struct ba_context {
     int nblk_pt = 0;
     bool prepared = false;
     int n_tiles = 0, n_ovf_obs = 0, n_tiled_pts = 0;
+    int n_adm_all = 0;  // admissible observations over all landmark shards
     int prep_nc = -1, prep_np = -1, prep_no = -1;
     // per-kernel profiling
     Prof prof;
@@ -120,6 +121,22 @@ static hipError_t upload(ba_context* ctx, int id, const T* src, size_t n) {
     if (e != hipSuccess) return e;
     if (n) e = hipMemcpyAsync(ctx->buf[id].p, src, sizeof(T) * n, hipMemcpyHostToDevice, ctx->stream);
     return e;
+}
+
+// Host-side all-reduce of a small int32 array across the landmark shards (prepare time).
+static int host_allreduce_i32(ba_context* ctx, int* v, size_t n, CommOp op) {
+    if (!ctx->W.comm.on() || n == 0) return BA_OK;
+    if (ctx->buf[B_PREP].ensure(sizeof(int) * n) != hipSuccess) { ctx->err = "prepare scratch allocation failed"; return BA_E_NOMEM; }
+    int* d = ctx->buf[B_PREP].as<int>();
+    hipStream_t s = ctx->stream;
+    if (hipMemcpyAsync(d, v, sizeof(int) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        comm_allreduce(ctx->W.comm, d, d, n, COMM_I32, op, s) != hipSuccess ||
+        hipMemcpyAsync(v, d, sizeof(int) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        ctx->err = std::string("landmark-shard all-reduce failed: ") + comm_last_error();
+        return BA_E_COMM;
+    }
+    return BA_OK;
 }
 
 extern "C" {
@@ -182,6 +199,7 @@ ba_context* ba_create(const ba_options* opts) {
         for (int i = 0; i < 2 * Prof::MAXP && e == hipSuccess; ++i) e = hipEventCreate(&ctx->prof.ev[i]);
         ctx->prof_events = (e == hipSuccess);
         ctx->prof.on = 1;
+        ctx->prof.mask = (unsigned)ctx->opts.profile_mask;
     }
     if (e != hipSuccess) {
         g_err = std::string("HIP init failed: ") + hipGetErrorString(e);
@@ -195,6 +213,7 @@ void ba_destroy(ba_context* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    comm_destroy(ctx->W.comm);
     for (auto& b : ctx->buf) b.release();
     for (auto& e : ctx->ev)
         if (e) hipEventDestroy(e);
@@ -205,6 +224,26 @@ void ba_destroy(ba_context* ctx) {
 }
 
 const char* ba_last_error(const ba_context* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int32_t ba_comm_unique_id(uint8_t id[BA_COMM_ID_BYTES]) {
+    if (!id) { g_err = "null id buffer"; return BA_E_INVALID; }
+    if (comm_unique_id(id, BA_COMM_ID_BYTES) != 0) {
+        g_err = comm_last_error();
+        return BA_E_COMM;
+    }
+    return BA_OK;
+}
+
+int32_t ba_comm_init(ba_context* ctx, int32_t nranks, int32_t rank, const uint8_t id[BA_COMM_ID_BYTES]) {
+    if (!ctx || !id) return BA_E_INVALID;
+    if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice failed"; return BA_E_DEVICE; }
+    if (comm_init(ctx->W.comm, nranks, rank, id) != 0) {
+        ctx->err = comm_last_error();
+        return nranks < 1 || rank < 0 || rank >= nranks ? BA_E_INVALID : BA_E_COMM;
+    }
+    ctx->prepared = false;  // the next solve re-prepares with the shard-global structure
+    return BA_OK;
+}
 
 int32_t ba_set_options(ba_context* ctx, const ba_options* opts) {
     if (!ctx || !opts) return BA_E_INVALID;
@@ -222,6 +261,7 @@ int32_t ba_set_options(ba_context* ctx, const ba_options* opts) {
         ctx->prof_events = true;
     }
     ctx->prof.on = ctx->opts.profile_kernels ? 1 : 0;
+    ctx->prof.mask = (unsigned)ctx->opts.profile_mask;
     return BA_OK;
 }
 
@@ -232,31 +272,60 @@ int32_t ba_set_options(ba_context* ctx, const ba_options* opts) {
 // active parameter blocks, point-major / camera-major orderings, envelope of S.
 static int prepare(ba_context* ctx, const ba_problem* p) {
     const ba_options& o = ctx->opts;
-    if (!p || p->n_cams < 0 || p->n_points < 0 || p->n_obs < 0) { ctx->err = "invalid problem sizes"; return BA_E_INVALID; }
-    if ((p->n_cams && !p->cams) || (p->n_points && !p->points) || !p->intr || !p->intr_prior ||
-        (p->n_obs && (!p->obs_cam || !p->obs_pt || !p->obs_uv || !p->obs_depth))) {
-        ctx->err = "null problem buffer";
-        return BA_E_INVALID;
+    const bool shard = ctx->W.comm.on();
+    // validation: with landmark shards every rank must reach the same verdict before any
+    // further collective (a rank that bailed out alone would leave the others waiting)
+    int verdict[3] = {0, 0, 0};  // [0] error code (max), [1] n_cams (min), [2] -n_cams (min)
+    std::string local_err;
+    if (!p || p->n_cams < 0 || p->n_points < 0 || p->n_obs < 0) { local_err = "invalid problem sizes"; verdict[0] = 1; }
+    else if ((p->n_cams && !p->cams) || (p->n_points && !p->points) || !p->intr || !p->intr_prior ||
+             (p->n_obs && (!p->obs_cam || !p->obs_pt || !p->obs_uv || !p->obs_depth))) {
+        local_err = "null problem buffer";
+        verdict[0] = 1;
     }
-    const int nc = p->n_cams, np = p->n_points, no = p->n_obs;
+    const int nc = verdict[0] ? 0 : p->n_cams, np = verdict[0] ? 0 : p->n_points, no = verdict[0] ? 0 : p->n_obs;
     std::vector<int> cam_cnt(nc, 0), pt_cnt(np, 0);
     std::vector<char> adm(no, 0);
     int n_adm = 0;
-    for (int k = 0; k < no; ++k) {
+    for (int k = 0; k < no && !verdict[0]; ++k) {
         const int ci = p->obs_cam[k], pi = p->obs_pt[k];
-        if (ci < 0 || ci >= nc || pi < 0 || pi >= np) { ctx->err = "observation index out of range"; return BA_E_INVALID; }
+        if (ci < 0 || ci >= nc || pi < 0 || pi >= np) { local_err = "observation index out of range"; verdict[0] = 1; break; }
         if (!(p->obs_depth[k] > 1e-15)) continue;
         adm[k] = 1;
         ++n_adm;
         ++cam_cnt[ci];
         ++pt_cnt[pi];
     }
-    if (n_adm == 0) { ctx->err = "no admissible observation (all depths <= 1e-15)"; return BA_E_INVALID; }
-    // active cameras (Ceres removes unused blocks; the gauge block is constant, :299)
+    if (!verdict[0] && n_adm == 0) { local_err = "no admissible observation (all depths <= 1e-15)"; verdict[0] = 1; }
+    if (shard) {
+        verdict[1] = nc;
+        verdict[2] = -nc;
+        int rc = host_allreduce_i32(ctx, verdict, 1, COMM_MAX);
+        if (rc == BA_OK) rc = host_allreduce_i32(ctx, verdict + 1, 2, COMM_MIN);
+        if (rc != BA_OK) return rc;
+        if (!verdict[0] && verdict[1] != -verdict[2]) { local_err = "landmark shards disagree on n_cams"; verdict[0] = 1; }
+        if (verdict[0]) {
+            ctx->err = local_err.empty() ? "another landmark shard rejected its problem" : local_err;
+            return BA_E_INVALID;
+        }
+    } else if (verdict[0]) {
+        ctx->err = local_err;
+        return BA_E_INVALID;
+    }
+    // active cameras (Ceres removes unused blocks; the gauge block is constant, :299): a camera
+    // is active when any shard observes it; N (the 1/N weights, :280/:290) counts every shard
+    std::vector<int> cam_seen(nc);
+    for (int i = 0; i < nc; ++i) cam_seen[i] = cam_cnt[i] > 0;
+    int n_adm_all = n_adm;
+    if (shard) {
+        int rc = host_allreduce_i32(ctx, cam_seen.data(), nc, COMM_MAX);
+        if (rc == BA_OK) rc = host_allreduce_i32(ctx, &n_adm_all, 1, COMM_SUM);
+        if (rc != BA_OK) return rc;
+    }
     std::vector<int> cam_ac(nc, -1);
     ctx->ac_cam.clear();
     for (int i = 0; i < nc; ++i)
-        if (cam_cnt[i] > 0 && i != p->fixed_cam) { cam_ac[i] = (int)ctx->ac_cam.size(); ctx->ac_cam.push_back(i); }
+        if (cam_seen[i] && i != p->fixed_cam) { cam_ac[i] = (int)ctx->ac_cam.size(); ctx->ac_cam.push_back(i); }
     const int nac = (int)ctx->ac_cam.size();
     // CSR of admissible obs by original point index, each list sorted by active camera
     std::vector<int> pptr(np + 1, 0);
@@ -376,6 +445,10 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         const int a = po_ac[q];
         if (a >= 0) fc[a] = std::min(fc[a], pmin[ctx->pt_idx[po_ap[q]]]);
     }
+    if (shard) {  // envelope / band of the summed S: union over the shards
+        const int rc = host_allreduce_i32(ctx, fc.data(), nac, COMM_MIN);
+        if (rc != BA_OK) return rc;
+    }
     const int n = 6 * nac + 4;
     const int npad = (n + 15) / 16 * 16;
     const int nb = npad / 16;
@@ -433,7 +506,21 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     const int n_seg = (int)seg_cam.size();
     const int nblk_pt = (n_ap + 255) / 256;
     const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, 1});
-    HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * CAMDATA * std::max(nac, 1)));
+    HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
+    // landmark sharding: envelope tile list of S, pack buffers, exchange scalars
+    std::vector<int2> env_tile;
+    if (shard) {
+        for (int i = 0; i < nb; ++i)
+            for (int j = fcol[i]; j <= i; ++j) env_tile.push_back(make_int2(i, j));
+        const size_t ne = env_tile.size() * 256 + (size_t)npad;
+        HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
+        HIPCHECK(ctx, upload(ctx, B_ENV_TILE, env_tile.data(), env_tile.size()));
+        HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
+        HIPCHECK(ctx, ctx->buf[B_ENV_GLOB].ensure(sizeof(double) * ne));
+        HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * 32));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * 32, s));
+    }
     HIPCHECK(ctx, ctx->buf[B_SEGINTR].ensure(sizeof(double) * SEGINTR * std::max(n_seg, 1)));
     HIPCHECK(ctx, ctx->buf[B_LIN].ensure(sizeof(double) * LIN_N));
     HIPCHECK(ctx, ctx->buf[B_SCALE].ensure(sizeof(double) * (6 * nac + 3 * (size_t)n_ap + 4)));
@@ -511,6 +598,14 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     }
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
+    W.camdata_loc = shard ? ctx->buf[B_CAMDATA_LOC].as<double>() : W.camdata;
+    W.env_tile = shard ? ctx->buf[B_ENV_TILE].as<int2>() : nullptr;
+    W.n_env = (int)env_tile.size();
+    W.env_loc = shard ? ctx->buf[B_ENV_LOC].as<double>() : nullptr;
+    W.env_glob = shard ? ctx->buf[B_ENV_GLOB].as<double>() : nullptr;
+    W.red = shard ? ctx->buf[B_RED].as<double>() : nullptr;
+    P.rank = W.comm.rank;
+    P.nranks = W.comm.nranks;
     W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
     W.cnp = ctx->buf[B_CNP].as<double>(); W.pdata = ctx->buf[B_PDATA].as<double>();
     W.S = ctx->buf[B_S].as<double>(); W.rhs = ctx->buf[B_RHS].as<double>();
@@ -519,7 +614,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     W.fcol = ctx->buf[B_FCOL].as<int>(); W.rptr = ctx->buf[B_RPTR].as<int>(); W.rows = ctx->buf[B_ROWS].as<int>();
     W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
     BaConsts& C = ctx->C;
-    const double N = (double)n_adm;
+    ctx->n_adm_all = n_adm_all;
+    const double N = (double)n_adm_all;  // all shards' admissible observations
     C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
     C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
     C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
@@ -555,6 +651,27 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         for (int k = 0; k < nb; ++k) {
             const double r = rptr[k + 1] - rptr[k];
             kf[K_CHOL] += (r * (r + 1) / 2) * 2.0 * 16 * 16 * 16 + r * 16 * 16 * 16 + 16 * 16 * 16 / 3.0;
+        }
+        if (P.solver == 2) {
+            // block cyclic reduction: per eliminated 64-dof block, Cholesky 64^3/3 + forward solve of
+            // 136 columns 64^2*136 (elim); 44 16x16x64 contribution tiles (contrib); per launch =
+            // solve total / launches per solve. Bytes: the blocks each kernel must read / write.
+            const int nblk = ctx->W.bcr.nblk, L = ctx->W.bcr.levels;
+            const double blk = 64.0 * 64 * 8, xblk = 64.0 * 136 * 8;
+            double e_fl = 64.0 * 64 * 64 / 3 + 2.0 * 64 * 64 * 8, e_by = 3 * blk + 2 * 64 * 8 * 8;  // root
+            double c_fl = 0, c_by = 0, b_by = 0;
+            for (int m = 0; m < L; ++m) {
+                const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
+                e_fl += nel * (64.0 * 64 * 64 / 3 + 64.0 * 64 * 136 * 2);
+                e_by += nel * (5 * blk + blk + xblk);
+                c_fl += nel * 44.0 * 16 * 16 * 64 * 2;
+                c_by += nel * (xblk + 3 * blk + 2 * 64 * 8 * 8);
+                b_by += nel * (blk + xblk + 3 * 64 * 8 * 8);
+            }
+            kf[K_BCR_ELIM] = e_fl / (L + 1); kb[K_BCR_ELIM] = e_by / (L + 1);
+            kf[K_BCR_CONTRIB] = c_fl / std::max(L, 1); kb[K_BCR_CONTRIB] = c_by / std::max(L, 1);
+            kf[K_BCR_BACK] = nblk * 2.0 * 64 * 64 * 8 * 2 / std::max(L, 1); kb[K_BCR_BACK] = b_by / std::max(L, 1);
+            kb[K_BCR_BORDER] = nblk * (32.0 + 64 * 8) * 8;
         }
         kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
         kb[K_BACKSUB_EVAL] = A * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;
@@ -650,7 +767,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     static thread_local LmState h_state;  // host staging (outlives the async copies)
     h_state = fresh_state(o, o.initial_trust_region_radius);
     HIPCHECK(ctx, hipMemcpyAsync(W.st, &h_state, sizeof(LmState), hipMemcpyHostToDevice, s));
-    sum->num_obs_admissible = P.n_adm;
+    sum->num_obs_admissible = ctx->n_adm_all;
     sum->num_active_cams = P.nac;
     sum->num_active_points = P.n_ap;
     sum->reduced_system_size = P.n;
@@ -727,7 +844,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     auto dk = [&](int k) { return ctx->k_ms[k] - kms0[k]; };
     sum->time_linearize_ms = dk(K_CAM_SIDE) + dk(K_LIN_FINALIZE) + dk(K_POINT_COLNORM) + dk(K_SCALE);
     sum->time_schur_ms = dk(K_MEMSET_S) + dk(K_ASSEMBLE) + dk(K_POINT_PREP) + dk(K_SCHUR_TILE) + dk(K_OBS_PAIRS);
-    sum->time_factor_ms = dk(K_CHOL);
+    sum->time_factor_ms = dk(K_CHOL) + dk(K_BCR_ELIM) + dk(K_BCR_CONTRIB) + dk(K_BCR_BACK) + dk(K_BCR_BORDER);
     sum->time_update_ms = dk(K_UPDATE_CAMS) + dk(K_BACKSUB_EVAL) + dk(K_FINAL) + dk(K_DECIDE);
     return BA_OK;
 }

@@ -53,7 +53,8 @@ class BaOptions(C.Structure):
         ("device", C.c_int32),
         ("deterministic", C.c_int32),
         ("profile_kernels", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("profile_mask", C.c_int32),
+        ("reserved", C.c_int32 * 4),
     ]
 
 

@@ -71,6 +71,22 @@ class Solver:
         self._check(self._L.ba_solve(self._h, C.byref(ps), C.byref(s)), "ba_solve")
         return s.as_dict()
 
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """RCCL unique id for ba_comm_init (rank 0 creates it, ships it to the other ranks)."""
+        L = _lib.lib()
+        buf = C.create_string_buffer(_lib.COMM_ID_BYTES)
+        rc = L.ba_comm_unique_id(buf)
+        if rc != 0:
+            raise MibaError(f"ba_comm_unique_id failed ({rc}): {(L.ba_last_error(None) or b'').decode()}")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        """Make this solver one landmark shard of an nranks-way sharded window (collective)."""
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError("unique id must be BA_COMM_ID_BYTES long")
+        self._check(self._L.ba_comm_init(self._h, nranks, rank, uid), "ba_comm_init")
+
     def set_options(self, **changes) -> None:
         for k, v in changes.items():
             setattr(self.options, k, v)

@@ -125,8 +125,10 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
                  outlier_frac: float = 0.02, outlier_px: float = 20.0, depth_noise: float = 0.01,
                  rot_noise: float = 0.01, trans_noise: float = 0.01, point_noise: float = 0.02,
                  intr_offset=(2.0, -1.5, 1.0, -0.8), fixed_cam: int = 0, shuffle_obs: bool = False,
-                 bad_depth_frac: float = 0.0, dup_frac: float = 0.0) -> ProblemArrays:
-    """Build one synthetic window. ``obs_per_point`` is an int or an inclusive (lo, hi) range."""
+                 bad_depth_frac: float = 0.0, dup_frac: float = 0.0, cam_seed: int | None = None) -> ProblemArrays:
+    """Build one synthetic window. ``obs_per_point`` is an int or an inclusive (lo, hi) range.
+    ``cam_seed`` draws the initial camera perturbation from its own stream, so landmark
+    shards generated with different ``seed`` share identical window cameras."""
     rng = np.random.default_rng(seed)
     if isinstance(obs_per_point, (tuple, list)):
         lo, hi = int(obs_per_point[0]), int(obs_per_point[1])
@@ -166,9 +168,10 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
         bad = rng.random(n_obs) < bad_depth_frac
         depth[bad] = np.where(rng.random(int(bad.sum())) < 0.5, 0.0, -np.inf)  # VirtualSensor MINF / 0
     # initial estimate
-    dR = _rodrigues(rng.normal(0.0, rot_noise, (n_cams, 3)))
+    crng = rng if cam_seed is None else np.random.default_rng(cam_seed)
+    dR = _rodrigues(crng.normal(0.0, rot_noise, (n_cams, 3)))
     R0 = R_wc @ dR
-    t0 = t_wc + rng.normal(0.0, trans_noise, (n_cams, 3))
+    t0 = t_wc + crng.normal(0.0, trans_noise, (n_cams, 3))
     if 0 <= fixed_cam < n_cams:
         R0[fixed_cam] = R_wc[fixed_cam]
         t0[fixed_cam] = t_wc[fixed_cam]
@@ -193,4 +196,16 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
 def make_config(name: str, **overrides) -> ProblemArrays:
     cfg = dict(CONFIGS[name])
     cfg.update(overrides)
+    return make_problem(**cfg)
+
+
+def make_landmark_shard(name: str, shard: int, **overrides) -> ProblemArrays:
+    """Landmark shard ``shard`` of a window with the cameras of config ``name``: the same
+    (seeded) initial cameras and intrinsics on every shard, an independent block of the
+    config's size of landmarks per shard (weak scaling of ba_comm_init sharding)."""
+    cfg = dict(CONFIGS[name])
+    cfg.update(overrides)
+    base = cfg["seed"]
+    cfg["seed"] = base + 1009 * shard
+    cfg["cam_seed"] = base
     return make_problem(**cfg)

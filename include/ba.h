@@ -82,8 +82,9 @@ typedef struct ba_options {
     /* MI355X execution knobs (no reference counterpart) */
     int32_t device;          /* HIP device ordinal for this context; -1 = current */
     int32_t deterministic;   /* 1 = fixed-order reductions only (no float atomics) */
-    int32_t profile_kernels; /* 1 = HIP-event timing of every kernel launch (ba_kernel_stats) */
-    int32_t reserved[5];
+    int32_t profile_kernels; /* 1 = HIP-event timing of kernel launches (ba_kernel_stats) */
+    int32_t profile_mask;    /* with profile_kernels: bit k selects kernel id k of ba_kernel_stats order; 0 = all */
+    int32_t reserved[4];
 } ba_options;
 
 /* One window, flattened. Mirrors what windowOptimize feeds to Ceres
@@ -162,6 +163,20 @@ int32_t ba_solve(ba_context* ctx, ba_problem* prob, ba_summary* summary);
  * (which must be the same window, same sizes). */
 int32_t ba_prepare(ba_context* ctx, const ba_problem* prob);
 int32_t ba_solve_prepared(ba_context* ctx, ba_problem* prob, ba_summary* summary);
+
+/* Landmark sharding (one process per GPU). Every rank passes the SAME window
+ * cameras, intrinsics, prior and fixed_cam to ba_solve / ba_prepare, and its OWN block of
+ * landmarks (points with all their observations). Per LM iteration the ranks all-reduce
+ * (RCCL over xGMI) the camera-side partials, the packed envelope of the reduced camera
+ * system and the step scalars; every rank then runs the identical deterministic solve of
+ * the reduced system, so poses and intrinsics stay bitwise identical across ranks and each
+ * rank updates its own points. Rank 0 calls ba_comm_unique_id() and ships the id to the
+ * other ranks (any host channel); then every rank calls ba_comm_init() collectively.
+ * Sharding pays only when the per-rank point work exceeds the all-reduce time (a few
+ * tens of us per iteration over xGMI): small windows should stay on one GPU. */
+#define BA_COMM_ID_BYTES 128
+int32_t ba_comm_unique_id(uint8_t id[BA_COMM_ID_BYTES]);
+int32_t ba_comm_init(ba_context* ctx, int32_t nranks, int32_t rank, const uint8_t id[BA_COMM_ID_BYTES]);
 
 /* Per-kernel device timing (requires ba_options.profile_kernels = 1).
  * bytes_per_launch is the ALGORITHMIC traffic model of DESIGN.md §Roofline

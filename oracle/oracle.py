@@ -35,9 +35,9 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        src = os.path.join(_HERE, "ba_oracle.c")
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
-            build()
+        deps = [os.path.join(_HERE, "ba_oracle.c"), os.path.join(_HERE, "..", "include", "ba.h")]
+        if not os.path.exists(_LIB_PATH) or any(os.path.getmtime(_LIB_PATH) < os.path.getmtime(d) for d in deps):
+            build()  # the oracle shares the ba_options / ba_summary layout of include/ba.h
         L = C.CDLL(_LIB_PATH)
         L.oracle_default_options.argtypes = [C.POINTER(BaOptions)]
         L.oracle_solve.argtypes = [C.POINTER(BaProblem), C.POINTER(BaOptions), C.POINTER(BaSummary)]

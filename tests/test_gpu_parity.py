@@ -122,3 +122,43 @@ def test_bcr_selected_on_long_windows(config):
     with Solver(minimizer_progress_to_stdout=0, max_num_iterations=2) as s:
         sg = s.solve(p)
     assert sg["linear_solver"] == LS["bcr"], sg
+
+
+@pytest.mark.parametrize("case", ["tum_like", "banded", "wide_overflow", "shuffled_bad_depth"])
+def test_sharded_path_single_rank(case):
+    """A context with a (1-rank) RCCL communicator runs the landmark-sharded path: split
+    camera-side finalisation, envelope pack / all-reduce / unpack of S, split step scalars.
+    It must solve exactly the unsharded problem."""
+    from miba.solver import Solver
+    p = synthetic.make_problem(**CASES[case])
+    q = p.copy()
+    with Solver(minimizer_progress_to_stdout=0) as a:
+        sa = a.solve(p)
+    with Solver(minimizer_progress_to_stdout=0) as b:
+        b.comm_init(1, 0, Solver.comm_unique_id())
+        sb = b.solve(q)
+    assert sb["num_obs_admissible"] == sa["num_obs_admissible"]
+    assert sb["linear_solver"] == sa["linear_solver"]
+    assert abs(sb["initial_cost"] - sa["initial_cost"]) <= 1e-13 * sa["initial_cost"]
+    assert abs(sb["final_cost"] - sa["final_cost"]) <= 1e-10 * sa["final_cost"], (sa, sb)
+    assert sb["num_iterations"] == sa["num_iterations"]
+    assert np.max(np.abs(p.points - q.points)) < 1e-8
+    assert np.max(np.abs(p.cams - q.cams)) < 1e-8
+
+
+def test_sharded_path_matches_oracle_c2():
+    from miba.solver import Solver
+    p = synthetic.make_config("C2")
+    q = p.copy()
+    with Solver(minimizer_progress_to_stdout=0) as b:
+        b.comm_init(1, 0, Solver.comm_unique_id())
+        sb = b.solve(p)
+    so = oracle.solve(q)
+    assert abs(sb["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sb, so)
+
+
+def test_comm_init_rejects_bad_rank():
+    from miba.solver import MibaError, Solver
+    with Solver(minimizer_progress_to_stdout=0) as b:
+        with pytest.raises(MibaError):
+            b.comm_init(2, 5, Solver.comm_unique_id())
