@@ -16,7 +16,10 @@ static constexpr int PDATA = 21;
 // tiled Schur reduction geometry
 static constexpr int TILE_WIN = 12;    // cameras per tile window
 static constexpr int CHUNK_PTS = 32;   // points per Schur chunk (K = 3 * CHUNK_PTS of the MFMA product)
-static constexpr int CHUNK_OBS = 256;  // observations per chunk (one per thread)
+static constexpr int CHUNK_OBS = 256;
+static constexpr int SUBSEG_OBS = 1024;  // observations per camera-side sub-segment (one workgroup)
+static constexpr int BS_PTS = 64;     // points per back-substitution chunk
+static constexpr int BS_OBS = 512;    // observations per back-substitution chunk (a single point may exceed)  // observations per chunk (one per thread)
 
 // partial-sum slots (each slot holds part_stride doubles, one per producing block)
 enum {
@@ -61,6 +64,7 @@ struct DevProblem {
     const int* seg_ptr;  // [n_seg+1]
     const int* seg_cam;  // [n_seg]
     const int* seg_ac;   // [n_seg]
+    const int2* ac_seg;  // [nac]: sub-segment range [x, y) of each active camera (camera-major order)
     const int* ac_cam;   // active camera -> camera index
     // tiled Schur reduction: tile t = chunks [tile_chunk[t], tile_chunk[t+1]),
     // chunk c = active points [chunk_ap[c], chunk_ap[c+1]); camera window [tile_base, +tile_span)
@@ -68,6 +72,8 @@ struct DevProblem {
     const int* tile_base;
     const int* tile_span;
     const int* chunk_ap;
+    const int* bs_chunk;   // back-substitution chunks: active-point boundaries (<= BS_PTS points, <= BS_OBS obs)
+    int n_bs_chunks;
     const int* ovf_obs;  // point-major obs of overflow points (active camera only)
     int n_tiles, n_ovf_obs;
     int n_seg, n_ap, n_adm, nac;
@@ -143,6 +149,7 @@ struct DevWork {
     // of S (+ rhs) before / after the all-reduce, and the step-scalar exchange buffer
     Comm comm;
     double* camdata_loc;   // [nac * CAMDATA + 16]; == camdata when unsharded
+    double* camdata_part;  // [n_seg * CAMDATA]: per sub-segment camera partials
     const int2* env_tile;  // (block row, block col) of every 16x16 envelope tile of S
     int n_env;
     double* env_loc;       // [n_env * 256 + npad]
@@ -155,12 +162,12 @@ struct DevWork {
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
     K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
-    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_COUNT
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
     "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
-    "bcr_back", "bcr_border", "comm"};
+    "bcr_back", "bcr_border", "comm", "cam_reduce"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {

@@ -13,7 +13,7 @@
 //   k_chol          envelope-blocked Cholesky of S + forward/back solve (1 workgroup,
 //                   v_mfma_f64_16x16x4_f64 for the trailing 16x16 tile updates)
 //   k_update_cams   delta = -s*y, Sophus T*exp(delta), prior-block terms
-//   k_backsub_eval  point back-substitution, model cost change -(J d)^T(f + J d/2),
+//   k_backsub_chunk point back-substitution, model cost change -(J d)^T(f + J d/2),
 //                   candidate cost at x + delta
 //   k_final         deterministic reduction of the per-block partials
 //
@@ -55,6 +55,54 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* lds /*4*NV*/,
     __syncthreads();
 }
 
+// Wave reduce-scatter by recursive halving: at the step with lane offset OFF a lane keeps
+// one half of its N running sums (chosen by lane bit OFF) and adds its partner's copy of
+// that half, so N values cost N/2 + N/4 + ... shuffles instead of 6 N. Afterwards lane l
+// holds the wave sums of indices [base, base + len).
+template <int N, int OFF>
+struct WaveHalve {
+    static __device__ __forceinline__ void run(double* v, int lane, int& base, int& len) {
+        constexpr int H = (N + 1) / 2;
+        const bool hi = (lane & OFF) != 0;
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            const double a = v[i];
+            const double b = (i + H < N) ? v[i + H] : 0.0;
+            const double keep = hi ? b : a;
+            const double send = hi ? a : b;
+            v[i] = keep + __shfl_xor(send, OFF);
+        }
+        if (hi) { base += H; len = len - H; } else { len = len < H ? len : H; }
+        WaveHalve<H, OFF / 2>::run(v, lane, base, len);
+    }
+};
+template <int N>
+struct WaveHalve<N, 0> {
+    static constexpr int kRemain = N;
+    static __device__ __forceinline__ void run(double*, int, int&, int&) {}
+};
+template <int N, int OFF>
+struct HalveRemain { static constexpr int value = HalveRemain<(N + 1) / 2, OFF / 2>::value; };
+template <int N>
+struct HalveRemain<N, 0> { static constexpr int value = N; };
+
+// Block (256 threads) sum of NV values via the wave reduce-scatter; out[0..NV) valid after return.
+// lds must hold 4 * NV doubles. Fixed summation order (deterministic).
+template <int NV>
+__device__ __forceinline__ void block_sum_rs(double (&v)[NV], double* lds, double* out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int base = 0, len = NV;
+    WaveHalve<NV, 32>::run(v, lane, base, len);
+    constexpr int R = HalveRemain<NV, 32>::value;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (j < len) lds[wave * NV + base + j] = v[j];
+    __syncthreads();
+    for (int i = threadIdx.x; i < NV; i += blockDim.x)
+        out[i] = lds[0 * NV + i] + lds[1 * NV + i] + lds[2 * NV + i] + lds[3 * NV + i];
+    __syncthreads();
+}
+
 __device__ __forceinline__ double block_max(double v, double* lds) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
@@ -67,8 +115,9 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
 }
 
 // ---------------------------------------------------------------- camera side
-// One workgroup per camera segment of the camera-major observation list.
-// camdata[ac*CAMDATA + ..]: U upper-packed (21), C (6x4 = 24), g (6)
+// One workgroup per sub-segment (<= SUBSEG_OBS observations of one camera) of the
+// camera-major observation list; k_cam_reduce sums a camera's sub-segments in order.
+// camdata (per sub-segment partial here): U upper-packed (21), C (6x4 = 24), g (6)
 // seg_intr[s*SEGINTR + ..]: Ukk upper-packed (10), gk (4), cost (1)
 __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
                                                   double* __restrict__ camdata, double* __restrict__ seg_intr) {
@@ -114,10 +163,23 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
         for (int m = 0; m < 4; ++m) acc[61 + m] += jk[m] * e.f[0] + jk[4 + m] * e.f[1];
         acc[65] += e.ok ? e.cost : __builtin_nan("");
     }
-    block_sum<66>(acc, lds, out);
+    block_sum_rs<66>(acc, lds, out);
     if (ac >= 0)
-        for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)ac * CAMDATA + i] = out[i];
+        for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)s * CAMDATA + i] = out[i];
     for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = out[51 + i];
+}
+
+// camdata[ac] = sum of the camera's sub-segment partials, in sub-segment order (zero when
+// this landmark shard has no observation of the camera).
+__global__ void k_cam_reduce(DevProblem P, const LmState* __restrict__ st, int gated, const double* __restrict__ part,
+                             double* __restrict__ camdata) {
+    if (st->done || (gated && !st->need_lin)) return;
+    const int ac = blockIdx.x, i = threadIdx.x;
+    if (i >= CAMDATA) return;
+    const int2 r = P.ac_seg[ac];
+    double v = 0.0;
+    for (int sg = r.x; sg < r.y; ++sg) v += part[(size_t)sg * CAMDATA + i];
+    camdata[(size_t)ac * CAMDATA + i] = v;
 }
 
 // Reduce intrinsics partials (fixed order), add the IntrinsicsPrior block
@@ -1298,24 +1360,72 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
     }
 }
 
-// Back-substitution y_p = V^-1 (e - sum W^T y_c - Kt^T y_k), delta_p = -s_p y_p,
-// model cost change over the point's observations and the candidate cost.
-__global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, const LmState* __restrict__ st,
-                                                      const double* __restrict__ scale,
-                                                      const double* __restrict__ pdata, const double* __restrict__ y,
-                                                      const double* __restrict__ delta, double* __restrict__ part) {
+// Back-substitution over a chunk of <= BS_PTS points / <= BS_OBS observations (one
+// workgroup; observation loads coalesced, one observation per thread):
+//   phase 1 (obs):   c_o = s_p (Jp^T (Jc (s_c y_c)))  -> LDS slot of the observation
+//   phase 2 (point): y_p = V~^-1 (e~ - Kt^T y_k - sum_o c_o) (fixed order), delta_p = -s_p y_p
+//   phase 3 (obs):   model cost change -(J delta)^T (f + J delta / 2), candidate cost at x + delta
+// A chunk holding a single point with more than BS_OBS observations sums c_o by block reduction.
+__global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                       const double* __restrict__ scale,
+                                                       const double* __restrict__ pdata, const double* __restrict__ y,
+                                                       const double* __restrict__ delta, double* __restrict__ part) {
+    __shared__ double co[BS_OBS][3];
+    __shared__ double dpl[BS_PTS][3];
     __shared__ double lds[4 * 5];
     __shared__ double out[5];
     if (st->done) return;
     const int cur = st->cur;
-    const int ap = blockIdx.x * TPB + threadIdx.x;
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    const int apb = P.bs_chunk[ch], ape = P.bs_chunk[ch + 1];
+    const int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
+    const int npts = ape - apb;
+    const bool big = oe - ob > BS_OBS;  // single point
+    const double* K = P.K[cur];
+    const double* Kn = P.K[cur ^ 1];
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cost, bad, |x_cand|^2
-    if (ap < P.n_ap) {
+    // ---- phase 1
+    double bsum[3] = {0.0, 0.0, 0.0};
+    for (int o = ob + tid; o < oe; o += TPB) {
+        const int ac = P.po_ac[o];
+        double v[3] = {0.0, 0.0, 0.0};
+        if (ac >= 0) {
+            const int ap = P.po_ap[o];
+            const double2 uv = P.po_uv[o];
+            ObsEval ev;
+            double jc[18], jp[9], jk[8];
+            lin_obs(c, P.cams[cur] + 7 * P.po_cam[o], P.pts[cur] + 3 * P.po_pt[o], K, uv.x, uv.y, P.po_depth[o], ev, jc,
+                    jp, jk);
+            const double* sc = scale + 6 * ac;
+            const double* yc = y + 6 * ac;
+            const double* sp = scale + P.off_pt + 3 * ap;
+            double jy[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                double sacc = 0.0;
+#pragma unroll
+                for (int d = 0; d < 6; ++d) sacc += jc[r * 6 + d] * (sc[d] * yc[d]);
+                jy[r] = sacc;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v[i] = sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
+        }
+        if (big) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) bsum[i] += v[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) co[o - ob][i] = v[i];
+        }
+    }
+    if (big) block_sum<3>(bsum, lds, out);  // out[0..3) valid for every thread after this
+    __syncthreads();
+    // ---- phase 2
+    if (tid < npts) {
+        const int ap = apb + tid;
         const int pi = P.pt_idx[ap];
         const double* X = P.pts[cur] + 3 * pi;
         double* Xn = P.pts[cur ^ 1] + 3 * pi;
-        const double* K = P.K[cur];
-        const double* Kn = P.K[cur ^ 1];
         const double* pd = pdata + (size_t)ap * PDATA;
         const double* sp = scale + P.off_pt + 3 * ap;
         const double* yk = y + P.kb;
@@ -1324,74 +1434,75 @@ __global__ __launch_bounds__(TPB) void k_backsub_eval(DevProblem P, BaConsts c, 
         for (int i = 0; i < 3; ++i)
             t[i] = pd[6 + i] - (pd[9 + 0 * 3 + i] * yk[0] + pd[9 + 1 * 3 + i] * yk[1] + pd[9 + 2 * 3 + i] * yk[2] +
                                 pd[9 + 3 * 3 + i] * yk[3]);
-        const int o0 = P.pt_ptr[ap], o1 = P.pt_ptr[ap + 1];
-        for (int o = o0; o < o1; ++o) {
-            const int ac = P.po_ac[o];
-            if (ac < 0) continue;
-            const double2 uv = P.po_uv[o];
-            ObsEval ev;
-            double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * P.po_cam[o], X, K, uv.x, uv.y, P.po_depth[o], ev, jc, jp, jk);
-            const double* sc = scale + 6 * ac;
-            const double* yc = y + 6 * ac;
-            double jy[3];
+        if (big) {
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                double s = 0.0;
+            for (int i = 0; i < 3; ++i) t[i] -= out[i];
+        } else {
+            for (int o = P.pt_ptr[ap]; o < P.pt_ptr[ap + 1]; ++o)
 #pragma unroll
-                for (int d = 0; d < 6; ++d) s += jc[r * 6 + d] * (sc[d] * yc[d]);
-                jy[r] = s;
-            }
-#pragma unroll
-            for (int i = 0; i < 3; ++i) t[i] -= sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
+                for (int i = 0; i < 3; ++i) t[i] -= co[o - ob][i];
         }
-        double dp[3], xn[3];
         double Vf[9];
         vinv_from_g(pd, Vf);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const double yp = Vf[i * 3 + 0] * t[0] + Vf[i * 3 + 1] * t[1] + Vf[i * 3 + 2] * t[2];
-            dp[i] = -sp[i] * yp;
-            xn[i] = X[i] + dp[i];
-            Xn[i] = xn[i];
-            const double df = X[i] - xn[i];
+            const double dp = -sp[i] * yp;
+            const double xn = X[i] + dp;
+            Xn[i] = xn;
+            dpl[tid][i] = dp;
+            const double df = X[i] - xn;
             acc[0] += df * df;
-            acc[4] += xn[i] * xn[i];
+            acc[4] += xn * xn;
         }
-        const double* dk = delta + P.kb;
-        for (int o = o0; o < o1; ++o) {
-            const int ac = P.po_ac[o];
-            const int cam = P.po_cam[o];
-            const double2 uv = P.po_uv[o];
-            const double dep = P.po_depth[o];
-            ObsEval ev;
-            double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * cam, X, K, uv.x, uv.y, dep, ev, jc, jp, jk);
+    }
+    __syncthreads();
+    // ---- phase 3
+    const double* dk = delta + P.kb;
+    for (int o = ob + tid; o < oe; o += TPB) {
+        const int ac = P.po_ac[o];
+        const int cam = P.po_cam[o];
+        const int pl = P.po_ap[o] - apb;
+        const double2 uv = P.po_uv[o];
+        const double dep = P.po_depth[o];
+        const double* X = P.pts[cur] + 3 * P.po_pt[o];
+        const double dp[3] = {dpl[pl][0], dpl[pl][1], dpl[pl][2]};
+        ObsEval ev;
+        double jc[18], jp[9], jk[8];
+        lin_obs(c, P.cams[cur] + 7 * cam, X, K, uv.x, uv.y, dep, ev, jc, jp, jk);
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                double jd = jp[r * 3 + 0] * dp[0] + jp[r * 3 + 1] * dp[1] + jp[r * 3 + 2] * dp[2];
-                if (ac >= 0) {
-                    const double* dc = delta + 6 * ac;
+        for (int r = 0; r < 3; ++r) {
+            double jd = jp[r * 3 + 0] * dp[0] + jp[r * 3 + 1] * dp[1] + jp[r * 3 + 2] * dp[2];
+            if (ac >= 0) {
+                const double* dc = delta + 6 * ac;
 #pragma unroll
-                    for (int d = 0; d < 6; ++d) jd += jc[r * 6 + d] * dc[d];
-                }
-                if (r < 2) jd += jk[r * 4 + 0] * dk[0] + jk[r * 4 + 1] * dk[1] + jk[r * 4 + 2] * dk[2] + jk[r * 4 + 3] * dk[3];
-                acc[1] += -jd * (ev.f[r] + jd / 2.0);
+                for (int d = 0; d < 6; ++d) jd += jc[r * 6 + d] * dc[d];
             }
-            ObsEval en;
-            eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, uv.x, uv.y, dep, en);
-            if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
+            if (r < 2) jd += jk[r * 4 + 0] * dk[0] + jk[r * 4 + 1] * dk[1] + jk[r * 4 + 2] * dk[2] + jk[r * 4 + 3] * dk[3];
+            acc[1] += -jd * (ev.f[r] + jd / 2.0);
         }
-        if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
+        const double xn[3] = {X[0] + dp[0], X[1] + dp[1], X[2] + dp[2]};
+        ObsEval en;
+        eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, uv.x, uv.y, dep, en);
+        if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
     }
+    if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
     block_sum<5>(acc, lds, out);
-    if (threadIdx.x == 0) {
-        part[PART_BS_SN2 * P.part_stride + blockIdx.x] = out[0];
-        part[PART_BS_MCC * P.part_stride + blockIdx.x] = out[1];
-        part[PART_BS_COST * P.part_stride + blockIdx.x] = out[2];
-        part[PART_BS_BAD * P.part_stride + blockIdx.x] = out[3];
-        part[PART_BS_XN2 * P.part_stride + blockIdx.x] = out[4];
+    if (tid == 0) {
+        part[PART_BS_SN2 * P.part_stride + ch] = out[0];
+        part[PART_BS_MCC * P.part_stride + ch] = out[1];
+        part[PART_BS_COST * P.part_stride + ch] = out[2];
+        part[PART_BS_BAD * P.part_stride + ch] = out[3] > 0.0 ? 1.0 : 0.0;
+        part[PART_BS_XN2 * P.part_stride + ch] = out[4];
     }
+}
+
+// Clear the envelope tiles of S (every solver reads only these; the rest stays zero).
+__global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st, const int2* __restrict__ tiles, int npad,
+                                                  double* __restrict__ S) {
+    if (st->done) return;
+    const int2 ij = tiles[blockIdx.x];
+    S[(size_t)(16 * ij.x + (threadIdx.x >> 4)) * npad + 16 * ij.y + (threadIdx.x & 15)] = 0.0;
 }
 
 // ---------------------------------------------------------------- final
@@ -1437,11 +1548,6 @@ __global__ __launch_bounds__(TPB) void k_final(DevProblem P, const LmState* __re
 }
 
 // ---------------------------------------------------------------- landmark sharding
-// Zero n doubles (gated: only when the window is re-linearised).
-__global__ void k_zero_gated(const LmState* __restrict__ st, int gated, double* __restrict__ p, size_t n) {
-    if (st->done || (gated && !st->need_lin)) return;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = 0.0;
-}
 // Envelope of S (its 16x16 tiles) + rhs <-> one contiguous buffer for the all-reduce.
 // unpack == 0: S, rhs -> buf; unpack == 1: buf -> S, rhs.
 __global__ __launch_bounds__(TPB) void k_env_pack(const LmState* __restrict__ st, const int2* __restrict__ tiles, int n_env,
@@ -1703,20 +1809,18 @@ static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
     } while (0)
 
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
+    if (P.n_seg > 0)
+        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr);
+    if (P.nac > 0)
+        PL(K_CAM_REDUCE, k_cam_reduce, dim3(P.nac), dim3(64), 0, s, P, W.st, gated, W.camdata_part, W.camdata_loc);
     if (!W.comm.on()) {
-        if (P.n_seg > 0)
-            PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr);
         PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin, 0,
            (double*)nullptr);
         return hipSuccess;
     }
-    // sharded: this rank's camera-side partials -> camdata_loc (cameras without local
-    // observations stay zero), one all-reduce of [camdata | intrinsics partials], finalize
+    // sharded: one all-reduce of [camdata | intrinsics partials] between the local sums and
+    // the finalisation (camdata_loc is zero for cameras this shard does not observe)
     const size_t ncd = (size_t)P.nac * CAMDATA;
-    PL(K_CAM_SIDE, k_zero_gated, dim3(nblocks((int)std::min<size_t>(ncd, 1 << 20), TPB)), dim3(TPB), 0, s, W.st, gated,
-       W.camdata_loc, ncd);
-    if (P.n_seg > 0)
-        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_loc, W.seg_intr);
     PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_loc, W.seg_intr, W.lin, 1,
        W.camdata_loc + ncd);
     COMM(W.camdata_loc, W.camdata, ncd + SEGINTR, COMM_F64, COMM_SUM);
@@ -1743,10 +1847,8 @@ hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Pro
 }
 
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
-    if (pf) pf->begin(K_MEMSET_S, s);
-    CK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
     CK(hipMemsetAsync(W.chol_flag, 0, sizeof(int), s));
-    if (pf) pf->end(s);
+    PL(K_MEMSET_S, k_env_zero, dim3(W.n_env), dim3(TPB), 0, s, W.st, W.env_tile, P.npad, W.S);
     if (P.rank == 0) {  // camera / intrinsics blocks, LM diagonal, pad: once over the shards
         PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, W.st, W.camdata, W.lin, W.scale,
            W.S, W.rhs);
@@ -1851,9 +1953,9 @@ hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* p
 hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
     const int nb_upd = nblocks(P.nac + 1, TPB);
     PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.rhs, W.delta, W.part);
-    const int nb_bs = nblocks(P.n_ap, TPB);
+    const int nb_bs = P.n_bs_chunks;
     if (P.n_ap > 0)
-        PL(K_BACKSUB_EVAL, k_backsub_eval, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
+        PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part);
     const int nb_pt = P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0;
     if (!W.comm.on()) {

@@ -57,7 +57,7 @@ enum BufId {
     B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PO_PT, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_ENV_GLOB, B_RED, B_PREP, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_ENV_GLOB, B_RED, B_PREP, B_BS_CHUNK, B_AC_SEG, B_CAMPART, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3,
     B_COUNT
 };
@@ -417,6 +417,15 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             po_dep[q] = p->obs_depth[k];
             if (a >= n_tiled && po_ac[q] >= 0) ovf_obs.push_back(q);
         }
+    // back-substitution chunks over all active points: <= BS_PTS points and <= BS_OBS observations
+    std::vector<int> bs_chunk(1, 0);
+    for (int a = 0; a < n_ap;) {
+        int b = a + 1;
+        while (b < n_ap && b - a < BS_PTS && pt_ptr[b + 1] - pt_ptr[a] <= BS_OBS) ++b;
+        bs_chunk.push_back(b);
+        a = b;
+    }
+    const int n_bs_chunks = (int)bs_chunk.size() - 1;
     // camera-major obs: one segment per camera with admissible obs (gauge included)
     std::vector<int> seg_ptr(1, 0), seg_cam, seg_ac;
     std::vector<int> cstart(nc + 1, 0);
@@ -432,11 +441,18 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             co_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
             co_dep[q] = p->obs_depth[k];
         }
+    // sub-segments of <= SUBSEG_OBS observations (one workgroup each); ac_seg[ac] = the
+    // sub-segment range of active camera ac (empty when this shard has no observation of it)
+    std::vector<int2> ac_seg(std::max(nac, 1), make_int2(0, 0));
     for (int i = 0; i < nc; ++i)
         if (cam_cnt[i] > 0) {
-            seg_cam.push_back(i);
-            seg_ac.push_back(cam_ac[i]);
-            seg_ptr.push_back(cstart[i + 1]);
+            const int first = (int)seg_cam.size();
+            for (int q0 = cstart[i]; q0 < cstart[i + 1]; q0 += SUBSEG_OBS) {
+                seg_cam.push_back(i);
+                seg_ac.push_back(cam_ac[i]);
+                seg_ptr.push_back(std::min(q0 + SUBSEG_OBS, cstart[i + 1]));
+            }
+            if (cam_ac[i] >= 0) ac_seg[cam_ac[i]] = make_int2(first, (int)seg_cam.size());
         }
     // envelope of S: first co-visible active camera of each active camera
     std::vector<int> fc(nac);
@@ -494,39 +510,45 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     HIPCHECK(ctx, upload(ctx, B_SEG_PTR, seg_ptr.data(), seg_ptr.size()));
     HIPCHECK(ctx, upload(ctx, B_SEG_CAM, seg_cam.data(), seg_cam.size()));
     HIPCHECK(ctx, upload(ctx, B_SEG_AC, seg_ac.data(), seg_ac.size()));
+    HIPCHECK(ctx, upload(ctx, B_AC_SEG, ac_seg.data(), ac_seg.size()));
     HIPCHECK(ctx, upload(ctx, B_AC_CAM, ctx->ac_cam.data(), nac));
     HIPCHECK(ctx, upload(ctx, B_FCOL, fcol.data(), nb));
     HIPCHECK(ctx, upload(ctx, B_TILE_CHUNK, tile_chunk.data(), tile_chunk.size()));
     HIPCHECK(ctx, upload(ctx, B_TILE_BASE, tile_base.data(), tile_base.size()));
     HIPCHECK(ctx, upload(ctx, B_TILE_SPAN, tile_span.data(), tile_span.size()));
     HIPCHECK(ctx, upload(ctx, B_CHUNK_AP, chunk_ap.data(), chunk_ap.size()));
+    HIPCHECK(ctx, upload(ctx, B_BS_CHUNK, bs_chunk.data(), bs_chunk.size()));
     HIPCHECK(ctx, upload(ctx, B_OVF_OBS, ovf_obs.data(), ovf_obs.size()));
     HIPCHECK(ctx, upload(ctx, B_RPTR, rptr.data(), nb + 1));
     HIPCHECK(ctx, upload(ctx, B_ROWS, rows.data(), rows.size()));
     const int n_seg = (int)seg_cam.size();
     const int nblk_pt = (n_ap + 255) / 256;
-    const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, 1});
+    const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, 1});
     HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
     // landmark sharding: envelope tile list of S, pack buffers, exchange scalars
+    // envelope tiles of S: every solver reads only these; the per-iteration clear of S covers
+    // only them (the rest is zeroed once here), and the shard all-reduce packs them
     std::vector<int2> env_tile;
+    for (int i = 0; i < nb; ++i)
+        for (int j = fcol[i]; j <= i; ++j) env_tile.push_back(make_int2(i, j));
+    HIPCHECK(ctx, upload(ctx, B_ENV_TILE, env_tile.data(), env_tile.size()));
     if (shard) {
-        for (int i = 0; i < nb; ++i)
-            for (int j = fcol[i]; j <= i; ++j) env_tile.push_back(make_int2(i, j));
         const size_t ne = env_tile.size() * 256 + (size_t)npad;
         HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
-        HIPCHECK(ctx, upload(ctx, B_ENV_TILE, env_tile.data(), env_tile.size()));
         HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
         HIPCHECK(ctx, ctx->buf[B_ENV_GLOB].ensure(sizeof(double) * ne));
         HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * 32));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * 32, s));
     }
     HIPCHECK(ctx, ctx->buf[B_SEGINTR].ensure(sizeof(double) * SEGINTR * std::max(n_seg, 1)));
+    HIPCHECK(ctx, ctx->buf[B_CAMPART].ensure(sizeof(double) * CAMDATA * std::max(n_seg, 1)));
     HIPCHECK(ctx, ctx->buf[B_LIN].ensure(sizeof(double) * LIN_N));
     HIPCHECK(ctx, ctx->buf[B_SCALE].ensure(sizeof(double) * (6 * nac + 3 * (size_t)n_ap + 4)));
     HIPCHECK(ctx, ctx->buf[B_CNP].ensure(sizeof(double) * 3 * std::max(n_ap, 1)));
     HIPCHECK(ctx, ctx->buf[B_PDATA].ensure(sizeof(double) * PDATA * std::max(n_ap, 1)));
     HIPCHECK(ctx, ctx->buf[B_S].ensure(sizeof(double) * (size_t)npad * npad));
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)npad * npad, s));
     HIPCHECK(ctx, ctx->buf[B_RHS].ensure(sizeof(double) * npad));
     HIPCHECK(ctx, ctx->buf[B_DELTA].ensure(sizeof(double) * npad));
     HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
@@ -550,9 +572,12 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     P.co_depth = ctx->buf[B_CO_DEP].as<double>();
     P.seg_ptr = ctx->buf[B_SEG_PTR].as<int>(); P.seg_cam = ctx->buf[B_SEG_CAM].as<int>();
     P.seg_ac = ctx->buf[B_SEG_AC].as<int>(); P.ac_cam = ctx->buf[B_AC_CAM].as<int>();
+    P.ac_seg = ctx->buf[B_AC_SEG].as<int2>();
     P.tile_chunk = ctx->buf[B_TILE_CHUNK].as<int>(); P.tile_base = ctx->buf[B_TILE_BASE].as<int>();
     P.tile_span = ctx->buf[B_TILE_SPAN].as<int>(); P.chunk_ap = ctx->buf[B_CHUNK_AP].as<int>();
     P.ovf_obs = ctx->buf[B_OVF_OBS].as<int>();
+    P.bs_chunk = ctx->buf[B_BS_CHUNK].as<int>();
+    P.n_bs_chunks = n_bs_chunks;
     P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
     ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
     P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
@@ -599,7 +624,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
     W.camdata_loc = shard ? ctx->buf[B_CAMDATA_LOC].as<double>() : W.camdata;
-    W.env_tile = shard ? ctx->buf[B_ENV_TILE].as<int2>() : nullptr;
+    W.camdata_part = ctx->buf[B_CAMPART].as<double>();
+    W.env_tile = ctx->buf[B_ENV_TILE].as<int2>();
     W.n_env = (int)env_tile.size();
     W.env_loc = shard ? ctx->buf[B_ENV_LOC].as<double>() : nullptr;
     W.env_glob = shard ? ctx->buf[B_ENV_GLOB].as<double>() : nullptr;
@@ -634,12 +660,13 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         const double env_bytes = env * 16 * 16 * 8;
         double* kb = ctx->k_bytes;
         double* kf = ctx->k_flops;
-        kb[K_CAM_SIDE] = A * 28 + Pn * 24 + (Cn + 1) * 56 + 32 + Cn * CAMDATA * 8 + Sg * SEGINTR * 8;
+        kb[K_CAM_SIDE] = A * 28 + Pn * 24 + (Cn + 1) * 56 + 32 + Sg * (CAMDATA + SEGINTR) * 8;
+        kb[K_CAM_REDUCE] = Sg * CAMDATA * 8 + Cn * CAMDATA * 8;
         kf[K_CAM_SIDE] = A * 420;
         kb[K_LIN_FINALIZE] = Sg * SEGINTR * 8 + Cn * (56 + 48) + LIN_N * 8;
         kb[K_POINT_COLNORM] = A * 28 + Pn * (8 + 24 + 24);
         kb[K_SCALE] = (6 * Cn + 3 * Pn + 4) * 16;
-        kb[K_MEMSET_S] = (double)npad * npad * 8;
+        kb[K_MEMSET_S] = (double)env_tile.size() * 256 * 8;
         kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
         kb[K_POINT_PREP] = A * 28 + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
         kf[K_POINT_PREP] = A * 300 + Pn * 200;
@@ -674,7 +701,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             kb[K_BCR_BORDER] = nblk * (32.0 + 64 * 8) * 8;
         }
         kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
-        kb[K_BACKSUB_EVAL] = A * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;
+        kb[K_BACKSUB_EVAL] = A * 2 * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read twice
         kf[K_BACKSUB_EVAL] = A * 700;
         kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
     }

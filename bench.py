@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F64_MFMA_PEAK_TF = 78.6  # MI355X FP64 matrix spec (tools/mfma_f64_rate.hip measures ~73 TF/s sustained)
 
 # kernels whose bound is HBM bandwidth (per-observation passes) vs the f64 matrix cores
-HBM_KERNELS = {"cam_side", "point_colnorm", "point_prep", "backsub_eval", "lin_finalize", "scale", "assemble",
+HBM_KERNELS = {"cam_side", "cam_reduce", "point_colnorm", "point_prep", "backsub_eval", "lin_finalize", "scale", "assemble",
                "update_cams", "memset_S", "obs_pairs", "final", "xnorm", "comm"}
 JACOBIAN_PASS = "cam_side"  # the roofline.achieved basis (Jacobian pass, J kept in registers)
 
