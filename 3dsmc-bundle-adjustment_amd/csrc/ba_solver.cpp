@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/ba.h"
+#include "ba_host.h"
 #include "ba_kernels.h"
 
 using namespace miba;
@@ -105,6 +106,8 @@ static void flush_prof(ba_context* ctx) {
 }
 
 static thread_local std::string g_err;
+
+void miba_set_error(const std::string& msg) { g_err = msg; }
 
 #define HIPCHECK(ctx, x)                                                                  \
     do {                                                                                  \
@@ -743,6 +746,7 @@ static void print_row(int it, double cost, double dc, double g, double st, doubl
 
 extern "C" int32_t ba_prepare(ba_context* ctx, const ba_problem* p) {
     if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
+    miba_maybe_dump_window(p, &ctx->opts);
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     int rc = prepare(ctx, p);
     if (rc) return rc;
@@ -755,6 +759,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
 extern "C" int32_t ba_solve(ba_context* ctx, ba_problem* p, ba_summary* sum) {
     if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
     if (!sum) { ctx->err = "null summary"; return BA_E_INVALID; }
+    miba_maybe_dump_window(p, &ctx->opts);
     const double t0 = now_ms();
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     int rc = prepare(ctx, p);

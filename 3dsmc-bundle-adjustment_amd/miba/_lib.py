@@ -12,11 +12,12 @@ from .capi import BaKernelStat, BaOptions, BaProblem, BaSummary
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libmiba.so")
 
-# exported symbols, exactly those declared in include/ba.h
+# exported symbols, exactly those declared in include/ba.h and include/ba_io.h
 EXPORTS = (
     "ba_api_version", "ba_build_info", "ba_default_options", "ba_create", "ba_destroy", "ba_last_error", "ba_set_options",
     "ba_solve", "ba_prepare", "ba_solve_prepared", "ba_kernel_stats", "ba_reset_kernel_stats",
     "ba_debug_linearize", "ba_debug_reduced_system", "ba_comm_unique_id", "ba_comm_init",
+    "ba_problem_write", "ba_problem_read_dims", "ba_problem_read", "ba_bal_read_dims", "ba_bal_read", "ba_bal_write",
 )
 COMM_ID_BYTES = 128  # BA_COMM_ID_BYTES
 
@@ -67,5 +68,15 @@ def lib():
     L.ba_comm_unique_id.restype = C.c_int32
     L.ba_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     L.ba_comm_init.restype = C.c_int32
+    ip = C.POINTER(C.c_int32)
+    L.ba_problem_write.argtypes = [C.c_char_p, C.POINTER(BaProblem), C.POINTER(BaOptions)]
+    L.ba_problem_read_dims.argtypes = [C.c_char_p, ip, ip, ip]
+    L.ba_problem_read.argtypes = [C.c_char_p, C.POINTER(BaProblem), C.POINTER(BaOptions)]
+    L.ba_bal_read_dims.argtypes = [C.c_char_p, ip, ip, ip]
+    L.ba_bal_read.argtypes = [C.c_char_p, C.POINTER(BaProblem)]
+    L.ba_bal_write.argtypes = [C.c_char_p, C.POINTER(BaProblem)]
+    for f in ("ba_problem_write", "ba_problem_read_dims", "ba_problem_read", "ba_bal_read_dims", "ba_bal_read",
+              "ba_bal_write"):
+        getattr(L, f).restype = C.c_int32
     _lib = L
     return L

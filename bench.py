@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--shard", action="store_true", help="landmark-sharded path even on one GPU")
+    ap.add_argument("--problem", default=None,
+                    help="bench a window file instead of a synthetic config: a .miba dump (MIBA_DUMP_DIR capture, "
+                         "solved with its captured cost options) or a BAL text problem")
     return ap.parse_args()
 
 
@@ -107,13 +110,21 @@ def main():
     from miba.solver import Solver
 
     sharded = world > 1 or args.shard
-    prob = synthetic.make_landmark_shard(args.config, rank)  # shard 0 == the single-GPU window
+    file_opts = None
+    if args.problem:
+        from miba import problem_io, shard
+        whole, file_opts = problem_io.load(args.problem)
+        prob = shard.split_landmarks(whole, world, rank)[0] if world > 1 else whole
+        args.config = "file"
+    else:
+        prob = synthetic.make_landmark_shard(args.config, rank)  # shard 0 == the single-GPU window
     prob0 = prob.copy()
 
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0,
                   minimizer_progress_to_stdout=0)
     prof = 0 if args.no_profile else 1
-    solver = Solver(device=local_rank, profile_kernels=prof, max_num_iterations=max(args.warmup, 1), **no_tol)
+    solver = Solver(file_opts, device=local_rank, profile_kernels=prof, max_num_iterations=max(args.warmup, 1),
+                    **no_tol)
     if sharded:
         box = [Solver.comm_unique_id() if rank == 0 else None]
         if world > 1:
@@ -183,6 +194,9 @@ def main():
             from oracle import oracle
             q = prob0.copy()
             o = oracle.default_options(max_num_iterations=args.cpu_iters, **no_tol)
+            if file_opts is not None:
+                for f in ("hub_p_repr", "hub_p_unpr", "weight_intrinsics", "weight_unpr"):
+                    setattr(o, f, getattr(file_opts, f))
             tc0 = time.perf_counter()
             so = oracle.solve(q, o)
             tc1 = time.perf_counter()
@@ -193,7 +207,12 @@ def main():
                              f"Ceres 2.0 LM path, not Ceres; single thread), wall {tc1 - tc0:.1f}s incl. setup"}
         wit = max(wsumm["num_iterations"], 1)
         phases = {k["name"]: round(k["total_ms"] / wit, 4) for k in live}  # warmup run, every kernel timed
-        if sharded:
+        if args.problem:
+            workload = (f"{os.path.basename(args.problem)}: {prob0.n_cams} cams / {world}x~{prob0.n_points} points / "
+                        f"{world}x~{prob0.n_obs} obs, one window from file"
+                        + (f", landmark-sharded across {world} GPUs" if sharded else ""))
+            par = f"landmark-shard{world}" if sharded else "single"
+        elif sharded:
             workload = (f"{args.config} landmark shards: {prob0.n_cams} cams / {world}x{prob0.n_points} points / "
                         f"{world}x{prob0.n_obs} obs, one window landmark-sharded across {world} GPU(s) "
                         f"(RCCL all-reduce of the reduced camera system per LM iteration)")
@@ -213,7 +232,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic",
+            "data": "file" if args.problem else "synthetic",
             "config": {"workload": workload, "cams": prob0.n_cams, "points": world * prob0.n_points,
                        "obs": world * prob0.n_obs, "parallelism": par},
             "roofline": roofs.get(dom),

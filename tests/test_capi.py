@@ -3,6 +3,7 @@ symbols include/ba.h declares, and refuses to run (loudly) with no device."""
 import ctypes as C
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -13,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_functions():
-    src = open(os.path.join(ROOT, "include", "ba.h")).read()
+    src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("ba.h", "ba_io.h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(ba_[a-z_]+)\s*\(", src)))
 
@@ -30,6 +31,10 @@ def test_exports_match_header(L):
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
         assert hasattr(L, name), name
+    # and nothing else with the ba_ prefix is exported
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = sorted({l.split()[-1] for l in nm.stdout.splitlines() if l.split()[-1].startswith("ba_")})
+    assert exported == decl
 
 
 def test_defaults_equal_oracle_defaults(L):
