@@ -209,6 +209,123 @@ __device__ void potrf64_fwd(double* T, double* rdiag64, double* X, int ncol, boo
 #undef PF_STAMP
 }
 
+// ---- look-ahead variant: the 16x16 diagonal tiles are inverted right after they are factored,
+// so every substitution becomes an MFMA product, and wave 0 runs the pivot chain while the other
+// waves do the previous panel's trailing update. Per panel kb (two barrier phases):
+//   phase 1  wave 0: potrf16(kb) and W_kb = L_kk^-1 (lanes 0..15, one column each)
+//            waves 1-7: trailing update of panel kb-1 on every tile except (kb,kb)
+//   phase 2  wave 0: L(kb+1,kb) = A(kb+1,kb) W^T, then (kb+1,kb+1) -= L(kb+1,kb) L(kb+1,kb)^T
+//            waves 1-7: L(i,kb) = A(i,kb) W^T for i >= kb+2, and X_kb <- W X_kb
+// Each tile receives its panel updates in panel order, as in potrf64_fwd.
+// acc = A * B^T over k = 0..15: A rows from a (stride lda), B rows from b (stride ldb)
+__device__ __forceinline__ d4b mfma16_abt(const double* a, int lda, const double* b, int ldb, int rr, int kk) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+        av[s4] = a[rr * lda + 4 * s4 + kk];
+        bv[s4] = b[rr * ldb + 4 * s4 + kk];
+    }
+    d4b acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+    return acc;
+}
+// acc = A * B over k = 0..15: A rows from a (stride lda), B rows (k) from b (stride ldb), columns rr
+__device__ __forceinline__ d4b mfma16_ab(const double* a, int lda, const double* b, int ldb, int rr, int kk,
+                                         bool colok) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+        av[s4] = a[rr * lda + 4 * s4 + kk];
+        bv[s4] = colok ? b[(4 * s4 + kk) * ldb + rr] : 0.0;
+    }
+    d4b acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+    return acc;
+}
+
+__device__ void potrf64_fwd_la(double* T, double* rdiag64, double* Wb, double* X, int ncol, bool& bad) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rr = lane & 15, kk = lane >> 4;
+    const int ncb = (ncol + 15) >> 4;
+    for (int kb = 0; kb < 4; ++kb) {
+        double* Tkk = T + (16 * kb) * BLD + 16 * kb;
+        // ---- phase 1
+        if (wave == 0) {
+            potrf16_tile(Tkk, BLD, rdiag64 + 16 * kb, lane, bad);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < 16) {
+                double v[16];
+#pragma unroll
+                for (int m = 0; m < 16; ++m) v[m] = (m == lane) ? 1.0 : 0.0;
+                fwd16(v, Tkk, rdiag64 + 16 * kb);
+#pragma unroll
+                for (int m = 0; m < 16; ++m) Wb[m * 16 + lane] = v[m];
+            }
+        } else if (kb > 0) {
+            const int p = kb - 1, nt = 4 - kb;
+            const int npairs = nt * (nt + 1) / 2 - 1;  // tiles (i,j), kb <= j <= i, minus (kb,kb)
+            const int ntile = npairs + nt * ncb;
+            for (int t = wave - 1; t < ntile; t += NWE - 1) {
+                if (t < npairs) {
+                    int q = t + 1, a = 0;
+                    while (q > a) { q -= a + 1; ++a; }
+                    const int i = kb + a, j = kb + q;
+                    const d4b acc = mfma16_abt(T + (16 * i) * BLD + 16 * p, BLD, T + (16 * j) * BLD + 16 * p, BLD, rr, kk);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) T[(16 * i + kk + 4 * g) * BLD + 16 * j + rr] -= acc[g];
+                } else {
+                    const int u = t - npairs, i = kb + u / ncb, cb = u % ncb;
+                    const bool colok = 16 * cb + rr < ncol;
+                    const d4b acc = mfma16_ab(T + (16 * i) * BLD + 16 * p, BLD, X + (16 * p) * XW + 16 * cb, XW, rr, kk,
+                                              colok);
+                    if (colok)
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) X[(16 * i + kk + 4 * g) * XW + 16 * cb + rr] -= acc[g];
+                }
+            }
+        }
+        __syncthreads();
+        // ---- phase 2
+        const int nrow = 3 - kb;  // row tiles below the panel
+        if (wave == 0) {
+            if (kb < 3) {
+                const int i = kb + 1;
+                double* Ai = T + (16 * i) * BLD + 16 * kb;
+                const d4b acc = mfma16_abt(Ai, BLD, Wb, 16, rr, kk);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) Ai[(kk + 4 * g) * BLD + rr] = acc[g];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const d4b acc2 = mfma16_abt(Ai, BLD, Ai, BLD, rr, kk);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) T[(16 * i + kk + 4 * g) * BLD + 16 * i + rr] -= acc2[g];
+            }
+        } else {
+            const int ntile = (nrow > 0 ? nrow - 1 : 0) + ncb;
+            for (int t = wave - 1; t < ntile; t += NWE - 1) {
+                if (t < nrow - 1) {
+                    double* Ai = T + (16 * (kb + 2 + t)) * BLD + 16 * kb;
+                    const d4b acc = mfma16_abt(Ai, BLD, Wb, 16, rr, kk);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Ai[(kk + 4 * g) * BLD + rr] = acc[g];
+                } else {
+                    const int cb = t - (nrow > 0 ? nrow - 1 : 0);
+                    const bool colok = 16 * cb + rr < ncol;
+                    double* Xc = X + (16 * kb) * XW + 16 * cb;
+                    const d4b acc = mfma16_ab(Wb, 16, Xc, XW, rr, kk, colok);
+                    if (colok)
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) Xc[(kk + 4 * g) * XW + rr] = acc[g];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // X <- L^-T X (backward), L 64x64 lower in LDS (stride BLD), X 64 x ncol (LDS, stride ldx).
 __device__ void trsm_lower64_t(const double* L, const double* rdiag64, double* X, int ldx, int ncol) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -312,6 +429,7 @@ struct ElimLds {
     double T[BB * BLD];  // D_i -> Cf
     double X[BB * XW];   // [A_l | A_r | R] -> [XL | XR | x]
     double rdiag[BB];
+    double Wb[256];      // inverse of the current 16x16 diagonal tile
     double Bl[4 * BB];   // root: border rows
     double red[80];
 };
@@ -408,8 +526,11 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
     __syncthreads();
     BCR_STAMP(m, 1);
     bool bad = false;
-    potrf64_fwd<STAMP>(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad,
-                       STAMP && blockIdx.x == 0 ? stamps + 8 * 24 + 4 * m : nullptr);
+    if (STAMP)
+        potrf64_fwd<STAMP>(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad,
+                           blockIdx.x == 0 ? stamps + 8 * 24 + 4 * m : nullptr);
+    else
+        potrf64_fwd_la(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad);
     if (bad) *flag = 1;
     BCR_STAMP(m, 2);
     if (root) {
@@ -646,6 +767,263 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
         rhs[b0 + tid] = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
     }
     if (i == 0 && tid < 4) rhs[P.kb + tid] = yk[tid];
+    if (i == 0 && tid == 0) Bw.flags[0] += 1;  // next call's epoch (k_bcr_persist)
+}
+
+// ---- persistent path: one resident workgroup per block for the whole solve -------------------
+// Workgroup i keeps D_i -> Cf_i and [A_l | A_r | R] -> [XL | XR | x] in LDS from its first load to
+// its back-substitution, so nothing of its own is stored or re-read. It folds the contributions of
+// its neighbours i -+ 2^m for every level m it survives (waiting on their "eliminated" flags),
+// eliminates at level ctz(i) (block 0: root) and publishes UL/UR/F/rL/rR, then waits for the
+// "back-substituted" flags of i -+ 2^ctz(i) and publishes y_i. The arithmetic and its order are
+// those of the per-level launches (k_bcr_elim / k_bcr_contrib / k_bcr_back): same results bit for bit.
+// Hand-offs follow the gfx950 inter-workgroup recipe: payload written and read with agent-scope
+// (sc1) 8-byte accesses, every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier
+// behind which ONE lane stores the flag; ONE lane polls (relaxed, s_sleep), the others read after a
+// barrier. Flags hold the call epoch (flags[0] + 1; k_bcr_border advances flags[0]), so nothing is
+// reset per call. Every spin is bounded: a timeout raises chol_flag and the step is rejected.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void st_pub(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_pub(const double* p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void publish_flag(unsigned* f, unsigned epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static constexpr unsigned SPIN_LIMIT = 1u << 22;
+// ONE lane polls fa then fb (either may be null); uniform result, false on timeout.
+__device__ bool wait_flags(const unsigned* fa, const unsigned* fb, unsigned epoch, int* lds_ok) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        const unsigned* fs[2] = {fa, fb};
+        for (int k = 0; k < 2 && ok; ++k) {
+            if (!fs[k]) continue;
+            unsigned n = 0;
+            while (__hip_atomic_load((gu32*)const_cast<unsigned*>(fs[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                   epoch) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++n > SPIN_LIMIT) { ok = 0; break; }
+            }
+        }
+        *lds_ok = ok;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+    __syncthreads();
+    return *lds_ok != 0;
+}
+
+struct PersistLds {
+    double T[BB * BLD];  // D_i -> Cf_i
+    double X[BB * XW];   // [A_l | A_r | R] -> [XL | XR | x]
+    double rdiag[BB];
+    double Wb[256];      // inverse of the current 16x16 diagonal tile
+    double Bl[4 * BB];   // border rows of block i
+    double red[80];
+    double yl[RSZ], yr[RSZ], yt[RSZ];
+    int ok;
+};
+
+__global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict__ st, DevProblem P,
+                                                       const double* __restrict__ S, const double* __restrict__ rhs,
+                                                       BcrWork Bw, int* __restrict__ flag) {
+    if (st->done) return;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    PersistLds& L = *reinterpret_cast<PersistLds*>(smem);
+    const int nblk = Bw.nblk;
+    const int i = blockIdx.x;
+    const bool root = i == 0;
+    const int mi = root ? Bw.levels : __builtin_ctz(i);  // elimination level of block i
+    const int tid = threadIdx.x;
+    const size_t ld = P.npad;
+    const int nd = 6 * P.nac;
+    const int b0 = i * G_DOF;
+    const unsigned epoch = Bw.flags[0] + 1;
+    unsigned* elim_f = Bw.flags + 16;
+    unsigned* back_f = Bw.flags + 16 + nblk;
+    constexpr int NQ = BSZ / TPB_E;
+    // ---- level-0 state (and the level-0 couplings of blocks eliminated at level 0)
+    {
+        double v[NQ], al[NQ], ar[NQ];
+        const bool has_r0 = i + 1 < nblk;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+            const bool ok = c <= r && r < G_DOF && b0 + r < nd;
+            v[q] = ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0);
+            if (mi == 0) {
+                const bool okl = r < G_DOF && b0 + r < nd && c < G_DOF;
+                al[q] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
+                const int b1 = b0 + G_DOF;
+                const bool okr = has_r0 && r < G_DOF && b1 + r < nd && c < G_DOF;
+                ar[q] = okr ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
+            }
+        }
+        const int r = tid >> 3, c = tid & 7, gr = b0 + r;
+        double rv = 0.0;
+        if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
+        const double blv = tid < 4 * BB ? border_load(P, S, i, tid) : 0.0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, rr_ = e >> 6, cc = e & 63;
+            L.T[rr_ * BLD + cc] = v[q];
+            if (mi == 0) {
+                L.X[rr_ * XW + cc] = al[q];
+                L.X[cc * XW + BB + rr_] = ar[q];
+            }
+        }
+        L.X[r * XW + 2 * BB + c] = rv;
+        if (tid < 4 * BB) L.Bl[tid] = blv;
+    }
+    // ---- survive levels 0 .. mi-1: fold the neighbours' contributions (same order as Dacc/Racc)
+    for (int m = 0; m < mi; ++m) {
+        const int s = 1 << m, a = i - s, b = i + s;
+        const bool last = m == mi - 1 && !root;
+        const bool has_r = i + 2 * s < nblk;  // right coupling at elimination level m + 1 = mi
+        if (!wait_flags(a >= 0 ? elim_f + a : nullptr, b < nblk ? elim_f + b : nullptr, epoch, &L.ok)) {
+            if (tid == 0) *flag = 1;
+            return;
+        }
+        double ua[NQ], ub[NQ], fl[NQ], fr[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q;
+            ua[q] = a >= 0 ? ld_pub(Bw.UR + (size_t)a * BSZ + e) : 0.0;
+            ub[q] = b < nblk ? ld_pub(Bw.UL + (size_t)b * BSZ + e) : 0.0;
+            if (last) {
+                fl[q] = ld_pub(Bw.F + (size_t)a * BSZ + e);
+                fr[q] = has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
+            }
+        }
+        const double ra = a >= 0 ? ld_pub(Bw.rR + (size_t)a * RSZ + tid) : 0.0;
+        const double rb = b < nblk ? ld_pub(Bw.rL + (size_t)b * RSZ + tid) : 0.0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, rr_ = e >> 6, cc = e & 63;
+            L.T[rr_ * BLD + cc] = (L.T[rr_ * BLD + cc] - ua[q]) - ub[q];
+            if (last) {
+                L.X[rr_ * XW + cc] = fl[q];
+                L.X[cc * XW + BB + rr_] = fr[q];
+            }
+        }
+        const int r = tid >> 3, c = tid & 7;
+        L.X[r * XW + 2 * BB + c] = (L.X[r * XW + 2 * BB + c] - ra) - rb;
+    }
+    __syncthreads();
+    // ---- eliminate: Cf = chol(D), X <- Cf^-1 X
+    bool bad = false;
+    potrf64_fwd_la(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad);
+    if (bad) *flag = 1;
+    if (root) {
+        double* Yl = L.yt;
+        {
+            const int r = tid >> 3, c = tid & 7;
+            Yl[tid] = L.X[r * XW + 2 * BB + c];
+        }
+        __syncthreads();
+        trsm_t_lanes(L.T, L.rdiag, Yl);
+        st_pub(Bw.Y + tid, Yl[tid]);
+        if (tid < 4) Bw.bk[tid] = rhs[P.kb + tid];
+        if (tid >= 4 && tid < 14) {
+            int q = tid - 4, mm = 0;
+            while (q > mm) { q -= mm + 1; ++mm; }
+            Bw.bk[tid] = S[(size_t)(P.kb + mm) * ld + P.kb + q];
+        }
+        __syncthreads();
+        border_partial(L.Bl, Yl, L.red, 0, Bw.Bp);
+        publish_flag(back_f, epoch);
+        return;
+    }
+    const int s = 1 << mi;
+    const bool has_r = i + s < nblk;
+    const int lane = tid & 63, wave = tid >> 6, rr = lane & 15, kq = lane >> 4;
+    // ---- Schur contributions from the LDS-resident X (tile map of k_bcr_contrib)
+    for (int t = wave; t < 4 * NCONTRIB_WG; t += NWE) {
+        int ib, cb, aoff, boff, ldd = BB;
+        double* dst;
+        double sign = 1.0;
+        bool rhs_tile = false;
+        if (t < 20) {
+            if (t >= 10 && !has_r) continue;
+            int p = 0, rem = t % 10;
+            while (rem > p) { rem -= p + 1; ++p; }
+            ib = p; cb = rem;
+            aoff = boff = (t < 10) ? 0 : BB;
+            dst = (t < 10 ? Bw.UL : Bw.UR) + (size_t)i * BSZ;
+        } else if (t < 36) {
+            if (!has_r) continue;
+            ib = (t - 20) >> 2; cb = (t - 20) & 3;
+            aoff = BB; boff = 0; sign = -1.0;
+            dst = Bw.F + (size_t)i * BSZ;
+        } else {
+            if (t >= 40 && !has_r) continue;
+            ib = (t - 36) & 3; cb = 0;
+            aoff = (t < 40) ? 0 : BB; boff = 2 * BB;
+            dst = (t < 40 ? Bw.rL : Bw.rR) + (size_t)i * RSZ;
+            ldd = RC;
+            rhs_tile = true;
+        }
+        const bool bcol_ok = !rhs_tile || rr < RC;
+        double av[16], bv[16];
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const double* row = L.X + (4 * s4 + kq) * XW;
+            av[s4] = row[aoff + 16 * ib + rr];
+            bv[s4] = bcol_ok ? row[boff + 16 * cb + rr] : 0.0;
+        }
+        d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 16; s4 += 2) {
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4 + 1], bv[s4 + 1], acc1, 0, 0, 0);
+        }
+        if (bcol_ok)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                st_pub(dst + (size_t)(16 * ib + kq + 4 * g) * ldd + 16 * cb + rr, sign * (acc0[g] + acc1[g]));
+    }
+    publish_flag(elim_f + i, epoch);
+    // ---- back-substitution: y_i = Cf^-T (x_i - XL y_{i-s} - XR y_{i+s})
+    if (!wait_flags(back_f + (i - s), has_r ? back_f + (i + s) : nullptr, epoch, &L.ok)) {
+        if (tid == 0) *flag = 1;
+        return;
+    }
+    L.yl[tid] = ld_pub(Bw.Y + (size_t)(i - s) * RSZ + tid);
+    L.yr[tid] = has_r ? ld_pub(Bw.Y + (size_t)(i + s) * RSZ + tid) : 0.0;
+    L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
+    __syncthreads();
+    if (wave < 4) {
+        double al[16], ar[16];
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const double* row = L.X + (16 * wave + rr) * XW + 4 * s4 + kq;
+            al[s4] = row[0];
+            ar[s4] = has_r ? row[BB] : 0.0;
+        }
+        d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const double bl = rr < RC ? L.yl[(4 * s4 + kq) * RC + rr] : 0.0;
+            const double br = rr < RC ? L.yr[(4 * s4 + kq) * RC + rr] : 0.0;
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bl, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s4], br, acc1, 0, 0, 0);
+        }
+        if (rr < RC)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) L.yt[(16 * wave + kq + 4 * g) * RC + rr] -= acc0[g] + acc1[g];
+    }
+    __syncthreads();
+    trsm_t_lanes(L.T, L.rdiag, L.yt);
+    st_pub(Bw.Y + (size_t)i * RSZ + tid, L.yt[tid]);
+    border_partial(L.Bl, L.yt, L.red, i, Bw.Bp);
+    publish_flag(back_f + i, epoch);
 }
 
 #define CKB(x)                            \
@@ -671,6 +1049,12 @@ template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
+    if (Bw.persist && !STAMP) {
+        BPL(K_BCR_PERSIST, k_bcr_persist, dim3(nblk), dim3(TPB_E), sizeof(PersistLds), s, W.st, P, W.S, W.rhs, Bw,
+            W.chol_flag);
+        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
+        return hipSuccess;
+    }
     for (int m = 0; m < Bw.levels; ++m) {
         const int nel = n_elim(nblk, m);
         const int nacc = m >= 1 ? (nblk + (2 << m) - 1) / (2 << m) : 0;
@@ -685,6 +1069,26 @@ static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& B
             stamps);
     BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
     return hipSuccess;
+}
+
+static hipError_t bcr_persist_attr() {
+    static bool done = false;
+    if (!done) {
+        CKB(hipFuncSetAttribute((const void*)k_bcr_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(PersistLds)));
+        done = true;
+    }
+    return hipSuccess;
+}
+
+bool bcr_persist_ok(int nblk) {
+    if (bcr_persist_attr() != hipSuccess) return false;
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist, TPB_E, sizeof(PersistLds)) != hipSuccess)
+        return false;
+    return per_cu >= 1 && nblk <= per_cu * ncu;
 }
 
 hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf) {

@@ -105,7 +105,11 @@ static constexpr int BCR_CAMS = 10;
 // plus one global slot: bk = [b_k (4) | S_kk lower (10)].
 struct BcrWork {
     double *Cf, *X, *UL, *UR, *F, *rL, *rR, *Dacc, *Racc, *Y, *Bp, *rd, *bk;
+    // persistent path: flags[0] = call epoch, flags[16 + i] = block i eliminated,
+    // flags[16 + nblk + i] = block i back-substituted (each holds the epoch that set it)
+    unsigned* flags;
     int nblk, levels;
+    int persist;  // 1 = one resident workgroup per block (k_bcr_persist), 0 = one launch per level
 };
 static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)5 * 64 * 64 + 64 * 136 + 4 * 64 * 8 + 32 + 64;
 
@@ -162,12 +166,12 @@ struct DevWork {
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
     K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
-    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_COUNT
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
     "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
-    "bcr_back", "bcr_border", "comm", "cam_reduce"};
+    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {
@@ -198,6 +202,8 @@ hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* p
 hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
+// true when nblk workgroups of k_bcr_persist can all be resident on the current device
+bool bcr_persist_ok(int nblk);
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s);
 

@@ -600,7 +600,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     }
     if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
     if (P.solver == 2) {
-        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16);
+        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 2 * bcr_nblk);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
         // upper tiles of UL/UR are never written and must read as zero
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
@@ -623,6 +623,11 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         Bw.Bp = Bw.Y + b8;
         Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
         Bw.bk = Bw.rd + (size_t)64 * bcr_nblk;
+        Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
+        Bw.persist = bcr_persist_ok(bcr_nblk) ? 1 : 0;
+        if (const char* e = std::getenv("MIBA_BCR")) {
+            if (!std::strcmp(e, "launch")) Bw.persist = 0;
+        }
     }
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
@@ -702,6 +707,18 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             kf[K_BCR_CONTRIB] = c_fl / std::max(L, 1); kb[K_BCR_CONTRIB] = c_by / std::max(L, 1);
             kf[K_BCR_BACK] = nblk * 2.0 * 64 * 64 * 8 * 2 / std::max(L, 1); kb[K_BCR_BACK] = b_by / std::max(L, 1);
             kb[K_BCR_BORDER] = nblk * (32.0 + 64 * 8) * 8;
+            // persistent kernel = the whole elimination + contributions + back-substitution in one
+            // launch; bytes: S blocks read once (D, level-0 couplings, border rows, rhs), the
+            // contributions written once and read by the two neighbours, y written / read twice.
+            double p_by = nblk * (blk + 4 * 64 * 8.0 + 64 * 8 * 8.0), n_el = 0;
+            for (int m = 0; m < L; ++m) {
+                const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
+                n_el += nel;
+                if (m == 0) p_by += nel * 2 * blk;
+            }
+            p_by += n_el * 3 * (3 * blk + 2 * 64 * 8 * 8.0) + nblk * 3 * 64 * 8 * 8.0;
+            kf[K_BCR_PERSIST] = e_fl + c_fl + kf[K_BCR_BACK] * std::max(L, 1);
+            kb[K_BCR_PERSIST] = p_by;
         }
         kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
         kb[K_BACKSUB_EVAL] = A * 2 * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read twice
