@@ -204,6 +204,8 @@ hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, h
 hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
 // true when nblk workgroups of k_bcr_persist can all be resident on the current device
 bool bcr_persist_ok(int nblk);
+// workgroups of k_schur_tile resident at once on the current device (CUs x blocks per CU)
+int schur_tile_slots();
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s);
 

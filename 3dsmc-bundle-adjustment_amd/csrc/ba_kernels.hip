@@ -1808,6 +1808,14 @@ static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
         if (pf) pf->end(s);                                                     \
     } while (0)
 
+int schur_tile_slots() {
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_schur_tile<false>, TPB, 0) != hipSuccess) return 0;
+    return per_cu * ncu;
+}
+
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
     if (P.n_seg > 0)
         PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr);

@@ -367,8 +367,12 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     for (int k = 0; k < 2; ++k)
         std::stable_sort(cls[k].begin(), cls[k].end(), [&](int a, int b) { return pmin[a] < pmin[b]; });
     // tiles over the tiled points: window [base, base + span), span <= TILE_WIN, <= TILE_PTS points;
-    // chunks of <= CHUNK_PTS points and <= CHUNK_OBS observations
-    constexpr int TILE_PTS = 128;
+    // chunks of <= CHUNK_PTS points and <= CHUNK_OBS observations. TILE_PTS spreads the points over
+    // (at least) one full wave of resident workgroups, so no second, partly empty wave of tiles runs.
+    int TILE_PTS = 128;
+    if (const int slots = schur_tile_slots(); slots > 0)
+        TILE_PTS = std::max(CHUNK_PTS, (int)((cls[0].size() + slots - 1) / slots));
+    if (const char* e = std::getenv("MIBA_TILE_PTS")) TILE_PTS = std::max(1, std::atoi(e));
     std::vector<int> tile_chunk(1, 0), tile_base, tile_span, chunk_ap(1, 0);
     {
         const std::vector<int>& T = cls[0];
