@@ -25,6 +25,7 @@
 // Cholesky; exact elimination, only the rounding order differs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -63,6 +64,11 @@ __device__ __forceinline__ unsigned long long bcr_stamp() {
         }                                                                                        \
     } while (0)
 
+__device__ __forceinline__ unsigned long long realtime_now() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
 __device__ __forceinline__ double bcast_b(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
@@ -245,7 +251,64 @@ __device__ __forceinline__ d4b mfma16_ab(const double* a, int lda, const double*
     return acc;
 }
 
-__device__ void potrf64_fwd_la(double* T, double* rdiag64, double* Wb, double* X, int ncol, bool& bad) {
+// Schur contributions of an eliminated block, accumulated k-block by k-block inside the
+// factorization: X's row block kb is final after phase 2 of panel kb, so waves 1-7 add
+// X_kb^T X_kb to their contribution tiles during phase 1 of panel kb + 1 (beside the trailing
+// update, while wave 0 runs the pivot chain); the caller adds the last row block. Tile map of
+// k_bcr_contrib: [0,10) UL lower, [10,20) UR lower, [20,36) F = -XR^T XL, [36,40) rL, [40,44) rR.
+static constexpr int NCONTRIB = 44;
+static constexpr int NCT = (NCONTRIB + NWE - 2) / (NWE - 1);  // tiles per helper wave
+struct ContribTile {
+    int ib, cb, aoff, boff, ldd;
+    double sign;
+    bool valid, rhs;
+};
+__device__ __forceinline__ ContribTile contrib_tile(int t, bool has_r) {
+    ContribTile c{0, 0, 0, 0, BB, 1.0, true, false};
+    if (t < 20) {
+        c.valid = t < 10 || has_r;
+        int p = 0, rem = t % 10;
+        while (rem > p) { rem -= p + 1; ++p; }
+        c.ib = p; c.cb = rem;
+        c.aoff = c.boff = (t < 10) ? 0 : BB;
+    } else if (t < 36) {
+        c.valid = has_r;
+        c.ib = (t - 20) >> 2; c.cb = (t - 20) & 3;
+        c.aoff = BB; c.boff = 0; c.sign = -1.0;
+    } else {
+        c.valid = t < 40 || has_r;
+        c.ib = (t - 36) & 3; c.cb = 0;
+        c.aoff = (t < 40) ? 0 : BB; c.boff = 2 * BB;
+        c.ldd = RC;
+        c.rhs = true;
+    }
+    return c;
+}
+__device__ __forceinline__ void contrib_accumulate(const double* X, int kbk, d4b (&cacc)[NCT], bool has_r, int wave,
+                                                   int rr, int kk) {
+    if (wave == 0) return;  // the pivot wave owns no contribution tile
+#pragma unroll
+    for (int q = 0; q < NCT; ++q) {
+        const int t = (wave - 1) + (NWE - 1) * q;
+        if (t >= NCONTRIB) continue;
+        const ContribTile ct = contrib_tile(t, has_r);
+        if (!ct.valid) continue;
+        const bool bok = !ct.rhs || rr < RC;
+        double av[4], bv[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const double* row = X + (16 * kbk + 4 * s4 + kk) * XW;
+            av[s4] = row[ct.aoff + 16 * ct.ib + rr];
+            bv[s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], cacc[q], 0, 0, 0);
+    }
+}
+
+template <bool CONTRIB>
+__device__ __forceinline__ void potrf64_fwd_la(double* T, double* rdiag64, double* Wb, double* X, int ncol, bool& bad,
+                                               d4b (&cacc)[NCT], bool has_r, unsigned long long* pst = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rr = lane & 15, kk = lane >> 4;
     const int ncb = (ncol + 15) >> 4;
@@ -286,8 +349,10 @@ __device__ void potrf64_fwd_la(double* T, double* rdiag64, double* Wb, double* X
                         for (int g = 0; g < 4; ++g) X[(16 * i + kk + 4 * g) * XW + 16 * cb + rr] -= acc[g];
                 }
             }
+            if constexpr (CONTRIB) contrib_accumulate(X, kb - 1, cacc, has_r, wave, rr, kk);
         }
         __syncthreads();
+        if (pst && tid == 0) pst[2 * kb] = realtime_now();
         // ---- phase 2
         const int nrow = 3 - kb;  // row tiles below the panel
         if (wave == 0) {
@@ -323,6 +388,7 @@ __device__ void potrf64_fwd_la(double* T, double* rdiag64, double* Wb, double* X
             }
         }
         __syncthreads();
+        if (pst && tid == 0) pst[2 * kb + 1] = realtime_now();
     }
 }
 
@@ -529,8 +595,10 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
     if (STAMP)
         potrf64_fwd<STAMP>(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad,
                            blockIdx.x == 0 ? stamps + 8 * 24 + 4 * m : nullptr);
-    else
-        potrf64_fwd_la(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad);
+    else {
+        d4b none[NCT];
+        potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad, none, false);
+    }
     if (bad) *flag = 1;
     BCR_STAMP(m, 2);
     if (root) {
@@ -831,10 +899,19 @@ struct PersistLds {
     int ok;
 };
 
+// timeline stamps (100 MHz realtime, comparable across XCDs): tl[32 i + k]
+#define TL(k)                                                                 \
+    do {                                                                      \
+        if constexpr (STAMP) if (threadIdx.x == 0) tl[32 * blockIdx.x + (k)] = realtime_now(); \
+    } while (0)
+
+template <bool STAMP>
 __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict__ st, DevProblem P,
                                                        const double* __restrict__ S, const double* __restrict__ rhs,
-                                                       BcrWork Bw, int* __restrict__ flag) {
+                                                       BcrWork Bw, int* __restrict__ flag,
+                                                       unsigned long long* __restrict__ tl) {
     if (st->done) return;
+    TL(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     PersistLds& L = *reinterpret_cast<PersistLds*>(smem);
     const int nblk = Bw.nblk;
@@ -882,6 +959,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
         L.X[r * XW + 2 * BB + c] = rv;
         if (tid < 4 * BB) L.Bl[tid] = blv;
     }
+    TL(1);
     // ---- survive levels 0 .. mi-1: fold the neighbours' contributions (same order as Dacc/Racc)
     for (int m = 0; m < mi; ++m) {
         const int s = 1 << m, a = i - s, b = i + s;
@@ -891,6 +969,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
             if (tid == 0) *flag = 1;
             return;
         }
+        TL(2 + m);
         double ua[NQ], ub[NQ], fl[NQ], fr[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -919,8 +998,21 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
     __syncthreads();
     // ---- eliminate: Cf = chol(D), X <- Cf^-1 X
     bool bad = false;
-    potrf64_fwd_la(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad);
+    __syncthreads();
+    TL(9);
+    const int s = 1 << mi;
+    const bool has_r = !root && i + s < nblk;
+    d4b cacc[NCT];
+#pragma unroll
+    for (int q = 0; q < NCT; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
+    unsigned long long* pst = nullptr;
+    if constexpr (STAMP) pst = tl + 32 * i + 16;
+    if (root)
+        potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, L.X + 2 * BB, RC, bad, cacc, false, pst);
+    else
+        potrf64_fwd_la<true>(L.T, L.rdiag, L.Wb, L.X, XW, bad, cacc, has_r, pst);
     if (bad) *flag = 1;
+    TL(10);
     if (root) {
         double* Yl = L.yt;
         {
@@ -939,62 +1031,35 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
         __syncthreads();
         border_partial(L.Bl, Yl, L.red, 0, Bw.Bp);
         publish_flag(back_f, epoch);
+        TL(14);
         return;
     }
-    const int s = 1 << mi;
-    const bool has_r = i + s < nblk;
     const int lane = tid & 63, wave = tid >> 6, rr = lane & 15, kq = lane >> 4;
-    // ---- Schur contributions from the LDS-resident X (tile map of k_bcr_contrib)
-    for (int t = wave; t < 4 * NCONTRIB_WG; t += NWE) {
-        int ib, cb, aoff, boff, ldd = BB;
-        double* dst;
-        double sign = 1.0;
-        bool rhs_tile = false;
-        if (t < 20) {
-            if (t >= 10 && !has_r) continue;
-            int p = 0, rem = t % 10;
-            while (rem > p) { rem -= p + 1; ++p; }
-            ib = p; cb = rem;
-            aoff = boff = (t < 10) ? 0 : BB;
-            dst = (t < 10 ? Bw.UL : Bw.UR) + (size_t)i * BSZ;
-        } else if (t < 36) {
-            if (!has_r) continue;
-            ib = (t - 20) >> 2; cb = (t - 20) & 3;
-            aoff = BB; boff = 0; sign = -1.0;
-            dst = Bw.F + (size_t)i * BSZ;
-        } else {
-            if (t >= 40 && !has_r) continue;
-            ib = (t - 36) & 3; cb = 0;
-            aoff = (t < 40) ? 0 : BB; boff = 2 * BB;
-            dst = (t < 40 ? Bw.rL : Bw.rR) + (size_t)i * RSZ;
-            ldd = RC;
-            rhs_tile = true;
-        }
-        const bool bcol_ok = !rhs_tile || rr < RC;
-        double av[16], bv[16];
+    // ---- Schur contributions: add the last row block of X, then publish (sc1)
+    contrib_accumulate(L.X, 3, cacc, has_r, wave, rr, kq);
 #pragma unroll
-        for (int s4 = 0; s4 < 16; ++s4) {
-            const double* row = L.X + (4 * s4 + kq) * XW;
-            av[s4] = row[aoff + 16 * ib + rr];
-            bv[s4] = bcol_ok ? row[boff + 16 * cb + rr] : 0.0;
-        }
-        d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < NCT; ++q) {
+        const int t = (wave - 1) + (NWE - 1) * q;
+        if (wave == 0 || t >= NCONTRIB) continue;
+        const ContribTile ct = contrib_tile(t, has_r);
+        if (!ct.valid || (ct.rhs && rr >= RC)) continue;
+        double* dst = (t < 10 ? Bw.UL : t < 20 ? Bw.UR : t < 36 ? Bw.F : t < 40 ? Bw.rL : Bw.rR) +
+                      (size_t)i * (ct.rhs ? RSZ : BSZ);
 #pragma unroll
-        for (int s4 = 0; s4 < 16; s4 += 2) {
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4 + 1], bv[s4 + 1], acc1, 0, 0, 0);
-        }
-        if (bcol_ok)
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                st_pub(dst + (size_t)(16 * ib + kq + 4 * g) * ldd + 16 * cb + rr, sign * (acc0[g] + acc1[g]));
+        for (int g = 0; g < 4; ++g)
+            st_pub(dst + (size_t)(16 * ct.ib + kq + 4 * g) * ct.ldd + 16 * ct.cb + rr, ct.sign * cacc[q][g]);
     }
     publish_flag(elim_f + i, epoch);
-    // ---- back-substitution: y_i = Cf^-T (x_i - XL y_{i-s} - XR y_{i+s})
+    TL(11);
+    // ---- off the critical path, while the higher levels finish: [P | Q | u] = Cf^-T [XL | XR | x]
+    trsm_lower64_t(L.T, L.rdiag, L.X, XW, XW);
+    TL(13);
+    // ---- back-substitution: y_i = u - P y_{i-s} - Q y_{i+s}  (= Cf^-T (x_i - XL y_{i-s} - XR y_{i+s}))
     if (!wait_flags(back_f + (i - s), has_r ? back_f + (i + s) : nullptr, epoch, &L.ok)) {
         if (tid == 0) *flag = 1;
         return;
     }
+    TL(12);
     L.yl[tid] = ld_pub(Bw.Y + (size_t)(i - s) * RSZ + tid);
     L.yr[tid] = has_r ? ld_pub(Bw.Y + (size_t)(i + s) * RSZ + tid) : 0.0;
     L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
@@ -1020,11 +1085,12 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
             for (int g = 0; g < 4; ++g) L.yt[(16 * wave + kq + 4 * g) * RC + rr] -= acc0[g] + acc1[g];
     }
     __syncthreads();
-    trsm_t_lanes(L.T, L.rdiag, L.yt);
     st_pub(Bw.Y + (size_t)i * RSZ + tid, L.yt[tid]);
     border_partial(L.Bl, L.yt, L.red, i, Bw.Bp);
     publish_flag(back_f + i, epoch);
+    TL(14);
 }
+#undef TL
 
 #define CKB(x)                            \
     do {                                  \
@@ -1032,6 +1098,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
         if (e_ != hipSuccess) return e_;  \
     } while (0)
 
+static constexpr int NSTAMP = 32 * 256;
 static inline int n_elim(int nblk, int m) {
     const int s = 1 << m;
     return (nblk - s + 2 * s - 1) / (2 * s);
@@ -1049,9 +1116,9 @@ template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
-    if (Bw.persist && !STAMP) {
-        BPL(K_BCR_PERSIST, k_bcr_persist, dim3(nblk), dim3(TPB_E), sizeof(PersistLds), s, W.st, P, W.S, W.rhs, Bw,
-            W.chol_flag);
+    if (Bw.persist) {
+        BPL(K_BCR_PERSIST, k_bcr_persist<STAMP>, dim3(nblk), dim3(TPB_E), sizeof(PersistLds), s, W.st, P, W.S, W.rhs,
+            Bw, W.chol_flag, stamps);
         BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
         return hipSuccess;
     }
@@ -1074,7 +1141,9 @@ static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& B
 static hipError_t bcr_persist_attr() {
     static bool done = false;
     if (!done) {
-        CKB(hipFuncSetAttribute((const void*)k_bcr_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
+        CKB(hipFuncSetAttribute((const void*)k_bcr_persist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(PersistLds)));
+        CKB(hipFuncSetAttribute((const void*)k_bcr_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(PersistLds)));
         done = true;
     }
@@ -1086,7 +1155,8 @@ bool bcr_persist_ok(int nblk) {
     int dev = 0, ncu = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist, TPB_E, sizeof(PersistLds)) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist<false>, TPB_E, sizeof(PersistLds)) !=
+        hipSuccess)
         return false;
     return per_cu >= 1 && nblk <= per_cu * ncu;
 }
@@ -1101,15 +1171,35 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         const char* e = getenv("MIBA_BCR_STAMPS");
-        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * 32 * 8 * 2));
+        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * NSTAMP));
         attr = true;
     }
     if (stamps) {
-        CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 32 * 8 * 2, s));
+        CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * NSTAMP, s));
         CKB(launch_bcr_t<true>(P, W, Bw, s, stamps, nullptr));
-        static unsigned long long h[32 * 8 * 2];
+        static unsigned long long h[NSTAMP];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
+        if (Bw.persist) {
+            // per block: level-0 loaded, survivor waits done, factor start/end, contributions published,
+            // back wait done, y published — us after the earliest start
+            unsigned long long t0 = ~0ull;
+            for (int i = 0; i < Bw.nblk && i < 256; ++i) if (h[32 * i]) t0 = std::min(t0, h[32 * i]);
+            auto us = [&](unsigned long long t) { return t ? (double)(t - t0) * 0.01 : -1.0; };
+            for (int i = 0; i < Bw.nblk && i < 256; ++i) {
+                const unsigned long long* q = h + 32 * i;
+                fprintf(stderr, "bcr blk %3d start %7.2f loaded %7.2f waits", i, us(q[0]), us(q[1]));
+                for (int m = 0; m < 7; ++m) if (q[2 + m]) fprintf(stderr, " %7.2f", us(q[2 + m]));
+                fprintf(stderr, " | factor %7.2f-%7.2f contrib %7.2f pre %7.2f back-wait %7.2f done %7.2f\n", us(q[9]),
+                        us(q[10]), us(q[11]), us(q[13]), us(q[12]), us(q[14]));
+                if (i <= 2) {
+                    fprintf(stderr, "    factor phases (end of phase 1 / phase 2 per panel):");
+                    for (int k = 0; k < 8; ++k) fprintf(stderr, " %7.2f", us(q[16 + k]));
+                    fprintf(stderr, "\n");
+                }
+            }
+            return hipSuccess;
+        }
         for (int m = 0; m <= Bw.levels; ++m) {
             const unsigned long long* q = h + (size_t)m * 8;
             const unsigned long long* b = h + (size_t)(16 + m) * 8;

@@ -166,22 +166,24 @@ def test_comm_init_rejects_bad_rank():
 
 @pytest.mark.parametrize("n_cams", [23, 64, 200, 333])
 def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
-    """The persistent BCR kernel (one resident workgroup per 10-camera block, flag hand-offs)
-    performs the same arithmetic in the same order as the per-level launches. The Schur flush into S
-    uses f64 atomics (summation order varies run to run), so the two agree to rounding, not bitwise."""
+    """The persistent BCR kernel (one resident workgroup per 10-camera block, flag hand-offs,
+    Schur contributions accumulated inside the factorization) against the per-level launches and
+    the oracle. The two GPU paths sum the contributions in different orders and the Schur flush into
+    S uses f64 atomics, so they agree to rounding: tolerances off, both run exactly 6 iterations."""
     from miba.solver import Solver
     p = synthetic.make_problem(n_cams, 40 * n_cams, obs_per_point=(4, 9), seed=n_cams)
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
     res = {}
     for mode in ("launch", "persist"):
         monkeypatch.setenv("MIBA_BCR", mode)
         q = p.copy()
-        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6) as s:
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
             res[mode] = (s.solve(q), q)
     (sa, qa), (sb, qb) = res["launch"], res["persist"]
     assert sa["linear_solver"] == sb["linear_solver"] == LS["bcr"]
-    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-12 * sa["final_cost"]
-    assert sa["num_iterations"] == sb["num_iterations"]
-    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-10)
-    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-9)
-    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6))
+    assert sa["num_iterations"] == sb["num_iterations"] == 6
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sa["final_cost"]
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
     assert abs(sb["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
