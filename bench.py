@@ -62,7 +62,7 @@ def parse():
 
 def load_pmc_traffic(kernel: str, config: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary, if present."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):  # newest first
         try:
             d = json.load(open(path))
         except Exception:
