@@ -199,7 +199,9 @@ hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevW
 hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
+// back-substitution, candidate evaluation, step scalars and the LM decision (k_final fuses k_lm_decide)
+hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, hipStream_t s,
+                         Prof* pf);
 hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
 // true when nblk workgroups of k_bcr_persist can all be resident on the current device

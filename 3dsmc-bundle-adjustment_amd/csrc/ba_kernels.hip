@@ -1505,11 +1505,66 @@ __global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st
     S[(size_t)(16 * ij.x + (threadIdx.x >> 4)) * npad + 16 * ij.y + (threadIdx.x & 15)] = 0.0;
 }
 
+// ---------------------------------------------------------------- envelope clear + assembly
+// One workgroup per envelope tile of S (16x16, one element per thread): every element is
+// written once — the camera blocks s U s + D^2 (lower), the border s C s_k, the intrinsics
+// block and the pad identity (rank 0; the landmark shards of other ranks contribute zeros),
+// zero elsewhere — and the diagonal tiles write their 16 rows of rhs. Replaces k_env_zero +
+// k_assemble + the chol_flag memset (same values as k_assemble, element for element).
+__global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                      const int2* __restrict__ tiles, const double* __restrict__ camdata,
+                                                      const double* __restrict__ lin, const double* __restrict__ scale,
+                                                      double* __restrict__ S, double* __restrict__ rhs,
+                                                      int* __restrict__ chol_flag) {
+    if (st->done) return;
+    const int2 ij = tiles[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
+    const int nd = 6 * P.nac, kb = P.kb;
+    const double* sk = scale + P.off_k;
+    double v = 0.0;
+    if (P.rank == 0) {
+        const double radius = st->radius;
+        if (r < nd && col <= r && r / 6 == col / 6) {
+            const int ac = r / 6, i = col - 6 * ac, j = r - 6 * ac;
+            const int q = 6 * i - i * (i - 1) / 2 + (j - i);
+            const double* sc = scale + 6 * ac;
+            v = sc[i] * camdata[(size_t)ac * CAMDATA + q] * sc[j];
+            if (i == j) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
+        } else if (r >= kb && r < kb + 4 && col < nd) {
+            const int m = r - kb, ac = col / 6, i = col - 6 * ac;
+            v = scale[6 * ac + i] * camdata[(size_t)ac * CAMDATA + 21 + i * 4 + m] * sk[m];
+        } else if (r >= kb && r < kb + 4 && col >= kb && col <= r) {
+            const int m = col - kb, l = r - kb;
+            const int q = 4 * m - m * (m - 1) / 2 + (l - m);
+            v = sk[m] * lin[2 + q] * sk[l];
+            if (l == m) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
+        } else if (r == col && r >= P.n) {
+            v = 1.0;
+        }
+    }
+    S[(size_t)r * P.npad + col] = v;
+    if (ij.x == ij.y && tid < 16) {
+        const int rr = 16 * ij.x + tid;
+        double b = 0.0;
+        if (P.rank == 0) {
+            if (rr < nd) b = scale[rr] * camdata[(size_t)(rr / 6) * CAMDATA + 45 + rr % 6];
+            else if (rr < kb + 4) b = sk[rr - kb] * lin[12 + rr - kb];
+        }
+        rhs[rr] = b;
+    }
+    if (blockIdx.x == 0 && tid == 0) *chol_flag = 0;
+}
+
 // ---------------------------------------------------------------- final
-// scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]
-__global__ __launch_bounds__(TPB) void k_final(DevProblem P, const LmState* __restrict__ st, int nblk_pt, int nblk_upd,
+__device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
+                               const double* __restrict__ scal, double* __restrict__ log);
+// scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]; then the LM decision (k_lm_decide's
+// body, fused: one launch less per iteration)
+__global__ __launch_bounds__(TPB) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                                int nblk_bs, const double* __restrict__ part,
-                                               const int* __restrict__ chol_flag, double* __restrict__ scal) {
+                                               const int* __restrict__ chol_flag, double* __restrict__ scal,
+                                               LmParams prm, const double* __restrict__ lin, double* __restrict__ log) {
     __shared__ double lds[4 * 4];
     __shared__ double out[4];
     __shared__ double red[4];
@@ -1544,6 +1599,7 @@ __global__ __launch_bounds__(TPB) void k_final(DevProblem P, const LmState* __re
         scal[SC_CAND] = out[2];
         scal[SC_GMAX_PT] = gm;
         scal[SC_BAD] = bad + (*chol_flag ? 4.0 : 0.0);
+        lm_decide_body(st, prm, lin, scal, log);
     }
 }
 
@@ -1608,7 +1664,8 @@ __global__ __launch_bounds__(TPB) void k_final_shard(DevProblem P, const LmState
         red[10] = *chol_flag ? 4.0 : 0.0;
     }
 }
-__global__ void k_combine(const LmState* __restrict__ st, const double* __restrict__ red, double* __restrict__ scal) {
+__global__ void k_combine(LmState* __restrict__ st, const double* __restrict__ red, double* __restrict__ scal,
+                          LmParams prm, const double* __restrict__ lin, double* __restrict__ log) {
     if (st->done || threadIdx.x != 0) return;
     scal[SC_SN2] = red[16 + 0] + red[6];
     scal[SC_MCC] = red[16 + 1] + red[7];
@@ -1616,6 +1673,7 @@ __global__ void k_combine(const LmState* __restrict__ st, const double* __restri
     scal[SC_XN2] = red[16 + 3] + red[9];
     scal[SC_GMAX_PT] = red[20];
     scal[SC_BAD] = red[21] + red[10];
+    lm_decide_body(st, prm, lin, scal, log);
 }
 
 // ---------------------------------------------------------------- LM control
@@ -1676,9 +1734,8 @@ __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* 
 // One thread: Ceres 2.0 TrustRegionMinimizer::Minimize bookkeeping for the step whose
 // scalars k_final produced (model cost change, candidate cost, |step|, |x_cand|, flags).
 // Same decisions, in the same order, as oracle_solve() (oracle/ba_oracle.c).
-__global__ void k_lm_decide(LmState* __restrict__ st, LmParams prm, const double* __restrict__ lin,
-                            const double* __restrict__ scal, double* __restrict__ log) {
-    if (threadIdx.x != 0) return;
+__device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
+                               const double* __restrict__ scal, double* __restrict__ log) {
     LmState S = *st;
     if (S.done) return;
     if (S.need_lin) {  // absorb the re-linearisation of the last accepted point
@@ -1762,6 +1819,11 @@ __global__ void k_lm_decide(LmState* __restrict__ st, LmParams prm, const double
     }
     lg[1] = cost_change; lg[3] = step_norm; lg[4] = rho; lg[5] = S.radius;
     *st = S;
+}
+
+__global__ void k_lm_decide(LmState* __restrict__ st, LmParams prm, const double* __restrict__ lin,
+                            const double* __restrict__ scal, double* __restrict__ log) {
+    if (threadIdx.x == 0) lm_decide_body(st, prm, lin, scal, log);
 }
 
 // ---------------------------------------------------------------- debug hook
@@ -1855,14 +1917,9 @@ hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Pro
 }
 
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
-    CK(hipMemsetAsync(W.chol_flag, 0, sizeof(int), s));
-    PL(K_MEMSET_S, k_env_zero, dim3(W.n_env), dim3(TPB), 0, s, W.st, W.env_tile, P.npad, W.S);
-    if (P.rank == 0) {  // camera / intrinsics blocks, LM diagonal, pad: once over the shards
-        PL(K_ASSEMBLE, k_assemble, dim3(nblocks(P.nac + 1, 64)), dim3(64), 0, s, P, c, W.st, W.camdata, W.lin, W.scale,
-           W.S, W.rhs);
-    } else {
-        CK(hipMemsetAsync(W.rhs, 0, sizeof(double) * P.npad, s));
-    }
+    // envelope of S: clear + camera / intrinsics blocks, LM diagonal, pad (rank 0 only), rhs, chol_flag
+    PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin, W.scale,
+       W.S, W.rhs, W.chol_flag);
     if (P.n_ap > 0)
         PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, W.st, 1, W.scale, W.cnp,
            W.pdata, W.S, W.rhs, W.part);
@@ -1958,7 +2015,8 @@ hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* p
     return hipSuccess;
 }
 
-hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
+hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, hipStream_t s,
+                         Prof* pf) {
     const int nb_upd = nblocks(P.nac + 1, TPB);
     PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.rhs, W.delta, W.part);
     const int nb_bs = P.n_bs_chunks;
@@ -1968,14 +2026,14 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, DevWork& W, hip
     const int nb_pt = P.n_ap > 0 ? nblocks(P.n_ap, TPB) : 0;
     if (!W.comm.on()) {
         PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
-           W.chol_flag, W.scal);
+           W.chol_flag, W.scal, prm, W.lin, W.log);
         return hipSuccess;
     }
     PL(K_FINAL, k_final_shard, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
        W.chol_flag, W.red);
     COMM(W.red, W.red + 16, 4, COMM_F64, COMM_SUM);
     COMM(W.red + 4, W.red + 20, 2, COMM_F64, COMM_MAX);
-    PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal);
+    PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal, prm, W.lin, W.log);
     return hipSuccess;
 }
 

@@ -368,21 +368,18 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         std::stable_sort(cls[k].begin(), cls[k].end(), [&](int a, int b) { return pmin[a] < pmin[b]; });
     // tiles over the tiled points: window [base, base + span), span <= TILE_WIN, <= TILE_PTS points;
     // chunks of <= CHUNK_PTS points and <= CHUNK_OBS observations. TILE_PTS spreads the points over
-    // (at least) one full wave of resident workgroups, so no second, partly empty wave of tiles runs.
-    int TILE_PTS = 128;
-    if (const int slots = schur_tile_slots(); slots > 0)
-        TILE_PTS = std::max(CHUNK_PTS, (int)((cls[0].size() + slots - 1) / slots));
-    if (const char* e = std::getenv("MIBA_TILE_PTS")) TILE_PTS = std::max(1, std::atoi(e));
-    std::vector<int> tile_chunk(1, 0), tile_base, tile_span, chunk_ap(1, 0);
-    {
+    // one wave of resident workgroups (no second, partly empty wave of tiles), grown until the tile
+    // count fits the resident slots.
+    std::vector<int> tile_chunk, tile_base, tile_span, chunk_ap;
+    auto build_tiles = [&](int tile_pts) {
+        tile_chunk.assign(1, 0); tile_base.clear(); tile_span.clear(); chunk_ap.assign(1, 0);
         const std::vector<int>& T = cls[0];
         const int n0 = (int)T.size();
         int i = 0;
         while (i < n0) {
             const int base = pmin[T[i]];
             int j = i, hi = base;
-            while (j < n0 && j - i < TILE_PTS && pmax[T[j]] - base < TILE_WIN) { hi = std::max(hi, pmax[T[j]]); ++j; }
-            // chunks
+            while (j < n0 && j - i < tile_pts && pmax[T[j]] - base < TILE_WIN) { hi = std::max(hi, pmax[T[j]]); ++j; }
             int c0 = i;
             while (c0 < j) {
                 int c1 = c0, nob = 0;
@@ -394,6 +391,18 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
             tile_base.push_back(base);
             tile_span.push_back(hi - base + 1);
             i = j;
+        }
+    };
+    {
+        const int slots = schur_tile_slots();
+        int tile_pts = 128;
+        if (slots > 0) tile_pts = std::max(CHUNK_PTS, (int)((cls[0].size() + slots - 1) / slots));
+        const char* e = std::getenv("MIBA_TILE_PTS");
+        if (e) tile_pts = std::max(1, std::atoi(e));
+        build_tiles(tile_pts);
+        for (int grow = 0; !e && slots > 0 && (int)tile_base.size() > slots && grow < 16; ++grow) {
+            tile_pts += std::max(1, tile_pts / 8);
+            build_tiles(tile_pts);
         }
     }
     // active point order: tiled (tile order), overflow, gauge-only
@@ -856,8 +865,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
             HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
             HIPCHECK(ctx, launch_build(P, C, W, s, pf));
             HIPCHECK(ctx, launch_factor(P, W, s, pf));
-            HIPCHECK(ctx, launch_update(P, C, W, s, pf));
-            HIPCHECK(ctx, launch_decide(P, prm, W, s, pf));
+            HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
         }
         HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
         HIPCHECK(ctx, hipStreamSynchronize(s));
