@@ -35,7 +35,8 @@ enum {
     PART_UPD_XN2,
     PART_BS_XN2,
     PART_INIT_XN2,
-    PART_NSLOTS
+    PART_PT_KK,                     // 14 slots: intrinsics Schur terms of k_point_prep (10 packed + 4)
+    PART_NSLOTS = PART_PT_KK + 14
 };
 // final scalars
 enum { SC_MCC = 0, SC_CAND, SC_SN2, SC_GMAX_PT, SC_BAD, SC_XN2, SC_N = 8 };

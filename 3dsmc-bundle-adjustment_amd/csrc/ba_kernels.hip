@@ -398,14 +398,36 @@ __global__ __launch_bounds__(TPB) void k_point_prep(DevProblem P, BaConsts c, co
     block_sum<14>(kk, lds, out);
     gmax = block_max(gmax, red);
     bad = block_max(bad, red);
+    // intrinsics terms: one partial per workgroup, summed in a fixed order by k_pp_reduce (a
+    // same-address f64 atomic per workgroup serialises at ~45 ns each: 391 x 14 of them cost ~17 us)
+    if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + blockIdx.x] = out[threadIdx.x];
     if (threadIdx.x == 0) {
-        const int kb = P.kb;
-        int q = 0;
-        for (int m = 0; m < 4; ++m)
-            for (int l = m; l < 4; ++l, ++q) atomicAdd(&S[(size_t)(kb + l) * P.npad + kb + m], out[q]);
-        for (int m = 0; m < 4; ++m) atomicAdd(&rhs[kb + m], out[10 + m]);
         part[PART_PT_GMAX * P.part_stride + blockIdx.x] = gmax;
         part[PART_PT_BAD * P.part_stride + blockIdx.x] = bad;
+    }
+}
+
+// S_kk += sum of the point workgroups' intrinsics Schur terms (fixed order), rhs_k likewise.
+__global__ __launch_bounds__(TPB) void k_pp_reduce(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
+                                                   const double* __restrict__ part, double* __restrict__ S,
+                                                   double* __restrict__ rhs) {
+    __shared__ double lds[4 * 14];
+    __shared__ double out[14];
+    if (st->done) return;
+    double acc[14];
+#pragma unroll
+    for (int q = 0; q < 14; ++q) acc[q] = 0.0;
+    for (int i = threadIdx.x; i < nblk_pt; i += TPB)
+#pragma unroll
+        for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + i];
+    block_sum<14>(acc, lds, out);
+    if (threadIdx.x < 10) {
+        int m = 0, q = threadIdx.x;
+        while (q >= 4 - m) { q -= 4 - m; ++m; }
+        const int l = m + q;  // packed (m, l), l >= m
+        S[(size_t)(P.kb + l) * P.npad + P.kb + m] += out[threadIdx.x];
+    } else if (threadIdx.x < 14) {
+        rhs[P.kb + threadIdx.x - 10] += out[threadIdx.x];
     }
 }
 
@@ -1923,6 +1945,8 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     if (P.n_ap > 0)
         PL(K_POINT_PREP, k_point_prep, dim3(nblocks(P.n_ap, TPB)), dim3(TPB), 0, s, P, c, W.st, 1, W.scale, W.cnp,
            W.pdata, W.S, W.rhs, W.part);
+    if (P.n_ap > 0)
+        PL(K_POINT_PREP, k_pp_reduce, dim3(1), dim3(TPB), 0, s, P, W.st, nblocks(P.n_ap, TPB), W.part, W.S, W.rhs);
     if (P.n_tiles > 0)
     {
         static int smode = -1;
