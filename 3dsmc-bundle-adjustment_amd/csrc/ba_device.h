@@ -33,12 +33,22 @@ __device__ __forceinline__ void quat_R(const double* __restrict__ p, double R[9]
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
 
+// 1/x: v_rcp_f64 + two Newton steps (within an ulp or two of the IEEE quotient; five dependent
+// ops instead of the ~10-instruction f64 division sequence on the per-observation critical path)
+__device__ __forceinline__ double rcp_f64(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-x, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+
 // Huber rho(s) and sqrt(rho'(s))  (Ceres HuberLoss::Evaluate; Corrector)
 __device__ __forceinline__ void huber(double s, double a, double b, double& rho0, double& sq_rho1) {
     if (s > b) {
         const double r = sqrt(s);
         rho0 = 2.0 * a * r - b;
-        sq_rho1 = sqrt(fmax(DBL_MIN, a / r));
+        sq_rho1 = sqrt(fmax(DBL_MIN, a * rcp_f64(r)));
     } else {
         rho0 = s;
         sq_rho1 = 1.0;
@@ -61,8 +71,9 @@ __device__ __forceinline__ void eval_obs(const BaConsts& c, const double* __rest
     const double x = R[0] * d0 + R[3] * d1 + R[6] * d2;
     const double y = R[1] * d0 + R[4] * d1 + R[7] * d2;
     const double z = R[2] * d0 + R[5] * d1 + R[8] * d2;
-    const double u = (K[0] * x + K[2] * z) / z;
-    const double v = (K[1] * y + K[3] * z) / z;
+    const double iz = rcp_f64(z);
+    const double u = (K[0] * x + K[2] * z) * iz;
+    const double v = (K[1] * y + K[3] * z) * iz;
     const double r0 = c.sw_r * (u - uo), r1 = c.sw_r * (v - vo), r2 = c.sw_d * (depth - z);
     double rr, gr, rd, gd;
     huber(r0 * r0 + r1 * r1, c.a_r, c.b_r, rr, gr);
@@ -85,8 +96,9 @@ __device__ __forceinline__ void lin_obs(const BaConsts& c, const double* __restr
     const double y = R[1] * d0 + R[4] * d1 + R[7] * d2;
     const double z = R[2] * d0 + R[5] * d1 + R[8] * d2;
     const double fx = K[0], fy = K[1], cx = K[2], cy = K[3];
-    const double u = (fx * x + cx * z) / z;
-    const double v = (fy * y + cy * z) / z;
+    const double iz = rcp_f64(z);
+    const double u = (fx * x + cx * z) * iz;
+    const double v = (fy * y + cy * z) * iz;
     const double r0 = c.sw_r * (u - uo), r1 = c.sw_r * (v - vo), r2 = c.sw_d * (depth - z);
     double rr, gr, rd, gd;
     huber(r0 * r0 + r1 * r1, c.a_r, c.b_r, rr, gr);
@@ -94,7 +106,6 @@ __device__ __forceinline__ void lin_obs(const BaConsts& c, const double* __restr
     o.cost = 0.5 * rr + 0.5 * rd;
     o.f[0] = gr * r0; o.f[1] = gr * r1; o.f[2] = gd * r2;
     o.ok = isfinite(o.cost) && isfinite(u) && isfinite(v);
-    const double iz = 1.0 / z;
     const double su = gr * c.sw_r;
     const double a00 = su * fx * iz, a02 = -su * fx * x * iz * iz;
     const double a11 = su * fy * iz, a12 = -su * fy * y * iz * iz;
