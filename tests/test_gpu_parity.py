@@ -187,3 +187,22 @@ def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
     np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
     assert abs(sb["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+
+
+@pytest.mark.parametrize("config,iters", [("C4", 3), ("C5", 2)])
+def test_large_configs_match_oracle(config, iters):
+    """BASELINE.json's largest single-window configurations (C4: 200 cams / 100k points / 1M obs,
+    C5: 1000 cams / 500k points / 5M obs) against the oracle for a few LM iterations (tolerances off,
+    the oracle needs ~1 s (C4) / ~6 s (C5) per iteration)."""
+    from miba.solver import Solver
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    p = synthetic.make_config(config)
+    q = p.copy()
+    with Solver(minimizer_progress_to_stdout=0, max_num_iterations=iters, **no_tol) as s:
+        sg = s.solve(p)
+    so = oracle.solve(q, oracle.default_options(max_num_iterations=iters, **no_tol))
+    assert sg["num_iterations"] == so["num_iterations"] == iters
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sg, so)
+    np.testing.assert_allclose(p.cams, q.cams, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(p.intr, q.intr, rtol=1e-9)
