@@ -974,8 +974,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int e = tid + TPB_E * q;
-            ua[q] = a >= 0 ? ld_pub(Bw.UR + (size_t)a * BSZ + e) : 0.0;
-            ub[q] = b < nblk ? ld_pub(Bw.UL + (size_t)b * BSZ + e) : 0.0;
+            const bool lower = ((e & 63) >> 4) <= ((e >> 6) >> 4);  // UR / UL upper tiles are zero and unread
+            ua[q] = a >= 0 && lower ? ld_pub(Bw.UR + (size_t)a * BSZ + e) : 0.0;
+            ub[q] = b < nblk && lower ? ld_pub(Bw.UL + (size_t)b * BSZ + e) : 0.0;
             if (last) {
                 fl[q] = ld_pub(Bw.F + (size_t)a * BSZ + e);
                 fr[q] = has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
