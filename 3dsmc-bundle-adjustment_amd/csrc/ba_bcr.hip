@@ -1093,6 +1093,358 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
 }
 #undef TL
 
+// ---- split persistent path: two resident workgroups per block --------------------------------
+// F(i) ("factor") holds D_i and runs only the pivot side of the 64x64 Cholesky (potrf16 + W per
+// panel, the T trailing updates and row panels), publishing each finished column panel (L tiles,
+// W_kb, 1/diag) to global memory. H(i) ("helper", another CU) holds [A_l | A_r | R] and applies the
+// panels as they arrive: X_kb <- W_kb X_kb, X_i -= L(i,kb) X_kb, and the Schur contributions of row
+// block kb; it publishes the contributions, then runs the back-substitution from its copy of L.
+// F's pivot chain thus no longer shares its CU's f64 pipes with the 136-column MFMA work.
+// Hand-offs as in k_bcr_persist; panel flags hold 4 * epoch + kb (monotone, polled with >=).
+struct FLds {
+    double T[BB * BLD];
+    double rdiag[BB];
+    double Wb[256];
+    int ok;
+};
+struct HLds {
+    double X[BB * XW];
+    double L[BB * BLD];   // copy of Cf, filled panel by panel
+    double rdiag[BB];
+    double W[4][256];
+    double Bl[4 * BB];
+    double red[80];
+    double yl[RSZ], yr[RSZ], yt[RSZ];
+    int ok;
+};
+static constexpr int PANEL_DOUBLES = BB * BB + 4 * 256 + BB;  // per block: L tiles | W_0..3 | 1/diag
+
+__device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        unsigned n = 0;
+        while (__hip_atomic_load((gu32*)const_cast<unsigned*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++n > SPIN_LIMIT) { ok = 0; break; }
+        }
+        *lds_ok = ok;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    return *lds_ok != 0;
+}
+
+static constexpr int NCT8 = (NCONTRIB + NWE - 1) / NWE;  // contribution tiles per wave (all 8 waves)
+__device__ __forceinline__ void contrib_accumulate8(const double* X, int kbk, d4b (&cacc)[NCT8], bool has_r, int wave,
+                                                    int rr, int kk) {
+#pragma unroll
+    for (int q = 0; q < NCT8; ++q) {
+        const int t = wave + NWE * q;
+        if (t >= NCONTRIB) continue;
+        const ContribTile ct = contrib_tile(t, has_r);
+        if (!ct.valid) continue;
+        const bool bok = !ct.rhs || rr < RC;
+        double av[4], bv[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const double* row = X + (16 * kbk + 4 * s4 + kk) * XW;
+            av[s4] = row[ct.aoff + 16 * ct.ib + rr];
+            bv[s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], cacc[q], 0, 0, 0);
+    }
+}
+
+#define TLS(k)                                                                                     \
+    do {                                                                                           \
+        if constexpr (STAMP) if (threadIdx.x == 0) tl[32 * blockIdx.x + (k)] = realtime_now();      \
+    } while (0)
+template <bool STAMP>
+__global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__ st, DevProblem P,
+                                                     const double* __restrict__ S, const double* __restrict__ rhs,
+                                                     BcrWork Bw, int* __restrict__ flag,
+                                                     unsigned long long* __restrict__ tl) {
+    if (st->done) return;
+    TLS(0);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nblk = Bw.nblk;
+    const int i = blockIdx.x >> 1;
+    const bool helper = blockIdx.x & 1;
+    const bool root = i == 0;
+    const int mi = root ? Bw.levels : __builtin_ctz(i);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
+    const size_t ld = P.npad;
+    const int nd = 6 * P.nac;
+    const int b0 = i * G_DOF;
+    const unsigned epoch = Bw.flags[0] + 1;
+    unsigned* elim_f = Bw.flags + 16;
+    unsigned* back_f = Bw.flags + 16 + nblk;
+    unsigned* panel_f = Bw.flags + 16 + 2 * nblk;
+    double* pg = Bw.Cf + (size_t)i * PANEL_DOUBLES;  // this block's published panels
+    constexpr int NQ = BSZ / TPB_E;
+    const int s_i = 1 << mi;
+    const bool has_r = !root && i + s_i < nblk;
+    if (!helper) {
+        // ================= F: D_i, pivot side of the factorization
+        FLds& L = *reinterpret_cast<FLds*>(smem);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+            const bool ok = c <= r && r < G_DOF && b0 + r < nd;
+            L.T[r * BLD + c] = ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0);
+        }
+        for (int m = 0; m < mi; ++m) {
+            const int s = 1 << m, a = i - s, b = i + s;
+            if (!wait_flags(a >= 0 ? elim_f + a : nullptr, b < nblk ? elim_f + b : nullptr, epoch, &L.ok)) {
+                if (tid == 0) *flag = 1;
+                return;
+            }
+            double ua[NQ], ub[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q;
+                const bool lower = ((e & 63) >> 4) <= ((e >> 6) >> 4);
+                ua[q] = a >= 0 && lower ? ld_pub(Bw.UR + (size_t)a * BSZ + e) : 0.0;
+                ub[q] = b < nblk && lower ? ld_pub(Bw.UL + (size_t)b * BSZ + e) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+                L.T[r * BLD + c] = (L.T[r * BLD + c] - ua[q]) - ub[q];
+            }
+        }
+        __syncthreads();
+        TLS(1);
+        bool bad = false;
+        double* T = L.T;
+        for (int kb = 0; kb < 4; ++kb) {
+            double* Tkk = T + (16 * kb) * BLD + 16 * kb;
+            if (wave == 0) {
+                potrf16_tile(Tkk, BLD, L.rdiag + 16 * kb, lane, bad);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < 16) {
+                    double v[16];
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) v[m] = (m == lane) ? 1.0 : 0.0;
+                    fwd16(v, Tkk, L.rdiag + 16 * kb);
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) L.Wb[m * 16 + lane] = v[m];
+                }
+            } else if (kb > 0) {
+                const int p = kb - 1, nt = 4 - kb;
+                const int npairs = nt * (nt + 1) / 2 - 1;
+                for (int t = wave - 1; t < npairs; t += NWE - 1) {
+                    int q = t + 1, a = 0;
+                    while (q > a) { q -= a + 1; ++a; }
+                    const int ii = kb + a, jj = kb + q;
+                    const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * p, BLD, T + (16 * jj) * BLD + 16 * p, BLD, rr, kk);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
+                }
+            }
+            __syncthreads();
+            if (wave == 0) {
+                if (kb < 3) {
+                    double* Ai = T + (16 * (kb + 1)) * BLD + 16 * kb;
+                    const d4b acc = mfma16_abt(Ai, BLD, L.Wb, 16, rr, kk);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Ai[(kk + 4 * g) * BLD + rr] = acc[g];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const d4b acc2 = mfma16_abt(Ai, BLD, Ai, BLD, rr, kk);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) T[(16 * (kb + 1) + kk + 4 * g) * BLD + 16 * (kb + 1) + rr] -= acc2[g];
+                }
+            } else {
+                for (int t = wave - 1; t < 2 - kb; t += NWE - 1) {
+                    double* Ai = T + (16 * (kb + 2 + t)) * BLD + 16 * kb;
+                    const d4b acc = mfma16_abt(Ai, BLD, L.Wb, 16, rr, kk);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Ai[(kk + 4 * g) * BLD + rr] = acc[g];
+                }
+            }
+            __syncthreads();
+            // publish column panel kb: tiles (ii, kb) for ii >= kb, W_kb, 1/diag
+            for (int e = tid; e < (4 - kb) * 256; e += TPB_E) {
+                const int r = 16 * kb + (e >> 4), c = 16 * kb + (e & 15);
+                st_pub(pg + r * BB + c, T[r * BLD + c]);
+            }
+            if (tid < 256) st_pub(pg + BB * BB + kb * 256 + tid, L.Wb[tid]);
+            if (tid < 16) st_pub(pg + BB * BB + 4 * 256 + 16 * kb + tid, L.rdiag[16 * kb + tid]);
+            publish_flag(panel_f + i, 4 * epoch + kb);
+            TLS(2 + kb);
+        }
+        if (bad) *flag = 1;
+        return;
+    }
+    // ================= H: [A_l | A_r | R], panel application, contributions, back-substitution
+    HLds& L = *reinterpret_cast<HLds*>(smem);
+    {
+        const bool has_r0 = i + 1 < nblk;
+        if (mi == 0) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+                const bool okl = r < G_DOF && b0 + r < nd && c < G_DOF;
+                L.X[r * XW + c] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
+                const int b1 = b0 + G_DOF;
+                const bool okr = has_r0 && r < G_DOF && b1 + r < nd && c < G_DOF;
+                L.X[c * XW + BB + r] = okr ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
+            }
+        }
+        const int r = tid >> 3, c = tid & 7, gr = b0 + r;
+        double rv = 0.0;
+        if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
+        L.X[r * XW + 2 * BB + c] = rv;
+        if (tid < 4 * BB) L.Bl[tid] = border_load(P, S, i, tid);
+    }
+    for (int m = 0; m < mi; ++m) {
+        const int s = 1 << m, a = i - s, b = i + s;
+        const bool last = m == mi - 1 && !root;
+        if (!wait_flags(a >= 0 ? elim_f + a : nullptr, b < nblk ? elim_f + b : nullptr, epoch, &L.ok)) {
+            if (tid == 0) *flag = 1;
+            return;
+        }
+        if (last) {
+            double fl[NQ], fr[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q;
+                fl[q] = ld_pub(Bw.F + (size_t)a * BSZ + e);
+                fr[q] = has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+                L.X[r * XW + c] = fl[q];
+                L.X[c * XW + BB + r] = fr[q];
+            }
+        }
+        const double ra = a >= 0 ? ld_pub(Bw.rR + (size_t)a * RSZ + tid) : 0.0;
+        const double rb = b < nblk ? ld_pub(Bw.rL + (size_t)b * RSZ + tid) : 0.0;
+        const int r = tid >> 3, c = tid & 7;
+        L.X[r * XW + 2 * BB + c] = (L.X[r * XW + 2 * BB + c] - ra) - rb;
+    }
+    TLS(1);
+    double* X = root ? L.X + 2 * BB : L.X;
+    const int ncol = root ? RC : XW;
+    const int ncb = (ncol + 15) >> 4;
+    d4b cacc[NCT8];
+#pragma unroll
+    for (int q = 0; q < NCT8; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
+    for (int kb = 0; kb < 4; ++kb) {
+        if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok)) {
+            if (tid == 0) *flag = 1;
+            return;
+        }
+        TLS(2 + 2 * kb);
+        for (int e = tid; e < (4 - kb) * 256; e += TPB_E) {
+            const int r = 16 * kb + (e >> 4), c = 16 * kb + (e & 15);
+            L.L[r * BLD + c] = ld_pub(pg + r * BB + c);
+        }
+        if (tid < 256) L.W[kb][tid] = ld_pub(pg + BB * BB + kb * 256 + tid);
+        if (tid < 16) L.rdiag[16 * kb + tid] = ld_pub(pg + BB * BB + 4 * 256 + 16 * kb + tid);
+        __syncthreads();
+        // X_kb <- W_kb X_kb
+        for (int t = wave; t < ncb; t += NWE) {
+            const bool colok = 16 * t + rr < ncol;
+            double* Xc = X + (16 * kb) * XW + 16 * t;
+            const d4b acc = mfma16_ab(L.W[kb], 16, Xc, XW, rr, kk, colok);
+            if (colok)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) Xc[(kk + 4 * g) * XW + rr] = acc[g];
+        }
+        __syncthreads();
+        // X_ii -= L(ii,kb) X_kb for ii > kb, and the contributions of row block kb
+        for (int t = wave; t < (3 - kb) * ncb; t += NWE) {
+            const int ii = kb + 1 + t / ncb, cb = t % ncb;
+            const bool colok = 16 * cb + rr < ncol;
+            const d4b acc = mfma16_ab(L.L + (16 * ii) * BLD + 16 * kb, BLD, X + (16 * kb) * XW + 16 * cb, XW, rr, kk, colok);
+            if (colok)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) X[(16 * ii + kk + 4 * g) * XW + 16 * cb + rr] -= acc[g];
+        }
+        if (!root) contrib_accumulate8(L.X, kb, cacc, has_r, wave, rr, kk);
+        __syncthreads();
+        TLS(3 + 2 * kb);
+    }
+    if (root) {
+        double* Yl = L.yt;
+        {
+            const int r = tid >> 3, c = tid & 7;
+            Yl[tid] = L.X[r * XW + 2 * BB + c];
+        }
+        __syncthreads();
+        trsm_t_lanes(L.L, L.rdiag, Yl);
+        st_pub(Bw.Y + tid, Yl[tid]);
+        if (tid < 4) Bw.bk[tid] = rhs[P.kb + tid];
+        if (tid >= 4 && tid < 14) {
+            int q = tid - 4, mm = 0;
+            while (q > mm) { q -= mm + 1; ++mm; }
+            Bw.bk[tid] = S[(size_t)(P.kb + mm) * ld + P.kb + q];
+        }
+        __syncthreads();
+        border_partial(L.Bl, Yl, L.red, 0, Bw.Bp);
+        publish_flag(back_f, epoch);
+        TLS(14);
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < NCT8; ++q) {
+        const int t = wave + NWE * q;
+        if (t >= NCONTRIB) continue;
+        const ContribTile ct = contrib_tile(t, has_r);
+        if (!ct.valid || (ct.rhs && rr >= RC)) continue;
+        double* dst = (t < 10 ? Bw.UL : t < 20 ? Bw.UR : t < 36 ? Bw.F : t < 40 ? Bw.rL : Bw.rR) +
+                      (size_t)i * (ct.rhs ? RSZ : BSZ);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            st_pub(dst + (size_t)(16 * ct.ib + kk + 4 * g) * ct.ldd + 16 * ct.cb + rr, ct.sign * cacc[q][g]);
+    }
+    publish_flag(elim_f + i, epoch);
+    TLS(10);
+    // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
+    trsm_lower64_t(L.L, L.rdiag, L.X, XW, XW);
+    if (!wait_flags(back_f + (i - s_i), has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
+        if (tid == 0) *flag = 1;
+        return;
+    }
+    TLS(12);
+    L.yl[tid] = ld_pub(Bw.Y + (size_t)(i - s_i) * RSZ + tid);
+    L.yr[tid] = has_r ? ld_pub(Bw.Y + (size_t)(i + s_i) * RSZ + tid) : 0.0;
+    L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
+    __syncthreads();
+    if (wave < 4) {
+        double al[16], ar[16];
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const double* row = L.X + (16 * wave + rr) * XW + 4 * s4 + kk;
+            al[s4] = row[0];
+            ar[s4] = has_r ? row[BB] : 0.0;
+        }
+        d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const double bl = rr < RC ? L.yl[(4 * s4 + kk) * RC + rr] : 0.0;
+            const double br = rr < RC ? L.yr[(4 * s4 + kk) * RC + rr] : 0.0;
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bl, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s4], br, acc1, 0, 0, 0);
+        }
+        if (rr < RC)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) L.yt[(16 * wave + kk + 4 * g) * RC + rr] -= acc0[g] + acc1[g];
+    }
+    __syncthreads();
+    st_pub(Bw.Y + (size_t)i * RSZ + tid, L.yt[tid]);
+    border_partial(L.Bl, L.yt, L.red, i, Bw.Bp);
+    publish_flag(back_f + i, epoch);
+    TLS(14);
+}
+#undef TLS
+static_assert(PANEL_DOUBLES <= BCR_BLOCK_DOUBLES, "published panels fit the block's workspace");
+
 #define CKB(x)                            \
     do {                                  \
         hipError_t e_ = (x);              \
@@ -1117,6 +1469,12 @@ template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
+    if (Bw.persist == 2) {
+        BPL(K_BCR_PERSIST, k_bcr_split<STAMP>, dim3(2 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw,
+            W.chol_flag, stamps);
+        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
+        return hipSuccess;
+    }
     if (Bw.persist) {
         BPL(K_BCR_PERSIST, k_bcr_persist<STAMP>, dim3(nblk), dim3(TPB_E), sizeof(PersistLds), s, W.st, P, W.S, W.rhs,
             Bw, W.chol_flag, stamps);
@@ -1146,20 +1504,27 @@ static hipError_t bcr_persist_attr() {
                                 (int)sizeof(PersistLds)));
         CKB(hipFuncSetAttribute((const void*)k_bcr_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(PersistLds)));
+        CKB(hipFuncSetAttribute((const void*)k_bcr_split<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(HLds)));
+        CKB(hipFuncSetAttribute((const void*)k_bcr_split<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(HLds)));
         done = true;
     }
     return hipSuccess;
 }
 
-bool bcr_persist_ok(int nblk) {
-    if (bcr_persist_attr() != hipSuccess) return false;
-    int dev = 0, ncu = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+int bcr_persist_ok(int nblk) {
+    if (bcr_persist_attr() != hipSuccess) return 0;
+    int dev = 0, ncu = 0, per_cu = 0, per_cu2 = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false>, TPB_E, sizeof(HLds)) == hipSuccess &&
+        per_cu2 >= 1 && 2 * nblk <= per_cu2 * ncu)
+        return 2;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist<false>, TPB_E, sizeof(PersistLds)) !=
         hipSuccess)
-        return false;
-    return per_cu >= 1 && nblk <= per_cu * ncu;
+        return 0;
+    return per_cu >= 1 && nblk <= per_cu * ncu ? 1 : 0;
 }
 
 hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf) {
@@ -1181,6 +1546,22 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
         static unsigned long long h[NSTAMP];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
+        if (Bw.persist == 2) {
+            unsigned long long t0 = ~0ull;
+            for (int g = 0; g < 2 * Bw.nblk && g < 256; ++g) if (h[32 * g]) t0 = std::min(t0, h[32 * g]);
+            auto us = [&](unsigned long long t) { return t ? (double)(t - t0) * 0.01 : -1.0; };
+            for (int g = 0; g < 2 * Bw.nblk && g < 256; ++g) {
+                const unsigned long long* q = h + 32 * g;
+                if (g % 2 == 0)
+                    fprintf(stderr, "bcr F%3d start %7.2f loaded %7.2f panels %7.2f %7.2f %7.2f %7.2f\n", g / 2, us(q[0]),
+                            us(q[1]), us(q[2]), us(q[3]), us(q[4]), us(q[5]));
+                else
+                    fprintf(stderr, "bcr H%3d start %7.2f loaded %7.2f panel got/done %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f contrib %7.2f back-wait %7.2f done %7.2f\n",
+                            g / 2, us(q[0]), us(q[1]), us(q[2]), us(q[3]), us(q[4]), us(q[5]), us(q[6]), us(q[7]), us(q[8]),
+                            us(q[9]), us(q[10]), us(q[12]), us(q[14]));
+            }
+            return hipSuccess;
+        }
         if (Bw.persist) {
             // per block: level-0 loaded, survivor waits done, factor start/end, contributions published,
             // back wait done, y published — us after the earliest start

@@ -110,7 +110,8 @@ struct BcrWork {
     // flags[16 + nblk + i] = block i back-substituted (each holds the epoch that set it)
     unsigned* flags;
     int nblk, levels;
-    int persist;  // 1 = one resident workgroup per block (k_bcr_persist), 0 = one launch per level
+    int persist;  // 2 = factor + helper workgroups per block (k_bcr_split), 1 = one resident workgroup per
+                  // block (k_bcr_persist), 0 = one launch per level
 };
 static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)5 * 64 * 64 + 64 * 136 + 4 * 64 * 8 + 32 + 64;
 
@@ -205,8 +206,9 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
                          Prof* pf);
 hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
-// true when nblk workgroups of k_bcr_persist can all be resident on the current device
-bool bcr_persist_ok(int nblk);
+// 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
+// when the nblk workgroups of k_bcr_persist can, else 0
+int bcr_persist_ok(int nblk);
 // workgroups of k_schur_tile resident at once on the current device (CUs x blocks per CU)
 int schur_tile_slots();
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,

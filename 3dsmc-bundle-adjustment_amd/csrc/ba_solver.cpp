@@ -613,7 +613,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     }
     if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
     if (P.solver == 2) {
-        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 2 * bcr_nblk);
+        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 3 * bcr_nblk);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
         // upper tiles of UL/UR are never written and must read as zero
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
@@ -637,9 +637,10 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
         Bw.bk = Bw.rd + (size_t)64 * bcr_nblk;
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
-        Bw.persist = bcr_persist_ok(bcr_nblk) ? 1 : 0;
+        Bw.persist = bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
+            else if (!std::strcmp(e, "persist") && Bw.persist == 2) Bw.persist = 1;  // "split" or unset: default
         }
     }
     DevWork& W = ctx->W;
