@@ -60,6 +60,9 @@ def parse():
     return ap.parse_args()
 
 
+PMC_ALIASES = {"bcr_persist": ("bcr_persist", "bcr_split")}  # profiler id -> kernel symbols it times
+
+
 def load_pmc_traffic(kernel: str, config: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary, if present."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):  # newest first
@@ -67,9 +70,10 @@ def load_pmc_traffic(kernel: str, config: str):
             d = json.load(open(path))
         except Exception:
             continue
-        rec = d.get(config, {}).get(kernel)
-        if rec and rec.get("hbm_bytes_per_launch"):
-            return float(rec["hbm_bytes_per_launch"])
+        for name in PMC_ALIASES.get(kernel, (kernel,)):
+            rec = d.get(config, {}).get(name)
+            if rec and rec.get("hbm_bytes_per_launch"):
+                return float(rec["hbm_bytes_per_launch"])
     return None
 
 
