@@ -40,7 +40,8 @@ static constexpr int TPB_C = 256;        // contrib / back workgroups: 4 waves
 static constexpr int BB = 64;            // block size (dofs)
 static constexpr int BLD = 66;           // LDS row stride of 64x64 blocks
 static constexpr int RC = 8;             // rhs columns: u, V(4), 3 pad
-static constexpr int XW = 2 * BB + RC;   // [XL | XR | x] width (global and LDS stride)
+static constexpr int XW = BCR_XW;        // [XL | XR | x] row stride (global and LDS)
+static constexpr int XC = 2 * BB + RC;   // [XL | XR | x] columns
 static constexpr int G_DOF = 6 * BCR_CAMS;
 static constexpr int BSZ = BB * BB;
 static constexpr int XSZ = BB * XW;
@@ -593,11 +594,11 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
     BCR_STAMP(m, 1);
     bool bad = false;
     if (STAMP)
-        potrf64_fwd<STAMP>(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad,
+        potrf64_fwd<STAMP>(L.T, L.rdiag, root ? L.X + 2 * BB : L.X, root ? RC : XC, bad,
                            blockIdx.x == 0 ? stamps + 8 * 24 + 4 * m : nullptr);
     else {
         d4b none[NCT];
-        potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XW, bad, none, false);
+        potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XC, bad, none, false);
     }
     if (bad) *flag = 1;
     BCR_STAMP(m, 2);
@@ -1011,7 +1012,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
     if (root)
         potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, L.X + 2 * BB, RC, bad, cacc, false, pst);
     else
-        potrf64_fwd_la<true>(L.T, L.rdiag, L.Wb, L.X, XW, bad, cacc, has_r, pst);
+        potrf64_fwd_la<true>(L.T, L.rdiag, L.Wb, L.X, XC, bad, cacc, has_r, pst);
     if (bad) *flag = 1;
     TL(10);
     if (root) {
@@ -1053,7 +1054,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
     publish_flag(elim_f + i, epoch);
     TL(11);
     // ---- off the critical path, while the higher levels finish: [P | Q | u] = Cf^-T [XL | XR | x]
-    trsm_lower64_t(L.T, L.rdiag, L.X, XW, XW);
+    trsm_lower64_t(L.T, L.rdiag, L.X, XW, XC);
     TL(13);
     // ---- back-substitution: y_i = u - P y_{i-s} - Q y_{i+s}  (= Cf^-T (x_i - XL y_{i-s} - XR y_{i+s}))
     if (!wait_flags(back_f + (i - s), has_r ? back_f + (i + s) : nullptr, epoch, &L.ok)) {
@@ -1329,7 +1330,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     }
     TLS(1);
     double* X = root ? L.X + 2 * BB : L.X;
-    const int ncol = root ? RC : XW;
+    const int ncol = root ? RC : XC;
     const int ncb = (ncol + 15) >> 4;
     d4b cacc[NCT8];
 #pragma unroll
@@ -1406,7 +1407,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     publish_flag(elim_f + i, epoch);
     TLS(10);
     // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
-    trsm_lower64_t(L.L, L.rdiag, L.X, XW, XW);
+    trsm_lower64_t(L.L, L.rdiag, L.X, XW, XC);
     if (!wait_flags(back_f + (i - s_i), has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
         if (tid == 0) *flag = 1;
         return;

@@ -113,7 +113,9 @@ struct BcrWork {
     int persist;  // 2 = factor + helper workgroups per block (k_bcr_split), 1 = one resident workgroup per
                   // block (k_bcr_persist), 0 = one launch per level
 };
-static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)5 * 64 * 64 + 64 * 136 + 4 * 64 * 8 + 32 + 64;
+// [XL | XR | x] row stride (136 columns; padding to 144 for conflict-free operand rows measured no gain)
+static constexpr int BCR_XW = 136;
+static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)5 * 64 * 64 + 64 * BCR_XW + 4 * 64 * 8 + 32 + 64;
 
 // Device-resident Levenberg-Marquardt state (Ceres 2.0 TrustRegionMinimizer +
 // LevenbergMarquardtStrategy bookkeeping, owned by k_lm_decide).

@@ -625,7 +625,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         const size_t b64 = (size_t)64 * 64 * bcr_nblk, b8 = (size_t)64 * 8 * bcr_nblk;
         Bw.Cf = base;
         Bw.X = Bw.Cf + b64;
-        Bw.UL = Bw.X + (size_t)64 * 136 * bcr_nblk;
+        Bw.UL = Bw.X + (size_t)64 * BCR_XW * bcr_nblk;
         Bw.UR = Bw.UL + b64;
         Bw.F = Bw.UR + b64;
         Bw.Dacc = Bw.F + b64;
