@@ -1107,6 +1107,7 @@ struct FLds {
     double rdiag[BB];
     double Wb[256];
     int ok;
+    int sync[12];  // look-ahead flags of the factor workgroup (k_bcr_split)
 };
 struct HLds {
     double X[BB * XW];
@@ -1117,14 +1118,19 @@ struct HLds {
     double red[80];
     double yl[RSZ], yr[RSZ], yt[RSZ];
     int ok;
+    int pre;  // next panel's flags already set (prefetch)
 };
 static constexpr int PANEL_DOUBLES = BB * BB + 4 * 256 + BB;  // per block: L tiles | W_0..3 | 1/diag
 
-__device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok) {
+// ONE lane polls f (>= target) and, if given, f2 (>= target2); uniform result, false on timeout.
+__device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok, const unsigned* f2 = nullptr,
+                        unsigned target2 = 0) {
     if (threadIdx.x == 0) {
         int ok = 1;
         unsigned n = 0;
-        while (__hip_atomic_load((gu32*)const_cast<unsigned*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load((gu32*)const_cast<unsigned*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target ||
+               (f2 && __hip_atomic_load((gu32*)const_cast<unsigned*>(f2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                          target2)) {
             __builtin_amdgcn_s_sleep(2);
             if (++n > SPIN_LIMIT) { ok = 0; break; }
         }
@@ -1161,7 +1167,48 @@ __device__ __forceinline__ void contrib_accumulate8(const double* X, int kbk, d4
     do {                                                                                           \
         if constexpr (STAMP) if (threadIdx.x == 0) tl[32 * blockIdx.x + (k)] = realtime_now();      \
     } while (0)
-template <bool STAMP>
+// Helper roles: NH = 1 -> one helper H per block owning all of [XL | XR | x] and every contribution;
+// NH = 2 -> helper A owns [XL | x] (UL, rL), helper B owns [XR | x] (UR, rR); A then publishes its
+// final XL and B forms the fill F = -XR^T XL, the back-substitution data [P | Q | u] and y_i.
+// x (8 columns) is forward-substituted by both (same arithmetic, bitwise identical copies): its row
+// block r lives in LDS and belongs to wave 4 + r (waves 0-3 hold the four XL / XR column tiles, one
+// per SIMD), so x_kb <- W_kb x_kb runs beside the column tiles and x_ii -= L(ii,kb) x_kb beside the
+// contributions.
+struct HelperMap {
+    int cb;                // column tile of [XL | XR | x] owned by this wave (-1: none)
+    int ntile;             // contribution tiles of this helper
+    int tiles[NCT8];       // contribution tile ids (contrib_tile map) of this wave
+};
+template <int NH>
+__device__ __forceinline__ HelperMap helper_map(int role, int wave, bool root) {
+    HelperMap h{-1, 0, {}};
+    if (root) {  // root: only the x columns (NH = 1: wave 0 of the helper; NH = 2: LDS rows, below)
+        h.cb = (NH == 1 && wave == 0) ? 0 : -1;
+        return h;
+    }
+    if (NH == 1) {
+        h.cb = wave;  // + the x tile (cb 8) on wave 0, handled by own2
+#pragma unroll
+        for (int q = 0; q < NCT8; ++q) {
+            const int t = (NWE - 1 - wave) + NWE * q;
+            h.tiles[q] = t < NCONTRIB ? t : -1;
+        }
+        return h;
+    }
+    const bool B = role == 2;
+    h.cb = wave < 4 ? (B ? 4 + wave : wave) : -1;  // one XL / XR tile per SIMD; x rows: x_rows_* below
+    // A: UL (0..9) + rL (36..39); B: UR (10..19) + rR (40..43); entry w and w + 8 of the list
+#pragma unroll
+    for (int q = 0; q < NCT8; ++q) {
+        const int e = wave + NWE * q;
+        int t = -1;
+        if (q < 2 && e < 14) t = e < 10 ? (B ? 10 + e : e) : (B ? 40 + e - 10 : 36 + e - 10);
+        h.tiles[q] = t;
+    }
+    return h;
+}
+
+template <bool STAMP, int NH>
 __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__ st, DevProblem P,
                                                      const double* __restrict__ S, const double* __restrict__ rhs,
                                                      BcrWork Bw, int* __restrict__ flag,
@@ -1170,8 +1217,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     TLS(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nblk = Bw.nblk;
-    const int i = blockIdx.x >> 1;
-    const bool helper = blockIdx.x & 1;
+    const int i = blockIdx.x / (NH + 1);
+    const int role = blockIdx.x % (NH + 1);  // 0 factor, 1 helper (A), 2 helper B
     const bool root = i == 0;
     const int mi = root ? Bw.levels : __builtin_ctz(i);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
@@ -1179,14 +1226,19 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const int nd = 6 * P.nac;
     const int b0 = i * G_DOF;
     const unsigned epoch = Bw.flags[0] + 1;
-    unsigned* elim_f = Bw.flags + 16;
+    unsigned* elim_f = Bw.flags + 16;              // NH = 1: all contributions; NH = 2: helper A's (UL, rL)
     unsigned* back_f = Bw.flags + 16 + nblk;
     unsigned* panel_f = Bw.flags + 16 + 2 * nblk;
+    unsigned* elimB_f = NH == 2 ? Bw.flags + 16 + 3 * nblk : elim_f;  // helper B's (UR, rR)
+    unsigned* fill_f = NH == 2 ? Bw.flags + 16 + 4 * nblk : elim_f;   // F of block i
+    unsigned* xl_f = Bw.flags + 16 + 5 * nblk;                         // NH = 2: final XL of block i
+    unsigned* ul_f = elim_f;   // producers of UL / rL
+    unsigned* ur_f = elimB_f;  // producers of UR / rR
     double* pg = Bw.Cf + (size_t)i * PANEL_DOUBLES;  // this block's published panels
     constexpr int NQ = BSZ / TPB_E;
     const int s_i = 1 << mi;
     const bool has_r = !root && i + s_i < nblk;
-    if (!helper) {
+    if (role == 0) {
         // ================= F: D_i, pivot side of the factorization
         FLds& L = *reinterpret_cast<FLds*>(smem);
 #pragma unroll
@@ -1195,9 +1247,10 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             const bool ok = c <= r && r < G_DOF && b0 + r < nd;
             L.T[r * BLD + c] = ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0);
         }
+        if (tid < 12) L.sync[tid] = 0;
         for (int m = 0; m < mi; ++m) {
             const int s = 1 << m, a = i - s, b = i + s;
-            if (!wait_flags(a >= 0 ? elim_f + a : nullptr, b < nblk ? elim_f + b : nullptr, epoch, &L.ok)) {
+            if (!wait_flags(a >= 0 ? ur_f + a : nullptr, b < nblk ? ul_f + b : nullptr, epoch, &L.ok)) {
                 if (tid == 0) *flag = 1;
                 return;
             }
@@ -1217,14 +1270,97 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
         __syncthreads();
         TLS(1);
-        bool bad = false;
+        // Look-ahead factorization with wave roles and LDS flags instead of workgroup barriers:
+        //   wave 0     pivot chain of the tall column block kb (rows 16 kb..63, all 64 lanes): the
+        //              diagonal tile and the row panels below it in one pass (no L_kk^-1 on this path)
+        //   waves 1-3  the critical update of column block kb + 1 by panel kb (one tile each), which
+        //              wave 0 waits for before its next chain
+        //   wave 5     W_kb = L_kk^-1 and the publication of panel kb (L tiles, W_kb, 1/diag) + flag
+        //   waves 6-7  the non-critical trailing tiles (panel 0 on column blocks 2, 3; panel 1 on 3)
+        //   wave 4     idle (it shares wave 0's SIMD: its f64 work would slow the pivot chain)
+        // Every tile's updates run in panel order on one wave or behind a counter.
         double* T = L.T;
-        for (int kb = 0; kb < 4; ++kb) {
-            double* Tkk = T + (16 * kb) * BLD + 16 * kb;
-            if (wave == 0) {
-                potrf16_tile(Tkk, BLD, L.rdiag + 16 * kb, lane, bad);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int* const sync = L.sync;  // [0] panels factored, [1..4] crit[kb], [5..8] trailing done per column block
+        auto lds_ld = [&](int k) { return __hip_atomic_load(sync + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
+        auto spin_ge = [&](int k, int v) {
+            unsigned n = 0;
+            while (lds_ld(k) < v) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++n > SPIN_LIMIT) return false;
+            }
+            return true;
+        };
+        auto tile_sub = [&](int ii, int jj, int p) {  // T(ii,jj) -= L(ii,p) L(jj,p)^T
+            const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * p, BLD, T + (16 * jj) * BLD + 16 * p, BLD, rr, kk);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
+        };
+        auto signal = [&](int k) {  // one add per wave, after the wave's LDS stores
+            if (lane == 0) __hip_atomic_fetch_add(sync + k, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        bool ok = true;
+        if (wave == 0) {
+            bool bad = false;
+            for (int kb = 0; kb < 4; ++kb) {
+                if (kb > 0 && !spin_ge(1 + kb - 1, 4 - kb)) { ok = false; break; }  // column block kb updated
+                TLS(17 + 3 * kb);
+                const int r = lane, row = 16 * kb + r;
+                const bool live = row < BB;
+                double a[16];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) a[c] = live ? T[row * BLD + 16 * kb + c] : 0.0;
+                double my_inv = 0.0;
+                double dn = bcast_b(a[0], 0);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    // d = current pivot; y ~ d^-1/2 (v_rsq_f64), one Newton step folded into l = a y (1 + e/2)
+                    const double d = dn;
+                    bad = bad || !(d > 0.0 && d < INFINITY);
+                    const double y = __builtin_amdgcn_rsq(d);
+                    const double e = __builtin_fma(-d * y, y, 1.0);
+                    const double l = __builtin_fma(0.5 * a[j] * y, e, a[j] * y);
+                    my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+                    a[j] = l;
+                    if (j < 15) {
+                        // next pivot first: on lane j + 1, bcast(l, j + 1) == l
+                        dn = bcast_b(__builtin_fma(-l, l, a[j + 1]), j + 1);
+#pragma unroll
+                        for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast_b(l, k), a[k]);
+                    }
+                }
+                if (live)
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) T[row * BLD + 16 * kb + c] = (r >= 16 || c <= r) ? a[c] : 0.0;
+                if (r < 16) L.rdiag[16 * kb + r] = my_inv;
+                if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                TLS(16 + 3 * kb);
+            }
+            if (bad) *flag = 1;
+        } else if (wave <= 3) {
+            for (int kb = 0; kb + wave <= 3 && kb < 3; ++kb) {
+                if (!spin_ge(0, kb + 1)) { ok = false; break; }
+                // earlier panels' (trailing) updates of column block kb + 1: 2 tiles each for blocks 2, 3
+                if (kb + 1 >= 2 && !spin_ge(5 + kb + 1, 2)) { ok = false; break; }
+                tile_sub(kb + wave, kb + 1, kb);
+                signal(1 + kb);
+            }
+        } else if (wave == 6) {  // tile (3,3): panel 0, then panel 1
+            for (int p = 0; p < 2 && ok; ++p) {
+                if (!spin_ge(0, p + 1)) { ok = false; break; }
+                tile_sub(3, 3, p);
+                signal(5 + 3);
+            }
+        } else if (wave == 7) {  // tiles (2,2), (3,2): panel 0
+            if (!spin_ge(0, 1)) ok = false;
+            else {
+                tile_sub(2, 2, 0);
+                tile_sub(3, 2, 0);
+                __hip_atomic_fetch_add(sync + 5 + 2, lane == 0 ? 2 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (wave == 5) {
+            for (int kb = 0; kb < 4; ++kb) {
+                if (!spin_ge(0, kb + 1)) { ok = false; break; }
+                const double* Tkk = T + (16 * kb) * BLD + 16 * kb;
                 if (lane < 16) {
                     double v[16];
 #pragma unroll
@@ -1233,54 +1369,30 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                     for (int m = 0; m < 16; ++m) L.Wb[m * 16 + lane] = v[m];
                 }
-            } else if (kb > 0) {
-                const int p = kb - 1, nt = 4 - kb;
-                const int npairs = nt * (nt + 1) / 2 - 1;
-                for (int t = wave - 1; t < npairs; t += NWE - 1) {
-                    int q = t + 1, a = 0;
-                    while (q > a) { q -= a + 1; ++a; }
-                    const int ii = kb + a, jj = kb + q;
-                    const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * p, BLD, T + (16 * jj) * BLD + 16 * p, BLD, rr, kk);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // publish column panel kb: tiles (ii, kb) for ii >= kb, W_kb, 1/diag
+                for (int e = lane; e < (4 - kb) * 256; e += 64) {
+                    const int r = 16 * kb + (e >> 4), c = 16 * kb + (e & 15);
+                    st_pub(pg + r * BB + c, T[r * BLD + c]);
+                }
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
+                for (int u = 0; u < 4; ++u) st_pub(pg + BB * BB + kb * 256 + lane + 64 * u, L.Wb[lane + 64 * u]);
+                if (lane < 16) st_pub(pg + BB * BB + 4 * 256 + 16 * kb + lane, L.rdiag[16 * kb + lane]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) {
+                    __hip_atomic_store((gu32*)(panel_f + i), 4 * epoch + kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if constexpr (STAMP) tl[32 * blockIdx.x + 2 + kb] = realtime_now();
                 }
             }
-            __syncthreads();
-            if (wave == 0) {
-                if (kb < 3) {
-                    double* Ai = T + (16 * (kb + 1)) * BLD + 16 * kb;
-                    const d4b acc = mfma16_abt(Ai, BLD, L.Wb, 16, rr, kk);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) Ai[(kk + 4 * g) * BLD + rr] = acc[g];
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    const d4b acc2 = mfma16_abt(Ai, BLD, Ai, BLD, rr, kk);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) T[(16 * (kb + 1) + kk + 4 * g) * BLD + 16 * (kb + 1) + rr] -= acc2[g];
-                }
-            } else {
-                for (int t = wave - 1; t < 2 - kb; t += NWE - 1) {
-                    double* Ai = T + (16 * (kb + 2 + t)) * BLD + 16 * kb;
-                    const d4b acc = mfma16_abt(Ai, BLD, L.Wb, 16, rr, kk);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) Ai[(kk + 4 * g) * BLD + rr] = acc[g];
-                }
-            }
-            __syncthreads();
-            // publish column panel kb: tiles (ii, kb) for ii >= kb, W_kb, 1/diag
-            for (int e = tid; e < (4 - kb) * 256; e += TPB_E) {
-                const int r = 16 * kb + (e >> 4), c = 16 * kb + (e & 15);
-                st_pub(pg + r * BB + c, T[r * BLD + c]);
-            }
-            if (tid < 256) st_pub(pg + BB * BB + kb * 256 + tid, L.Wb[tid]);
-            if (tid < 16) st_pub(pg + BB * BB + 4 * 256 + 16 * kb + tid, L.rdiag[16 * kb + tid]);
-            publish_flag(panel_f + i, 4 * epoch + kb);
-            TLS(2 + kb);
         }
-        if (bad) *flag = 1;
+        if (!ok) *flag = 1;
         return;
     }
-    // ================= H: [A_l | A_r | R], panel application, contributions, back-substitution
+    // ================= helpers: panel application, contributions, back-substitution
+    const bool roleA = NH == 2 && role == 1;  // NH = 2: XL side (exits after publishing XL)
+    const bool roleB = NH == 1 || role == 2;  // owns XR, the fill and the back-substitution
+    if (root && roleA) return;                // the root has only the x columns (helper B)
     HLds& L = *reinterpret_cast<HLds*>(smem);
     {
         const bool has_r0 = i + 1 < nblk;
@@ -1288,39 +1400,53 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-                const bool okl = r < G_DOF && b0 + r < nd && c < G_DOF;
-                L.X[r * XW + c] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
-                const int b1 = b0 + G_DOF;
-                const bool okr = has_r0 && r < G_DOF && b1 + r < nd && c < G_DOF;
-                L.X[c * XW + BB + r] = okr ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
+                if (NH == 1 || roleA) {
+                    const bool okl = r < G_DOF && b0 + r < nd && c < G_DOF;
+                    L.X[r * XW + c] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
+                }
+                if (NH == 1 || roleB) {
+                    const int b1 = b0 + G_DOF;
+                    const bool okr = has_r0 && r < G_DOF && b1 + r < nd && c < G_DOF;
+                    L.X[c * XW + BB + r] = okr ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
+                }
             }
         }
         const int r = tid >> 3, c = tid & 7, gr = b0 + r;
         double rv = 0.0;
         if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
         L.X[r * XW + 2 * BB + c] = rv;
-        if (tid < 4 * BB) L.Bl[tid] = border_load(P, S, i, tid);
+        if (roleB && tid < 4 * BB) L.Bl[tid] = border_load(P, S, i, tid);
     }
     for (int m = 0; m < mi; ++m) {
         const int s = 1 << m, a = i - s, b = i + s;
         const bool last = m == mi - 1 && !root;
-        if (!wait_flags(a >= 0 ? elim_f + a : nullptr, b < nblk ? elim_f + b : nullptr, epoch, &L.ok)) {
+        // x -= rR(a) + rL(b); at the last survived level the fills F(a) -> XL, F(b)^T -> XR
+        const unsigned* fa = a >= 0 ? ur_f + a : nullptr;
+        const unsigned* fb = b < nblk ? ul_f + b : nullptr;
+        if (!wait_flags(fa, fb, epoch, &L.ok)) {
             if (tid == 0) *flag = 1;
             return;
+        }
+        if (last && NH == 2) {
+            const unsigned* ff = roleA ? fill_f + a : (has_r ? fill_f + b : nullptr);
+            if (!wait_flags(ff, nullptr, epoch, &L.ok)) {
+                if (tid == 0) *flag = 1;
+                return;
+            }
         }
         if (last) {
             double fl[NQ], fr[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int e = tid + TPB_E * q;
-                fl[q] = ld_pub(Bw.F + (size_t)a * BSZ + e);
-                fr[q] = has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
+                fl[q] = (NH == 1 || roleA) ? ld_pub(Bw.F + (size_t)a * BSZ + e) : 0.0;
+                fr[q] = (NH == 1 || roleB) && has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
             }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-                L.X[r * XW + c] = fl[q];
-                L.X[c * XW + BB + r] = fr[q];
+                if (NH == 1 || roleA) L.X[r * XW + c] = fl[q];
+                if (NH == 1 || roleB) L.X[c * XW + BB + r] = fr[q];
             }
         }
         const double ra = a >= 0 ? ld_pub(Bw.rR + (size_t)a * RSZ + tid) : 0.0;
@@ -1331,46 +1457,223 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     TLS(1);
     double* X = root ? L.X + 2 * BB : L.X;
     const int ncol = root ? RC : XC;
-    const int ncb = (ncol + 15) >> 4;
+    // Column-tile ownership (helper_map): each wave keeps its column tiles of X in registers
+    // (MFMA accumulator layout x[g] = X[16 ii + kk + 4 g][16 cb + rr], which is also the B-operand
+    // layout of a 16x16x4 step), so the forward substitution of its columns (X_kb <- W_kb X_kb,
+    // X_ii -= L(ii,kb) X_kb) needs no barrier and no LDS round trip; only the finished row block kb
+    // is stored to LDS, for the Schur contributions of all waves.
+    const HelperMap hm = helper_map<NH>(role, wave, root);
+    constexpr int MAXOWN = NH == 1 ? 2 : 1;
+    int own_cb[MAXOWN];
+    own_cb[0] = hm.cb;
+    if constexpr (MAXOWN > 1) own_cb[1] = (!root && wave == 0) ? 8 : -1;
+    d4b xt[MAXOWN][4];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MAXOWN; ++j) {
+        const int cb = own_cb[j];
+        const bool colok = cb >= 0 && 16 * cb + rr < ncol;
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) xt[j][ii][g] = colok ? X[(16 * ii + kk + 4 * g) * XW + 16 * cb + rr] : 0.0;
+    }
     d4b cacc[NCT8];
 #pragma unroll
     for (int q = 0; q < NCT8; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
+    // NH = 2: helper A stores its finished XL row block kb (sc1) during its X update of panel kb and
+    // raises xl_f = 4 epoch + kb after that panel's contributions (the drain is then nearly free);
+    // helper B loads it at the start of panel kb + 2 (rows 2, 3 after its last panel; its
+    // back-substitution needs XL) and, when the block has a right neighbour, accumulates the fill
+    // F = -XR^T XL row block by row block.
+    const bool xl_on = NH == 2 && !root;
+    const bool fill_on = xl_on && has_r;
+    // XL of this block, 64 x 64 (stride BB), in the Dacc slot (used only by the per-level launches;
+    // the published panels, 5184 doubles per block, run past Cf into the X slots)
+    double* xlg = Bw.Dacc + (size_t)i * BSZ;
+    d4b facc[2] = {d4b{0.0, 0.0, 0.0, 0.0}, d4b{0.0, 0.0, 0.0, 0.0}};
+    auto fill_rows = [&](int kbk) {  // facc += XR_kbk^T XL_kbk for F tiles 20 + wave + 8 q
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const ContribTile ct = contrib_tile(20 + wave + NWE * q, true);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const double* row = L.X + (16 * kbk + 4 * s4 + kk) * XW;
+                facc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(row[ct.aoff + 16 * ct.ib + rr], row[ct.boff + 16 * ct.cb + rr],
+                                                               facc[q], 0, 0, 0);
+            }
+        }
+    };
+    // Panel data of panel kb (and helper B's XL_{kb-2} rows) -> registers, then LDS. When the helper
+    // runs behind the factor workgroup, the flags of panel kb + 1 are already set by the end of the
+    // X update of panel kb: its loads are then issued before the contributions of panel kb, which
+    // hide their latency (one poll round trip + one load round trip per panel otherwise).
+    double pv[6];
+    auto issue = [&](int k) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + TPB_E * u;
+            const int r = 16 * k + (e >> 4), c = 16 * k + (e & 15);
+            pv[u] = e < (4 - k) * 256 ? ld_pub(pg + r * BB + c) : 0.0;
+        }
+        pv[2] = tid < 256 ? ld_pub(pg + BB * BB + k * 256 + tid) : 0.0;
+        pv[3] = tid < 16 ? ld_pub(pg + BB * BB + 4 * 256 + 16 * k + tid) : 0.0;
+        if (xl_on && roleB && k >= 2)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = tid + TPB_E * u, r = 16 * (k - 2) + (e >> 6), c = e & 63;
+                pv[4 + u] = ld_pub(xlg + r * BB + c);
+            }
+    };
+    auto commit = [&](int k) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + TPB_E * u;
+            if (e < (4 - k) * 256) L.L[(16 * k + (e >> 4)) * BLD + 16 * k + (e & 15)] = pv[u];
+        }
+        if (tid < 256) L.W[k][tid] = pv[2];
+        if (tid < 16) L.rdiag[16 * k + tid] = pv[3];
+        if (xl_on && roleB && k >= 2)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = tid + TPB_E * u;
+                L.X[(16 * (k - 2) + (e >> 6)) * XW + (e & 63)] = pv[4 + u];
+            }
+    };
+    bool have = false;  // panel kb's loads already issued (prefetched)
+#pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-        if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok)) {
-            if (tid == 0) *flag = 1;
-            return;
+        if (!have) {
+            const bool xl_now = xl_on && roleB && kb >= 2;
+            if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok, xl_now ? xl_f + i : nullptr, 4 * epoch + kb - 2)) {
+                if (tid == 0) *flag = 1;
+                return;
+            }
+            issue(kb);
         }
         TLS(2 + 2 * kb);
-        for (int e = tid; e < (4 - kb) * 256; e += TPB_E) {
-            const int r = 16 * kb + (e >> 4), c = 16 * kb + (e & 15);
-            L.L[r * BLD + c] = ld_pub(pg + r * BB + c);
+        commit(kb);
+        // early flag reads for the prefetch test (consumed after the X update)
+        // (lane 0 of wave 7: in the two-helper layout it has no work in the X-update phase of panels 0-2,
+        // so the flag loads' latency stays off the waves that compute)
+        constexpr int TPOLL = 7 * 64;
+        unsigned fpan = 0, fxl = ~0u;
+        if (kb < 3 && tid == TPOLL) {
+            fpan = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xl_on && roleB && kb + 1 >= 2)
+                fxl = __hip_atomic_load((gu32*)(xl_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (tid < 256) L.W[kb][tid] = ld_pub(pg + BB * BB + kb * 256 + tid);
-        if (tid < 16) L.rdiag[16 * kb + tid] = ld_pub(pg + BB * BB + 4 * 256 + 16 * kb + tid);
         __syncthreads();
-        // X_kb <- W_kb X_kb
-        for (int t = wave; t < ncb; t += NWE) {
-            const bool colok = 16 * t + rr < ncol;
-            double* Xc = X + (16 * kb) * XW + 16 * t;
-            const d4b acc = mfma16_ab(L.W[kb], 16, Xc, XW, rr, kk, colok);
-            if (colok)
+        TLS(16 + 4 * kb);
+        if (NH == 2 && wave == 4 + kb) {  // x_kb <- W_kb x_kb (LDS row block, 8 valid columns)
+            double aw[4], bx[4];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) Xc[(kk + 4 * g) * XW + rr] = acc[g];
-        }
-        __syncthreads();
-        // X_ii -= L(ii,kb) X_kb for ii > kb, and the contributions of row block kb
-        for (int t = wave; t < (3 - kb) * ncb; t += NWE) {
-            const int ii = kb + 1 + t / ncb, cb = t % ncb;
-            const bool colok = 16 * cb + rr < ncol;
-            const d4b acc = mfma16_ab(L.L + (16 * ii) * BLD + 16 * kb, BLD, X + (16 * kb) * XW + 16 * cb, XW, rr, kk, colok);
-            if (colok)
+            for (int s4 = 0; s4 < 4; ++s4) {
+                aw[s4] = L.W[kb][rr * 16 + 4 * s4 + kk];
+                bx[s4] = rr < RC ? L.X[(16 * kb + 4 * s4 + kk) * XW + 2 * BB + rr] : 0.0;
+            }
+            d4b w = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int g = 0; g < 4; ++g) X[(16 * ii + kk + 4 * g) * XW + 16 * cb + rr] -= acc[g];
+            for (int s4 = 0; s4 < 4; ++s4) w = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[s4], bx[s4], w, 0, 0, 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (rr < RC)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) L.X[(16 * kb + kk + 4 * g) * XW + 2 * BB + rr] = w[g];
         }
-        if (!root) contrib_accumulate8(L.X, kb, cacc, has_r, wave, rr, kk);
+#pragma unroll
+        for (int j = 0; j < MAXOWN; ++j) {
+            const int cb = own_cb[j];
+            if (cb < 0) continue;
+            // operands first, then the three update chains interleaved (independent accumulators)
+            double aw[4], al[3][4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) aw[s4] = L.W[kb][rr * 16 + 4 * s4 + kk];
+#pragma unroll
+            for (int ii = kb + 1; ii < 4; ++ii)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) al[ii - kb - 1][s4] = -L.L[(16 * ii + rr) * BLD + 16 * kb + 4 * s4 + kk];
+            d4b w = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) w = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[s4], xt[j][kb][s4], w, 0, 0, 0);
+            xt[j][kb] = w;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                for (int ii = kb + 1; ii < 4; ++ii)
+                    xt[j][ii] = __builtin_amdgcn_mfma_f64_16x16x4f64(al[ii - kb - 1][s4], w[s4], xt[j][ii], 0, 0, 0);
+            if (16 * cb + rr < ncol)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) X[(16 * kb + kk + 4 * g) * XW + 16 * cb + rr] = w[g];
+            if (xl_on && roleA && cb < 4)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) st_pub(xlg + (16 * kb + kk + 4 * g) * BB + 16 * cb + rr, w[g]);
+        }
+        // second flag read (its value is tested after the contributions, when the first test failed)
+        unsigned fpan2 = 0, fxl2 = ~0u;
+        if (kb < 3 && tid == TPOLL) {
+            L.pre = fpan >= 4 * epoch + kb + 1 && (!(xl_on && roleB && kb + 1 >= 2) || fxl >= 4 * epoch + kb - 1);
+            fpan2 = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xl_on && roleB && kb + 1 >= 2)
+                fxl2 = __hip_atomic_load((gu32*)(xl_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         __syncthreads();
+        TLS(17 + 4 * kb);
+        have = kb < 3 && L.pre;
+        if (have) issue(kb + 1);
+        if (NH == 2 && wave > 4 + kb) {  // x_ii -= L(ii,kb) x_kb, ii = wave - 4
+            const int ii = wave - 4;
+            double al[4], bx[4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                al[s4] = -L.L[(16 * ii + rr) * BLD + 16 * kb + 4 * s4 + kk];
+                bx[s4] = rr < RC ? L.X[(16 * kb + 4 * s4 + kk) * XW + 2 * BB + rr] : 0.0;
+            }
+            d4b acc;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = rr < RC ? L.X[(16 * ii + kk + 4 * g) * XW + 2 * BB + rr] : 0.0;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bx[s4], acc, 0, 0, 0);
+            if (rr < RC)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + 2 * BB + rr] = acc[g];
+        }
+        if (fill_on && roleB && kb >= 2) fill_rows(kb - 2);
+        if (!root) {  // contributions of row block kb: operands of every tile first, then interleaved chains
+            double av[NCT8][4], bv[NCT8][4];
+#pragma unroll
+            for (int q = 0; q < NCT8; ++q) {
+                const int t = hm.tiles[q];
+                const ContribTile ct = contrib_tile(t < 0 ? 0 : t, has_r);
+                const bool on = t >= 0 && ct.valid;
+                const bool bok = on && (!ct.rhs || rr < RC);
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    const double* row = L.X + (16 * kb + 4 * s4 + kk) * XW;
+                    av[q][s4] = on ? row[ct.aoff + 16 * ct.ib + rr] : 0.0;
+                    bv[q][s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                for (int q = 0; q < NCT8; ++q)
+                    if (hm.tiles[q] >= 0)
+                        cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][s4], bv[q][s4], cacc[q], 0, 0, 0);
+        }
+        const bool late = kb < 3 && !have;
+        if (late && tid == TPOLL)
+            L.pre = fpan2 >= 4 * epoch + kb + 1 && (!(xl_on && roleB && kb + 1 >= 2) || fxl2 >= 4 * epoch + kb - 1);
+        if (xl_on && roleA) publish_flag(xl_f + i, 4 * epoch + kb);  // XL_kb stores (issued above) drained
+        else if (late) __syncthreads();
+        if (late && L.pre) {  // panel kb + 1 arrived during the contributions: no poll round trip
+            issue(kb + 1);
+            have = true;
+        }
+        if constexpr (STAMP) __syncthreads();
         TLS(3 + 2 * kb);
     }
+    __syncthreads();
     if (root) {
         double* Yl = L.yt;
         {
@@ -1394,8 +1697,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     }
 #pragma unroll
     for (int q = 0; q < NCT8; ++q) {
-        const int t = wave + NWE * q;
-        if (t >= NCONTRIB) continue;
+        const int t = hm.tiles[q];
+        if (t < 0) continue;
         const ContribTile ct = contrib_tile(t, has_r);
         if (!ct.valid || (ct.rhs && rr >= RC)) continue;
         double* dst = (t < 10 ? Bw.UL : t < 20 ? Bw.UR : t < 36 ? Bw.F : t < 40 ? Bw.rL : Bw.rR) +
@@ -1404,8 +1707,37 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         for (int g = 0; g < 4; ++g)
             st_pub(dst + (size_t)(16 * ct.ib + kk + 4 * g) * ct.ldd + 16 * ct.cb + rr, ct.sign * cacc[q][g]);
     }
-    publish_flag(elim_f + i, epoch);
+    publish_flag((roleA || NH == 1) ? elim_f + i : elimB_f + i, epoch);
     TLS(10);
+    if (roleA) {
+        TLS(11);
+        return;
+    }
+    if (NH == 2) {
+        // last row block of the fill, then F = -XR^T XL; the back-substitution needs all of XL
+        if (!wait_ge(xl_f + i, 4 * epoch + 3, &L.ok)) {
+            if (tid == 0) *flag = 1;
+            return;
+        }
+        for (int e = tid; e < 32 * BB; e += TPB_E) {
+            const int r = 32 + (e >> 6), c = e & 63;
+            L.X[r * XW + c] = ld_pub(xlg + r * BB + c);
+        }
+        __syncthreads();
+        if (fill_on) {
+            fill_rows(2);
+            fill_rows(3);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const ContribTile ct = contrib_tile(20 + wave + NWE * q, true);
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    st_pub(Bw.F + (size_t)i * BSZ + (size_t)(16 * ct.ib + kk + 4 * g) * BB + 16 * ct.cb + rr, -facc[q][g]);
+            }
+        }
+        publish_flag(fill_f + i, epoch);
+        TLS(11);
+    }
     // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
     trsm_lower64_t(L.L, L.rdiag, L.X, XW, XC);
     if (!wait_flags(back_f + (i - s_i), has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
@@ -1470,9 +1802,13 @@ template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
-    if (Bw.persist == 2) {
-        BPL(K_BCR_PERSIST, k_bcr_split<STAMP>, dim3(2 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw,
-            W.chol_flag, stamps);
+    if (Bw.persist >= 2) {
+        if (Bw.persist == 3)
+            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 2>), dim3(3 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
+                Bw, W.chol_flag, stamps);
+        else
+            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 1>), dim3(2 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
+                Bw, W.chol_flag, stamps);
         BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
         return hipSuccess;
     }
@@ -1505,9 +1841,13 @@ static hipError_t bcr_persist_attr() {
                                 (int)sizeof(PersistLds)));
         CKB(hipFuncSetAttribute((const void*)k_bcr_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(PersistLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_split<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        CKB(hipFuncSetAttribute((const void*)k_bcr_split<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(HLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_split<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        CKB(hipFuncSetAttribute((const void*)k_bcr_split<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(HLds)));
+        CKB(hipFuncSetAttribute((const void*)k_bcr_split<false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(HLds)));
+        CKB(hipFuncSetAttribute((const void*)k_bcr_split<true, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(HLds)));
         done = true;
     }
@@ -1519,7 +1859,10 @@ int bcr_persist_ok(int nblk) {
     int dev = 0, ncu = 0, per_cu = 0, per_cu2 = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false>, TPB_E, sizeof(HLds)) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 2>, TPB_E, sizeof(HLds)) == hipSuccess &&
+        per_cu2 >= 1 && 3 * nblk <= per_cu2 * ncu)
+        return 3;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 1>, TPB_E, sizeof(HLds)) == hipSuccess &&
         per_cu2 >= 1 && 2 * nblk <= per_cu2 * ncu)
         return 2;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist<false>, TPB_E, sizeof(PersistLds)) !=
@@ -1547,19 +1890,31 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
         static unsigned long long h[NSTAMP];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
-        if (Bw.persist == 2) {
+        if (Bw.persist >= 2) {
+            const int nr = Bw.persist;  // workgroups per block
             unsigned long long t0 = ~0ull;
-            for (int g = 0; g < 2 * Bw.nblk && g < 256; ++g) if (h[32 * g]) t0 = std::min(t0, h[32 * g]);
+            for (int g = 0; g < nr * Bw.nblk && g < 256; ++g) if (h[32 * g]) t0 = std::min(t0, h[32 * g]);
             auto us = [&](unsigned long long t) { return t ? (double)(t - t0) * 0.01 : -1.0; };
-            for (int g = 0; g < 2 * Bw.nblk && g < 256; ++g) {
+            for (int g = 0; g < nr * Bw.nblk && g < 256; ++g) {
                 const unsigned long long* q = h + 32 * g;
-                if (g % 2 == 0)
-                    fprintf(stderr, "bcr F%3d start %7.2f loaded %7.2f panels %7.2f %7.2f %7.2f %7.2f\n", g / 2, us(q[0]),
+                if (g % nr == 0) {
+                    fprintf(stderr, "bcr F%3d start %7.2f loaded %7.2f panels %7.2f %7.2f %7.2f %7.2f\n", g / nr, us(q[0]),
                             us(q[1]), us(q[2]), us(q[3]), us(q[4]), us(q[5]));
-                else
-                    fprintf(stderr, "bcr H%3d start %7.2f loaded %7.2f panel got/done %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f contrib %7.2f back-wait %7.2f done %7.2f\n",
-                            g / 2, us(q[0]), us(q[1]), us(q[2]), us(q[3]), us(q[4]), us(q[5]), us(q[6]), us(q[7]), us(q[8]),
-                            us(q[9]), us(q[10]), us(q[12]), us(q[14]));
+                    fprintf(stderr, "        chain start | chain end | published:");
+                    for (int kb = 0; kb < 4; ++kb)
+                        fprintf(stderr, "  %7.2f %7.2f %7.2f", us(q[17 + 3 * kb]), us(q[16 + 3 * kb]), us(q[2 + kb]));
+                    fprintf(stderr, "\n");
+                } else
+                {
+                    fprintf(stderr, "bcr H%c%3d start %7.2f loaded %7.2f panel got/done %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f contrib %7.2f fill/xl %7.2f back-wait %7.2f done %7.2f\n",
+                            nr == 2 ? ' ' : (g % nr == 1 ? 'A' : 'B'), g / nr, us(q[0]), us(q[1]), us(q[2]), us(q[3]), us(q[4]), us(q[5]), us(q[6]), us(q[7]), us(q[8]),
+                            us(q[9]), us(q[10]), us(q[11]), us(q[12]), us(q[14]));
+                    fprintf(stderr, "        panel got | loaded | x-updated | contrib:");
+                    for (int kb = 0; kb < 4; ++kb)
+                        fprintf(stderr, "  %7.2f %7.2f %7.2f %7.2f", us(q[2 + 2 * kb]), us(q[16 + 4 * kb]), us(q[17 + 4 * kb]),
+                                us(q[3 + 2 * kb]));
+                    fprintf(stderr, "\n");
+                }
             }
             return hipSuccess;
         }

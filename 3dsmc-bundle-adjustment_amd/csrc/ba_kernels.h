@@ -19,7 +19,14 @@ static constexpr int CHUNK_PTS = 32;   // points per Schur chunk (K = 3 * CHUNK_
 static constexpr int CHUNK_OBS = 256;
 static constexpr int SUBSEG_OBS = 1024;  // observations per camera-side sub-segment (one workgroup)
 static constexpr int BS_PTS = 64;     // points per back-substitution chunk
-static constexpr int BS_OBS = 512;    // observations per back-substitution chunk (a single point may exceed)  // observations per chunk (one per thread)
+static constexpr int BS_OBS = 512;    // observations per back-substitution chunk (a single point may exceed)
+// k_point_prep: PP_LANES lanes per active point (one aligned lane group), each taking every
+// PP_LANES-th observation of the point; the group sums by xor-shuffles (fixed order)
+static constexpr int PP_LANES_MAX = 4;
+static constexpr int PP_TPB = 256;
+int pp_lanes();  // lanes per point of k_point_prep (MIBA_PP_LANES: 1, 2 or 4)
+inline int pp_blocks(int n_ap, int lanes) { return (n_ap * lanes + PP_TPB - 1) / PP_TPB; }
+inline int pp_blocks(int n_ap) { return pp_blocks(n_ap, pp_lanes()); }
 
 // partial-sum slots (each slot holds part_stride doubles, one per producing block)
 enum {
@@ -106,12 +113,15 @@ static constexpr int BCR_CAMS = 10;
 // plus one global slot: bk = [b_k (4) | S_kk lower (10)].
 struct BcrWork {
     double *Cf, *X, *UL, *UR, *F, *rL, *rR, *Dacc, *Racc, *Y, *Bp, *rd, *bk;
-    // persistent path: flags[0] = call epoch, flags[16 + i] = block i eliminated,
-    // flags[16 + nblk + i] = block i back-substituted (each holds the epoch that set it)
+    // persistent path: flags[0] = call epoch, flags[16 + i] = block i eliminated (helper A's part
+    // when split 3-way), flags[16 + nblk + i] = block i back-substituted, [16 + 2 nblk + i] panels
+    // published, [16 + 3 nblk + i] helper B's part, [16 + 4 nblk + i] fill F, [16 + 5 nblk + i] XL
+    // (each holds the epoch that set it; panels 4 * epoch + panel)
     unsigned* flags;
     int nblk, levels;
-    int persist;  // 2 = factor + helper workgroups per block (k_bcr_split), 1 = one resident workgroup per
-                  // block (k_bcr_persist), 0 = one launch per level
+    int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
+                  // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
+                  // 0 = one launch per level
 };
 // [XL | XR | x] row stride (136 columns; padding to 144 for conflict-free operand rows measured no gain)
 static constexpr int BCR_XW = 136;
@@ -170,12 +180,12 @@ struct DevWork {
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
     K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
-    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_COUNT
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
     "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
-    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist"};
+    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {

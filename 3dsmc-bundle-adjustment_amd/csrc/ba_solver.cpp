@@ -538,7 +538,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     HIPCHECK(ctx, upload(ctx, B_RPTR, rptr.data(), nb + 1));
     HIPCHECK(ctx, upload(ctx, B_ROWS, rows.data(), rows.size()));
     const int n_seg = (int)seg_cam.size();
-    const int nblk_pt = (n_ap + 255) / 256;
+    const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
     const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, 1});
     HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
     // landmark sharding: envelope tile list of S, pack buffers, exchange scalars
@@ -613,7 +613,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     }
     if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
     if (P.solver == 2) {
-        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 3 * bcr_nblk);
+        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 6 * bcr_nblk);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
         // upper tiles of UL/UR are never written and must read as zero
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
@@ -640,7 +640,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         Bw.persist = bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
-            else if (!std::strcmp(e, "persist") && Bw.persist == 2) Bw.persist = 1;  // "split" or unset: default
+            else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
+            else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;  // "split3" or unset: default
         }
     }
     DevWork& W = ctx->W;

@@ -166,27 +166,31 @@ def test_comm_init_rejects_bad_rank():
 
 @pytest.mark.parametrize("n_cams", [23, 64, 200, 333])
 def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
-    """The persistent BCR kernel (one resident workgroup per 10-camera block, flag hand-offs,
-    Schur contributions accumulated inside the factorization) against the per-level launches and
-    the oracle. The two GPU paths sum the contributions in different orders and the Schur flush into
-    S uses f64 atomics, so they agree to rounding: tolerances off, both run exactly 6 iterations."""
+    """The persistent BCR kernels (one resident workgroup per 10-camera block; factor + one helper;
+    factor + two helpers, the default where 3 workgroups per block fit) against the per-level
+    launches and the oracle. The GPU paths sum the contributions in different orders and the Schur
+    flush into S uses f64 atomics, so they agree to rounding: tolerances off, all run exactly 6
+    iterations."""
     from miba.solver import Solver
     p = synthetic.make_problem(n_cams, 40 * n_cams, obs_per_point=(4, 9), seed=n_cams)
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
     res = {}
-    for mode in ("launch", "persist"):
+    for mode in ("launch", "persist", "split", "split3"):
         monkeypatch.setenv("MIBA_BCR", mode)
         q = p.copy()
         with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
             res[mode] = (s.solve(q), q)
-    (sa, qa), (sb, qb) = res["launch"], res["persist"]
-    assert sa["linear_solver"] == sb["linear_solver"] == LS["bcr"]
-    assert sa["num_iterations"] == sb["num_iterations"] == 6
-    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sa["final_cost"]
-    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
-    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
-    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
-    assert abs(sb["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    sa, qa = res["launch"]
+    assert sa["linear_solver"] == LS["bcr"]
+    for mode in ("persist", "split", "split3"):
+        sb, qb = res[mode]
+        assert sb["linear_solver"] == LS["bcr"], mode
+        assert sa["num_iterations"] == sb["num_iterations"] == 6, mode
+        assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sa["final_cost"], mode
+        np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8, err_msg=mode)
+        np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7, err_msg=mode)
+        assert abs(sb["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], mode
 
 
 @pytest.mark.parametrize("config,iters", [("C4", 3), ("C5", 2)])
