@@ -11,8 +11,8 @@ namespace miba {
 static constexpr int CAMDATA = 51;
 // per camera-segment intrinsics partial: Ukk packed (10) | gk (4) | cost (1)
 static constexpr int SEGINTR = 15;
-// per active point Schur record: G = chol(V~)^-1 packed lower (6) | e~ (3) | K~ 4x3 (12)
-static constexpr int PDATA = 21;
+// per active point Schur record: G = chol(V~)^-1 packed lower (6) | e~ (3) | K~ 4x3 (12) | LM diagonal D~ (3)
+static constexpr int PDATA = 24;
 // tiled Schur reduction geometry
 static constexpr int TILE_WIN = 12;    // cameras per tile window
 static constexpr int CHUNK_PTS = 32;   // points per Schur chunk (K = 3 * CHUNK_PTS of the MFMA product)

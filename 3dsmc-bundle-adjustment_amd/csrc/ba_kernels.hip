@@ -12,8 +12,8 @@
 //   k_obs_pairs     Schur scatter  S -= W V^-1 W^T, rhs -= W V^-1 e (global f64 atomics)
 //   k_chol          envelope-blocked Cholesky of S + forward/back solve (1 workgroup,
 //                   v_mfma_f64_16x16x4_f64 for the trailing 16x16 tile updates)
-//   k_update_cams   delta = -s*y, Sophus T*exp(delta), prior-block terms
-//   k_backsub_chunk point back-substitution, model cost change -(J d)^T(f + J d/2),
+//   k_update_cams   delta = -s*y, Sophus T*exp(delta), camera/intrinsics model-change terms
+//   k_backsub_chunk point back-substitution, point model-change terms 0.5(e~^T y + y^T D~ y),
 //                   candidate cost at x + delta
 //   k_final         deterministic reduction of the per-block partials
 //
@@ -286,7 +286,7 @@ __device__ __forceinline__ void w_tilde(const double jc[18], const double jp[9],
 }
 // mode 0: column norms only (iteration 0, before the Jacobi scale exists)
 // mode 1: full Schur preparation.
-// pdata[ap*PDATA]: Vinv packed (6: 00 01 02 11 12 22), e (3), Kt (12, [m][i])
+// pdata[ap*PDATA]: G = chol(V~)^-1 packed (6), e~ (3), K~ (12, [m][i]), D~ (3)
 // PP_LANES lanes per point: lane q of the group evaluates observations q, q + PP_LANES, ... of
 // the point; the group's xor-shuffle sums leave identical totals in every lane, each lane then
 // runs the (redundant) 3x3 factorisation and stores its share of the point's record.
@@ -362,11 +362,14 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
             // scaled, damped V  (Ceres: lm_diagonal = sqrt(clamp(diag(JtJ~)) / radius))
             double v00 = s0 * V[0] * s0, v01 = s0 * V[1] * s1, v02 = s0 * V[2] * s2;
             double v11 = s1 * V[3] * s1, v12 = s1 * V[4] * s2, v22 = s2 * V[5] * s2;
-            v00 += fmin(fmax(v00, c.min_diag), c.max_diag) / radius;
-            v11 += fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
-            v22 += fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
-            // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
             double rec[PDATA];
+            rec[21] = fmin(fmax(v00, c.min_diag), c.max_diag) / radius;  // D~ (model cost change, k_backsub_chunk)
+            rec[22] = fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
+            rec[23] = fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
+            v00 += rec[21];
+            v11 += rec[22];
+            v22 += rec[23];
+            // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
 #pragma unroll
             for (int i = 0; i < 6; ++i) rec[i] = 0.0;  // g00 g10 g11 g20 g21 g22
             const bool pd = v00 > 0.0;
@@ -1348,23 +1351,36 @@ __global__ __launch_bounds__(TPB) void k_chol_band(const LmState* __restrict__ s
 }
 
 // ---------------------------------------------------------------- update
-// delta = -s * y over cameras and intrinsics; candidate poses; prior-block model
-// change and candidate prior cost. part[PART_UPD_* * stride + block]
+// delta = -s * y over cameras and intrinsics; candidate poses; the camera / intrinsics terms of the
+// model cost change and the candidate prior cost. part[PART_UPD_* * stride + block]
+// Model cost change (Ceres ComputeTrustRegionStep: -(J d)^T (f + J d / 2)) from the normal equations:
+// in scaled coordinates the step z = -y solves (A~ + D~) z = -g~ exactly (A~ = J~^T J~, g~ = J~^T f,
+// D~ the LM diagonal; the Schur solve is exact), so -(J~ z)^T (f + J~ z / 2) = 0.5 (g~^T y + y^T D~ y):
+// a sum of per-parameter terms (cameras and intrinsics here, points in k_backsub_chunk) that needs no
+// second Jacobian evaluation per observation. g~ and D~ are the values k_env_assemble / k_point_prep
+// put into the system, element for element.
 __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restrict__ st, const double* __restrict__ scale,
+                              const double* __restrict__ camdata, const double* __restrict__ lin,
                               const double* __restrict__ y, double* __restrict__ delta, double* __restrict__ part) {
     __shared__ double lds[4 * 4];
     __shared__ double out[4];
     if (st->done) return;
     const int cur = st->cur;
+    const double radius = st->radius;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
     if (t < P.nac) {
         const int cam = P.ac_cam[t];
+        const double* cd = camdata + (size_t)t * CAMDATA;
         double d[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            d[k] = -y[6 * t + k] * scale[6 * t + k];
+            const double sc = scale[6 * t + k], yk = y[6 * t + k];
+            d[k] = -yk * sc;
             delta[6 * t + k] = d[k];
+            const double u = sc * cd[k * 6 - (k * (k - 1)) / 2] * sc;  // diag of s U s (k_env_assemble)
+            const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+            acc[1] += 0.5 * ((sc * cd[45 + k]) * yk + dd * yk * yk);
         }
         const double* x = P.cams[cur] + 7 * cam;
         double* xn = P.cams[cur ^ 1] + 7 * cam;
@@ -1381,15 +1397,16 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
         const double* K = P.K[cur];
         double* Kn = P.K[cur ^ 1];
         for (int m = 0; m < 4; ++m) {
-            const double dk = -y[P.kb + m] * scale[P.off_k + m];
+            const double sk = scale[P.off_k + m], ym = y[P.kb + m];
+            const double dk = -ym * sk;
             delta[P.kb + m] = dk;
             const double kn = K[m] + dk;
             Kn[m] = kn;
             const double df = K[m] - kn;
             acc[0] += df * df;
-            const double fk = c.sw_k * (P.prior[m] - K[m]);
-            const double jd = -c.sw_k * dk;
-            acc[1] += -jd * (fk + jd / 2.0);
+            const double u = sk * lin[2 + 4 * m - (m * (m - 1)) / 2] * sk;  // Ukk incl. the prior block
+            const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+            acc[1] += 0.5 * ((sk * lin[12 + m]) * ym + dd * ym * ym);
             const double fn = c.sw_k * (P.prior[m] - kn);
             acc[2] += 0.5 * fn * fn;
             acc[3] += kn * kn;
@@ -1408,7 +1425,9 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
 // workgroup; observation loads coalesced, one observation per thread):
 //   phase 1 (obs):   c_o = s_p (Jp^T (Jc (s_c y_c)))  -> LDS slot of the observation
 //   phase 2 (point): y_p = V~^-1 (e~ - Kt^T y_k - sum_o c_o) (fixed order), delta_p = -s_p y_p
-//   phase 3 (obs):   model cost change -(J delta)^T (f + J delta / 2), candidate cost at x + delta
+//   phase 3 (obs):   candidate cost at x + delta
+// The points' share of the model cost change, 0.5 (e~^T y_p + y_p^T D~_p y_p), is summed in phase 2
+// (k_update_cams states the identity).
 // A chunk holding a single point with more than BS_OBS observations sums c_o by block reduction.
 __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                        const double* __restrict__ scale,
@@ -1491,6 +1510,7 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const double yp = Vf[i * 3 + 0] * t[0] + Vf[i * 3 + 1] * t[1] + Vf[i * 3 + 2] * t[2];
+            acc[1] += 0.5 * (pd[6 + i] * yp + pd[21 + i] * yp * yp);
             const double dp = -sp[i] * yp;
             const double xn = X[i] + dp;
             Xn[i] = xn;
@@ -1502,30 +1522,14 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
     }
     __syncthreads();
     // ---- phase 3
-    const double* dk = delta + P.kb;
+    (void)delta;
     for (int o = ob + tid; o < oe; o += TPB) {
-        const int ac = P.po_ac[o];
         const int cam = P.po_cam[o];
         const int pl = P.po_ap[o] - apb;
         const double2 uv = P.po_uv[o];
         const double dep = P.po_depth[o];
         const double* X = P.pts[cur] + 3 * P.po_pt[o];
-        const double dp[3] = {dpl[pl][0], dpl[pl][1], dpl[pl][2]};
-        ObsEval ev;
-        double jc[18], jp[9], jk[8];
-        lin_obs(c, P.cams[cur] + 7 * cam, X, K, uv.x, uv.y, dep, ev, jc, jp, jk);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            double jd = jp[r * 3 + 0] * dp[0] + jp[r * 3 + 1] * dp[1] + jp[r * 3 + 2] * dp[2];
-            if (ac >= 0) {
-                const double* dc = delta + 6 * ac;
-#pragma unroll
-                for (int d = 0; d < 6; ++d) jd += jc[r * 6 + d] * dc[d];
-            }
-            if (r < 2) jd += jk[r * 4 + 0] * dk[0] + jk[r * 4 + 1] * dk[1] + jk[r * 4 + 2] * dk[2] + jk[r * 4 + 3] * dk[3];
-            acc[1] += -jd * (ev.f[r] + jd / 2.0);
-        }
-        const double xn[3] = {X[0] + dp[0], X[1] + dp[1], X[2] + dp[2]};
+        const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
         ObsEval en;
         eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, uv.x, uv.y, dep, en);
         if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
@@ -2095,7 +2099,8 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
         ndummy = e ? atoi(e) : 0;
     }
     for (int k = 0; k < ndummy; ++k) PL(K_DUMMY, k_dummy, dim3(1), dim3(64), 0, s, W.st);
-    PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.rhs, W.delta, W.part);
+    PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.camdata, W.lin, W.rhs, W.delta,
+       W.part);
     const int nb_bs = P.n_bs_chunks;
     if (P.n_ap > 0)
         PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,

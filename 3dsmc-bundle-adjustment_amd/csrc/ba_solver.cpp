@@ -737,7 +737,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         }
         kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
         kb[K_BACKSUB_EVAL] = A * 2 * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read twice
-        kf[K_BACKSUB_EVAL] = A * 700;
+        kf[K_BACKSUB_EVAL] = A * 450;
         kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
     }
     return BA_OK;
