@@ -135,11 +135,34 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
 #pragma unroll
     for (int i = 0; i < 66; ++i) acc[i] = 0.0;
     const int o0 = P.seg_ptr[s], o1 = P.seg_ptr[s + 1];
-    for (int o = o0 + threadIdx.x; o < o1; o += TPB) {
-        const double2 uv = P.co_uv[o];
+    // software pipeline: point index two observations ahead, point / pixel / depth one ahead
+    const int oa = o0 + threadIdx.x;
+    int pt_n = oa < o1 ? P.co_pt[oa] : 0;
+    const int pt_nn = oa + TPB < o1 ? P.co_pt[oa + TPB] : 0;
+    double X_n[3] = {0.0, 0.0, 0.0}, dep_n = 0.0;
+    double2 uv_n = double2{0.0, 0.0};
+    if (oa < o1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) X_n[k] = pts[3 * pt_n + k];
+        uv_n = P.co_uv[oa];
+        dep_n = P.co_depth[oa];
+    }
+    pt_n = pt_nn;
+    for (int o = oa; o < o1; o += TPB) {
+        const double X[3] = {X_n[0], X_n[1], X_n[2]};
+        const double2 uv = uv_n;
+        const double dep = dep_n;
+        const int on = o + TPB;
+        if (on < o1) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) X_n[k] = pts[3 * pt_n + k];
+            uv_n = P.co_uv[on];
+            dep_n = P.co_depth[on];
+            pt_n = on + TPB < o1 ? P.co_pt[on + TPB] : 0;
+        }
         ObsEval e;
         double jc[18], jp[9], jk[8];
-        lin_obs(c, pose, pts + 3 * P.co_pt[o], K, uv.x, uv.y, P.co_depth[o], e, jc, jp, jk);
+        lin_obs(c, pose, X, K, uv.x, uv.y, dep, e, jc, jp, jk);
         (void)jp;
         if (ac >= 0) {
             int q = 0;
@@ -323,11 +346,37 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
 #pragma unroll
         for (int i = 0; i < 21; ++i) acc[i] = 0.0;
         const int o1 = P.pt_ptr[ap + 1];
-        for (int o = P.pt_ptr[ap] + q; o < o1; o += PP_LANES) {
-            const double2 uv = P.po_uv[o];
+        // software pipeline: camera index two observations ahead, pose / pixel / depth one ahead
+        const double* cams = P.cams[cur];
+        const int o0 = P.pt_ptr[ap] + q;
+        int cam_n = o0 < o1 ? P.po_cam[o0] : 0;
+        const int cam_nn = o0 + PP_LANES < o1 ? P.po_cam[o0 + PP_LANES] : 0;
+        double pose_n[7], dep_n = 0.0;
+        double2 uv_n = double2{0.0, 0.0};
+        if (o0 < o1) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) pose_n[k] = cams[7 * cam_n + k];
+            uv_n = P.po_uv[o0];
+            dep_n = P.po_depth[o0];
+        }
+        cam_n = cam_nn;
+        for (int o = o0; o < o1; o += PP_LANES) {
+            double pose[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) pose[k] = pose_n[k];
+            const double2 uv = uv_n;
+            const double dep = dep_n;
+            const int on = o + PP_LANES;
+            if (on < o1) {
+#pragma unroll
+                for (int k = 0; k < 7; ++k) pose_n[k] = cams[7 * cam_n + k];
+                uv_n = P.po_uv[on];
+                dep_n = P.po_depth[on];
+                cam_n = on + PP_LANES < o1 ? P.po_cam[on + PP_LANES] : 0;
+            }
             ObsEval ev;
             double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * P.po_cam[o], X, K, uv.x, uv.y, P.po_depth[o], ev, jc, jp, jk);
+            lin_obs(c, pose, X, K, uv.x, uv.y, dep, ev, jc, jp, jk);
             (void)jc;
             acc[0] += jp[0] * jp[0] + jp[3] * jp[3] + jp[6] * jp[6];
             acc[1] += jp[0] * jp[1] + jp[3] * jp[4] + jp[6] * jp[7];
