@@ -1219,8 +1219,10 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const int nblk = Bw.nblk;
     const int i = blockIdx.x / (NH + 1);
     const int role = blockIdx.x % (NH + 1);  // 0 factor, 1 helper (A), 2 helper B
-    const bool root = i == 0;
-    const int mi = root ? Bw.levels : __builtin_ctz(i);
+    // elimination tree on virtual indices v = i + voff (balanced: the root is the middle block, depth
+    // floor(log2 nblk) + 1 instead of ceil(log2 nblk) + 1 with block 0 as the root)
+    const bool root = i == Bw.vroot;
+    const int mi = root ? Bw.vlevels : __builtin_ctz(i + Bw.voff);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
     const size_t ld = P.npad;
     const int nd = 6 * P.nac;
@@ -1238,6 +1240,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     constexpr int NQ = BSZ / TPB_E;
     const int s_i = 1 << mi;
     const bool has_r = !root && i + s_i < nblk;
+    const bool has_l = !root && i - s_i >= 0;
     if (role == 0) {
         // ================= F: D_i, pivot side of the factorization
         FLds& L = *reinterpret_cast<FLds*>(smem);
@@ -1401,7 +1404,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             for (int q = 0; q < NQ; ++q) {
                 const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
                 if (NH == 1 || roleA) {
-                    const bool okl = r < G_DOF && b0 + r < nd && c < G_DOF;
+                    const bool okl = i >= 1 && r < G_DOF && b0 + r < nd && c < G_DOF;
                     L.X[r * XW + c] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
                 }
                 if (NH == 1 || roleB) {
@@ -1428,7 +1431,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             return;
         }
         if (last && NH == 2) {
-            const unsigned* ff = roleA ? fill_f + a : (has_r ? fill_f + b : nullptr);
+            const unsigned* ff = roleA ? (a >= 0 ? fill_f + a : nullptr) : (has_r ? fill_f + b : nullptr);
             if (!wait_flags(ff, nullptr, epoch, &L.ok)) {
                 if (tid == 0) *flag = 1;
                 return;
@@ -1439,7 +1442,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int e = tid + TPB_E * q;
-                fl[q] = (NH == 1 || roleA) ? ld_pub(Bw.F + (size_t)a * BSZ + e) : 0.0;
+                fl[q] = (NH == 1 || roleA) && a >= 0 ? ld_pub(Bw.F + (size_t)a * BSZ + e) : 0.0;
                 fr[q] = (NH == 1 || roleB) && has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
             }
 #pragma unroll
@@ -1682,7 +1685,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
         __syncthreads();
         trsm_t_lanes(L.L, L.rdiag, Yl);
-        st_pub(Bw.Y + tid, Yl[tid]);
+        st_pub(Bw.Y + (size_t)i * RSZ + tid, Yl[tid]);
         if (tid < 4) Bw.bk[tid] = rhs[P.kb + tid];
         if (tid >= 4 && tid < 14) {
             int q = tid - 4, mm = 0;
@@ -1690,8 +1693,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             Bw.bk[tid] = S[(size_t)(P.kb + mm) * ld + P.kb + q];
         }
         __syncthreads();
-        border_partial(L.Bl, Yl, L.red, 0, Bw.Bp);
-        publish_flag(back_f, epoch);
+        border_partial(L.Bl, Yl, L.red, i, Bw.Bp);
+        publish_flag(back_f + i, epoch);
         TLS(14);
         return;
     }
@@ -1740,12 +1743,12 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     }
     // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
     trsm_lower64_t(L.L, L.rdiag, L.X, XW, XC);
-    if (!wait_flags(back_f + (i - s_i), has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
+    if (!wait_flags(has_l ? back_f + (i - s_i) : nullptr, has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
         if (tid == 0) *flag = 1;
         return;
     }
     TLS(12);
-    L.yl[tid] = ld_pub(Bw.Y + (size_t)(i - s_i) * RSZ + tid);
+    L.yl[tid] = has_l ? ld_pub(Bw.Y + (size_t)(i - s_i) * RSZ + tid) : 0.0;
     L.yr[tid] = has_r ? ld_pub(Bw.Y + (size_t)(i + s_i) * RSZ + tid) : 0.0;
     L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
     __syncthreads();

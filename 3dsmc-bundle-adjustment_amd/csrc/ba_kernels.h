@@ -119,6 +119,7 @@ struct BcrWork {
     // (each holds the epoch that set it; panels 4 * epoch + panel)
     unsigned* flags;
     int nblk, levels;
+    int voff, vroot, vlevels;  // k_bcr_split: balanced tree on v = i + voff, root block vroot, depth vlevels + 1
     int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level

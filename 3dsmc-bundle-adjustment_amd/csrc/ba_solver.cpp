@@ -622,6 +622,12 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         Bw.nblk = bcr_nblk;
         Bw.levels = 0;
         while ((1 << Bw.levels) < bcr_nblk) ++Bw.levels;
+        // balanced elimination tree for the split kernels: K = floor(log2 nblk), v = i + 2^K - nblk/2,
+        // so [voff, voff + nblk) holds one multiple of 2^K (the root, block nblk/2) and none of 2^(K+1)
+        Bw.vlevels = 0;
+        while ((2 << Bw.vlevels) <= bcr_nblk) ++Bw.vlevels;
+        Bw.voff = (1 << Bw.vlevels) - bcr_nblk / 2;
+        Bw.vroot = bcr_nblk / 2;
         const size_t b64 = (size_t)64 * 64 * bcr_nblk, b8 = (size_t)64 * 8 * bcr_nblk;
         Bw.Cf = base;
         Bw.X = Bw.Cf + b64;

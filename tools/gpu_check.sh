@@ -10,3 +10,4 @@ d=json.loads(open('gpurun_out/bench_c4.log').read().strip().splitlines()[-1])
 print(d['value'], d['ms_per_step']); print(d['kernel_ms_per_step'])
 PY
 MIBA_BCR_STAMPS=1 timeout -k 10 120 python tools/kernel_stamps.py C4 1 > gpurun_out/stamps_c4.log 2>&1 || echo STAMPS_FAIL
+bash tools/ab_run.sh
