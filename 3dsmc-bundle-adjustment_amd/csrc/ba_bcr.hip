@@ -779,11 +779,19 @@ __global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ 
 // 4x4 system C' y_k = b' (C' = S_kk - B^T V, b' = b_k - B^T u); workgroup i then writes
 // y_a = u - V y_k for the rows of block i into rhs (workgroup 0 also y_k).
 static constexpr int TPB_BD = 64;
+// Fused camera update (was k_update_cams): lanes < BCR_CAMS of workgroup i apply the step of the block's
+// cameras from the y rows it just produced, workgroup 0 also the intrinsics; one partial per workgroup
+// of the step scalars for k_final.
 __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict__ st, DevProblem P,
-                                                       double* __restrict__ rhs, BcrWork Bw, int* __restrict__ flag) {
+                                                       double* __restrict__ rhs, BcrWork Bw, int* __restrict__ flag,
+                                                       BaConsts c, const double* __restrict__ scale,
+                                                       const double* __restrict__ camdata,
+                                                       const double* __restrict__ lin, double* __restrict__ delta,
+                                                       double* __restrict__ part) {
     if (st->done) return;
     __shared__ double red[20];
     __shared__ double yk[4];
+    __shared__ double ybl[G_DOF];
     const int tid = threadIdx.x;
     if (tid < 20) {
         double acc = 0.0;
@@ -833,10 +841,31 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
     const int b0 = i * G_DOF, nd = 6 * P.nac;
     if (tid < G_DOF && b0 + tid < nd) {
         const double* y = Bw.Y + (size_t)i * RSZ + tid * RC;
-        rhs[b0 + tid] = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
+        const double ya = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
+        rhs[b0 + tid] = ya;
+        ybl[tid] = ya;
     }
     if (i == 0 && tid < 4) rhs[P.kb + tid] = yk[tid];
     if (i == 0 && tid == 0) Bw.flags[0] += 1;  // next call's epoch (k_bcr_persist)
+    __syncthreads();
+    const int cur = st->cur;
+    const double radius = st->radius;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
+    const int ac = i * BCR_CAMS + tid;
+    if (tid < BCR_CAMS && ac < P.nac)
+        update_camera(P, c, cur, radius, scale, camdata, ac, ybl + 6 * tid, delta, acc);
+    else if (i == 0 && tid == BCR_CAMS)
+        update_intrinsics(P, c, cur, radius, scale, lin, yk, delta, acc);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+    if (tid == 0) {
+        part[PART_UPD_SN2 * P.part_stride + i] = acc[0];
+        part[PART_UPD_MCC * P.part_stride + i] = acc[1];
+        part[PART_UPD_COST * P.part_stride + i] = acc[2];
+        part[PART_UPD_XN2 * P.part_stride + i] = acc[3];
+    }
 }
 
 // ---- persistent path: one resident workgroup per block for the whole solve -------------------
@@ -1802,7 +1831,7 @@ static inline int n_elim(int nblk, int m) {
     } while (0)
 
 template <bool STAMP>
-static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s,
+static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
     if (Bw.persist >= 2) {
@@ -1812,13 +1841,15 @@ static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& B
         else
             BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 1>), dim3(2 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
                 Bw, W.chol_flag, stamps);
-        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
+        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag, c, W.scale,
+            W.camdata, W.lin, W.delta, W.part);
         return hipSuccess;
     }
     if (Bw.persist) {
         BPL(K_BCR_PERSIST, k_bcr_persist<STAMP>, dim3(nblk), dim3(TPB_E), sizeof(PersistLds), s, W.st, P, W.S, W.rhs,
             Bw, W.chol_flag, stamps);
-        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
+        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag, c, W.scale,
+            W.camdata, W.lin, W.delta, W.part);
         return hipSuccess;
     }
     for (int m = 0; m < Bw.levels; ++m) {
@@ -1833,7 +1864,8 @@ static hipError_t launch_bcr_t(const DevProblem& P, DevWork& W, const BcrWork& B
     for (int m = Bw.levels - 1; m >= 0; --m)
         BPL(K_BCR_BACK, k_bcr_back<STAMP>, dim3(n_elim(nblk, m)), dim3(TPB_C), sizeof(BackLds), s, W.st, P, W.S, Bw, m,
             stamps);
-    BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag);
+    BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag, c, W.scale,
+            W.camdata, W.lin, W.delta, W.part);
     return hipSuccess;
 }
 
@@ -1874,7 +1906,7 @@ int bcr_persist_ok(int nblk) {
     return per_cu >= 1 && nblk <= per_cu * ncu ? 1 : 0;
 }
 
-hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf) {
+hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf) {
     static bool attr = false;
     static unsigned long long* stamps = nullptr;
     if (!attr) {
@@ -1889,7 +1921,7 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
     }
     if (stamps) {
         CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * NSTAMP, s));
-        CKB(launch_bcr_t<true>(P, W, Bw, s, stamps, nullptr));
+        CKB(launch_bcr_t<true>(P, c, W, Bw, s, stamps, nullptr));
         static unsigned long long h[NSTAMP];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
@@ -1950,7 +1982,7 @@ hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStr
                     b[0] ? b[2] - b[1] : 0ull, b[0] ? b[3] - b[2] : 0ull);
         }
     } else {
-        CKB(launch_bcr_t<false>(P, W, Bw, s, nullptr, pf));
+        CKB(launch_bcr_t<false>(P, c, W, Bw, s, nullptr, pf));
     }
     return hipSuccess;
 }

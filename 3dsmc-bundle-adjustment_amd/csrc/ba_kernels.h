@@ -135,6 +135,58 @@ struct LmState {
     double msg_a, msg_b;
     int iter, n_succ, n_unsucc, n_invalid, step_ok, cur, need_lin, done, termination, msg;
 };
+// Camera / intrinsics step application (k_update_cams, or fused into k_bcr_border): delta = -s*y,
+// Sophus T*exp(delta) into the candidate slot, and the block's terms of the step scalars
+// acc = {|step|^2, model cost change 0.5 (g~ y + D~ y^2), candidate prior cost, |x_cand|^2}.
+__device__ __forceinline__ void update_camera(const DevProblem& P, const BaConsts& c, int cur, double radius,
+                                              const double* __restrict__ scale, const double* __restrict__ camdata,
+                                              int t, const double* yv, double* __restrict__ delta, double acc[4]) {
+    const int cam = P.ac_cam[t];
+    const double* cd = camdata + (size_t)t * CAMDATA;
+    double d[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const double sc = scale[6 * t + k], yk = yv[k];
+        d[k] = -yk * sc;
+        delta[6 * t + k] = d[k];
+        const double u = sc * cd[k * 6 - (k * (k - 1)) / 2] * sc;  // diag of s U s (k_env_assemble)
+        const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+        acc[1] += 0.5 * ((sc * cd[45 + k]) * yk + dd * yk * yk);
+    }
+    const double* x = P.cams[cur] + 7 * cam;
+    double* xn = P.cams[cur ^ 1] + 7 * cam;
+    double tp[7];
+    se3_plus(x, d, tp);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+        xn[j] = tp[j];
+        const double df = x[j] - tp[j];
+        acc[0] += df * df;
+        acc[3] += tp[j] * tp[j];
+    }
+}
+__device__ __forceinline__ void update_intrinsics(const DevProblem& P, const BaConsts& c, int cur, double radius,
+                                                  const double* __restrict__ scale, const double* __restrict__ lin,
+                                                  const double* yk4, double* __restrict__ delta, double acc[4]) {
+    const double* K = P.K[cur];
+    double* Kn = P.K[cur ^ 1];
+    for (int m = 0; m < 4; ++m) {
+        const double sk = scale[P.off_k + m], ym = yk4[m];
+        const double dk = -ym * sk;
+        delta[P.kb + m] = dk;
+        const double kn = K[m] + dk;
+        Kn[m] = kn;
+        const double df = K[m] - kn;
+        acc[0] += df * df;
+        const double u = sk * lin[2 + 4 * m - (m * (m - 1)) / 2] * sk;  // Ukk incl. the prior block
+        const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+        acc[1] += 0.5 * ((sk * lin[12 + m]) * ym + dd * ym * ym);
+        const double fn = c.sw_k * (P.prior[m] - kn);
+        acc[2] += 0.5 * fn * fn;
+        acc[3] += kn * kn;
+    }
+}
+
 struct LmParams {
     double min_relative_decrease, max_radius, min_radius, function_tolerance, gradient_tolerance,
         parameter_tolerance;
@@ -213,12 +265,12 @@ hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, D
 hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
+hipError_t launch_factor(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 // back-substitution, candidate evaluation, step scalars and the LM decision (k_final fuses k_lm_decide)
 hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, hipStream_t s,
                          Prof* pf);
 hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_bcr(const DevProblem& P, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
+hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
 // 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);

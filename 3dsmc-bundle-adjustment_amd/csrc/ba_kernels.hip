@@ -116,11 +116,15 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
 
 // ---------------------------------------------------------------- camera side
 // One workgroup per sub-segment (<= SUBSEG_OBS observations of one camera) of the
-// camera-major observation list; k_cam_reduce sums a camera's sub-segments in order.
+// camera-major observation list; k_cam_finalize sums a camera's sub-segments in order.
 // camdata (per sub-segment partial here): U upper-packed (21), C (6x4 = 24), g (6)
 // seg_intr[s*SEGINTR + ..]: Ukk upper-packed (10), gk (4), cost (1)
 __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
-                                                  double* __restrict__ camdata, double* __restrict__ seg_intr) {
+                                                  double* __restrict__ camdata, double* __restrict__ seg_intr,
+                                                  double* __restrict__ gmax_word) {
+    // lin[1] is max-accumulated by k_cam_finalize (read only after a linearisation): clear it here,
+    // one kernel boundary ahead, whether or not this iteration linearises
+    if (blockIdx.x == 0 && threadIdx.x == 0) *gmax_word = 0.0;
     if (st->done || (gated && !st->need_lin)) return;
     const int cur = st->cur;
     __shared__ double lds[4 * 66];
@@ -192,17 +196,77 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
     for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = out[51 + i];
 }
 
-// camdata[ac] = sum of the camera's sub-segment partials, in sub-segment order (zero when
-// this landmark shard has no observation of the camera).
-__global__ void k_cam_reduce(DevProblem P, const LmState* __restrict__ st, int gated, const double* __restrict__ part,
-                             double* __restrict__ camdata) {
+// One launch for what follows the camera-side pass (was k_cam_reduce + k_lin_finalize):
+//   workgroup ac < nac: camdata[ac] = sum of the camera's sub-segment partials, in sub-segment order
+//     (zero when this landmark shard has no observation of the camera); mode 0 also takes the camera's
+//     share of the gradient max-norm ||x - Plus(x, -g)||_inf and max-accumulates it into lin[1]
+//     (non-negative doubles order like their bit patterns; k_cam_side cleared the word);
+//   workgroup nac: the intrinsics partials, in a fixed order. mode 0: k_lin_finalize's mode-0 body
+//     without the camera loop (lin[0], lin[2..16), intrinsics gradient max into lin[1]); mode 1
+//     (sharded, before the all-reduce): the sums go to linpart, k_lin_finalize mode 2 finishes.
+__global__ __launch_bounds__(TPB) void k_cam_finalize(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                      int gated, const double* __restrict__ cpart,
+                                                      double* __restrict__ camdata, const double* __restrict__ seg_intr,
+                                                      double* __restrict__ lin, int mode, double* __restrict__ linpart) {
     if (st->done || (gated && !st->need_lin)) return;
-    const int ac = blockIdx.x, i = threadIdx.x;
-    if (i >= CAMDATA) return;
-    const int2 r = P.ac_seg[ac];
-    double v = 0.0;
-    for (int sg = r.x; sg < r.y; ++sg) v += part[(size_t)sg * CAMDATA + i];
-    camdata[(size_t)ac * CAMDATA + i] = v;
+    __shared__ double lds[4 * SEGINTR];
+    __shared__ double out[SEGINTR];
+    __shared__ double g6[6];
+    const int cur = st->cur;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (b < P.nac) {
+        if (tid < CAMDATA) {
+            const int2 r = P.ac_seg[b];
+            double v = 0.0;
+            for (int sg = r.x; sg < r.y; ++sg) v += cpart[(size_t)sg * CAMDATA + tid];
+            camdata[(size_t)b * CAMDATA + tid] = v;
+            if (tid >= 45) g6[tid - 45] = v;
+        }
+        if (mode != 0) return;
+        __syncthreads();
+        if (tid == 0) {
+            const double* x = P.cams[cur] + 7 * P.ac_cam[b];
+            double ng[6], tp[7];
+#pragma unroll
+            for (int d = 0; d < 6; ++d) ng[d] = -g6[d];
+            se3_plus(x, ng, tp);
+            double gm = 0.0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) gm = fmax(gm, fabs(x[j] - tp[j]));
+            atomicMax((unsigned long long*)(lin + 1), (unsigned long long)__double_as_longlong(gm));
+        }
+        return;
+    }
+    double acc[SEGINTR];
+#pragma unroll
+    for (int i = 0; i < SEGINTR; ++i) acc[i] = 0.0;
+    for (int sg = tid; sg < P.n_seg; sg += TPB)
+#pragma unroll
+        for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)sg * SEGINTR + i];
+    block_sum<SEGINTR>(acc, lds, out);
+    if (mode == 1) {
+        if (tid < SEGINTR) linpart[tid] = out[tid];
+        return;
+    }
+    if (tid == 0) {
+        const double* K = P.K[cur];
+        double pc = 0.0, gm = 0.0;
+        double gk[4];
+        for (int m = 0; m < 4; ++m) {
+            const double fk = c.sw_k * (P.prior[m] - K[m]);
+            pc += fk * fk;
+            gk[m] = out[10 + m] + (-c.sw_k) * fk;
+            gm = fmax(gm, fabs(K[m] - (K[m] + -gk[m])));
+        }
+        lin[0] = out[14] + 0.5 * pc;
+        atomicMax((unsigned long long*)(lin + 1), (unsigned long long)__double_as_longlong(gm));
+        for (int q = 0; q < 10; ++q) lin[2 + q] = out[q];
+        int q = 0;
+        for (int m = 0; m < 4; ++m)
+            for (int l = m; l < 4; ++l, ++q)
+                if (l == m) lin[2 + q] += c.sw_k * c.sw_k;
+        for (int m = 0; m < 4; ++m) lin[12 + m] = gk[m];
+    }
 }
 
 // Reduce intrinsics partials (fixed order), add the IntrinsicsPrior block
@@ -472,36 +536,12 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
     block_sum<14>(kk, lds, out);
     gmax = block_max(gmax, red);
     bad = block_max(bad, red);
-    // intrinsics terms: one partial per workgroup, summed in a fixed order by k_pp_reduce (a
+    // intrinsics terms: one partial per workgroup, summed in a fixed order by k_env_assemble (a
     // same-address f64 atomic per workgroup serialises at ~45 ns each: 391 x 14 of them cost ~17 us)
     if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + blockIdx.x] = out[threadIdx.x];
     if (threadIdx.x == 0) {
         part[PART_PT_GMAX * P.part_stride + blockIdx.x] = gmax;
         part[PART_PT_BAD * P.part_stride + blockIdx.x] = bad;
-    }
-}
-
-// S_kk += sum of the point workgroups' intrinsics Schur terms (fixed order), rhs_k likewise.
-__global__ __launch_bounds__(TPB) void k_pp_reduce(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
-                                                   const double* __restrict__ part, double* __restrict__ S,
-                                                   double* __restrict__ rhs) {
-    __shared__ double lds[4 * 14];
-    __shared__ double out[14];
-    if (st->done) return;
-    double acc[14];
-#pragma unroll
-    for (int q = 0; q < 14; ++q) acc[q] = 0.0;
-    for (int i = threadIdx.x; i < nblk_pt; i += TPB)
-#pragma unroll
-        for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + i];
-    block_sum<14>(acc, lds, out);
-    if (threadIdx.x < 10) {
-        int m = 0, q = threadIdx.x;
-        while (q >= 4 - m) { q -= 4 - m; ++m; }
-        const int l = m + q;  // packed (m, l), l >= m
-        S[(size_t)(P.kb + l) * P.npad + P.kb + m] += out[threadIdx.x];
-    } else if (threadIdx.x < 14) {
-        rhs[P.kb + threadIdx.x - 10] += out[threadIdx.x];
     }
 }
 
@@ -1418,49 +1458,10 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
     const double radius = st->radius;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
-    if (t < P.nac) {
-        const int cam = P.ac_cam[t];
-        const double* cd = camdata + (size_t)t * CAMDATA;
-        double d[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const double sc = scale[6 * t + k], yk = y[6 * t + k];
-            d[k] = -yk * sc;
-            delta[6 * t + k] = d[k];
-            const double u = sc * cd[k * 6 - (k * (k - 1)) / 2] * sc;  // diag of s U s (k_env_assemble)
-            const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
-            acc[1] += 0.5 * ((sc * cd[45 + k]) * yk + dd * yk * yk);
-        }
-        const double* x = P.cams[cur] + 7 * cam;
-        double* xn = P.cams[cur ^ 1] + 7 * cam;
-        double tp[7];
-        se3_plus(x, d, tp);
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-            xn[j] = tp[j];
-            const double df = x[j] - tp[j];
-            acc[0] += df * df;
-            acc[3] += tp[j] * tp[j];
-        }
-    } else if (t == P.nac) {
-        const double* K = P.K[cur];
-        double* Kn = P.K[cur ^ 1];
-        for (int m = 0; m < 4; ++m) {
-            const double sk = scale[P.off_k + m], ym = y[P.kb + m];
-            const double dk = -ym * sk;
-            delta[P.kb + m] = dk;
-            const double kn = K[m] + dk;
-            Kn[m] = kn;
-            const double df = K[m] - kn;
-            acc[0] += df * df;
-            const double u = sk * lin[2 + 4 * m - (m * (m - 1)) / 2] * sk;  // Ukk incl. the prior block
-            const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
-            acc[1] += 0.5 * ((sk * lin[12 + m]) * ym + dd * ym * ym);
-            const double fn = c.sw_k * (P.prior[m] - kn);
-            acc[2] += 0.5 * fn * fn;
-            acc[3] += kn * kn;
-        }
-    }
+    if (t < P.nac)
+        update_camera(P, c, cur, radius, scale, camdata, t, y + 6 * t, delta, acc);
+    else if (t == P.nac)
+        update_intrinsics(P, c, cur, radius, scale, lin, y + P.kb, delta, acc);
     block_sum<4>(acc, lds, out);
     if (threadIdx.x == 0) {
         part[PART_UPD_SN2 * P.part_stride + blockIdx.x] = out[0];
@@ -1612,12 +1613,28 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
                                                       const int2* __restrict__ tiles, const double* __restrict__ camdata,
                                                       const double* __restrict__ lin, const double* __restrict__ scale,
                                                       double* __restrict__ S, double* __restrict__ rhs,
-                                                      int* __restrict__ chol_flag) {
+                                                      int* __restrict__ chol_flag, int nblk_pt,
+                                                      const double* __restrict__ part) {
+    __shared__ double lds[4 * 14];
+    __shared__ double kko[14];
     if (st->done) return;
     const int2 ij = tiles[blockIdx.x];
     const int tid = threadIdx.x;
     const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
     const int nd = 6 * P.nac, kb = P.kb;
+    // tiles meeting the intrinsics block (rows/cols kb..kb+3; it can straddle two tile rows) add the
+    // points' intrinsics Schur terms: k_point_prep's per-workgroup partials, summed in a fixed order
+    // (identical in every such tile). This was k_pp_reduce (one launch less per LM iteration).
+    const bool kk_tile = 16 * ij.x + 15 >= kb && 16 * ij.x < kb + 4 && 16 * ij.y + 15 >= kb && 16 * ij.y < kb + 4;
+    if (kk_tile) {  // uniform per workgroup
+        double acc[14];
+#pragma unroll
+        for (int q = 0; q < 14; ++q) acc[q] = 0.0;
+        for (int i = tid; i < nblk_pt; i += TPB)
+#pragma unroll
+            for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + i];
+        block_sum<14>(acc, lds, kko);
+    }
     const double* sk = scale + P.off_k;
     double v = 0.0;
     if (P.rank == 0) {
@@ -1640,6 +1657,10 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
             v = 1.0;
         }
     }
+    if (kk_tile && r >= kb && r < kb + 4 && col >= kb && col <= r) {
+        const int m = col - kb, l = r - kb;
+        v += kko[4 * m - m * (m - 1) / 2 + (l - m)];
+    }
     S[(size_t)r * P.npad + col] = v;
     if (ij.x == ij.y && tid < 16) {
         const int rr = 16 * ij.x + tid;
@@ -1648,6 +1669,7 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
             if (rr < nd) b = scale[rr] * camdata[(size_t)(rr / 6) * CAMDATA + 45 + rr % 6];
             else if (rr < kb + 4) b = sk[rr - kb] * lin[12 + rr - kb];
         }
+        if (kk_tile && rr >= kb && rr < kb + 4) b += kko[10 + rr - kb];
         rhs[rr] = b;
     }
     if (blockIdx.x == 0 && tid == 0) *chol_flag = 0;
@@ -2004,19 +2026,20 @@ int schur_tile_slots() {
 
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
     if (P.n_seg > 0)
-        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr);
-    if (P.nac > 0)
-        PL(K_CAM_REDUCE, k_cam_reduce, dim3(P.nac), dim3(64), 0, s, P, W.st, gated, W.camdata_part, W.camdata_loc);
-    if (!W.comm.on()) {
-        PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin, 0,
-           (double*)nullptr);
+        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr,
+           W.lin + 1);
+    else
+        CK(hipMemsetAsync(W.lin + 1, 0, sizeof(double), s));
+    const size_t ncd = (size_t)P.nac * CAMDATA;
+    if (!W.comm.on()) {  // camdata_loc == camdata unsharded
+        PL(K_LIN_FINALIZE, k_cam_finalize, dim3(P.nac + 1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part,
+           W.camdata_loc, W.seg_intr, W.lin, 0, (double*)nullptr);
         return hipSuccess;
     }
     // sharded: one all-reduce of [camdata | intrinsics partials] between the local sums and
     // the finalisation (camdata_loc is zero for cameras this shard does not observe)
-    const size_t ncd = (size_t)P.nac * CAMDATA;
-    PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_loc, W.seg_intr, W.lin, 1,
-       W.camdata_loc + ncd);
+    PL(K_LIN_FINALIZE, k_cam_finalize, dim3(P.nac + 1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part,
+       W.camdata_loc, W.seg_intr, W.lin, 1, W.camdata_loc + ncd);
     COMM(W.camdata_loc, W.camdata, ncd + SEGINTR, COMM_F64, COMM_SUM);
     PL(K_LIN_FINALIZE, k_lin_finalize, dim3(1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata, W.seg_intr, W.lin, 2,
        W.camdata + ncd);
@@ -2040,13 +2063,12 @@ hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Pro
 }
 
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
-    // envelope of S: clear + camera / intrinsics blocks, LM diagonal, pad (rank 0 only), rhs, chol_flag
-    PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin, W.scale,
-       W.S, W.rhs, W.chol_flag);
+    // point records + intrinsics Schur partials, then the envelope of S: clear + camera / intrinsics
+    // blocks, LM diagonal, pad (rank 0 only), the points' intrinsics terms, rhs, chol_flag
     if (P.n_ap > 0)
         CK(launch_point_prep(P, c, 1, W, s, pf));
-    if (P.n_ap > 0)
-        PL(K_PP_REDUCE, k_pp_reduce, dim3(1), dim3(TPB), 0, s, P, W.st, pp_blocks(P.n_ap), W.part, W.S, W.rhs);
+    PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin, W.scale,
+       W.S, W.rhs, W.chol_flag, P.n_ap > 0 ? pp_blocks(P.n_ap) : 0, W.part);
     if (P.n_tiles > 0)
     {
         static int smode = -1;
@@ -2123,8 +2145,8 @@ static hipError_t launch_band(const DevProblem& P, DevWork& W, hipStream_t s, Pr
     return hipSuccess;
 }
 
-hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
-    if (P.solver == 2) return launch_bcr(P, W, W.bcr, s, pf);
+hipError_t launch_factor(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
+    if (P.solver == 2) return launch_bcr(P, c, W, W.bcr, s, pf);  // k_bcr_border also applies the camera step
     if (P.solver == 1) switch (P.band_w) {
         case 1: return launch_band<1>(P, W, s, pf);
         case 2: return launch_band<2>(P, W, s, pf);
@@ -2141,15 +2163,18 @@ hipError_t launch_factor(const DevProblem& P, DevWork& W, hipStream_t s, Prof* p
 
 hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, hipStream_t s,
                          Prof* pf) {
-    const int nb_upd = nblocks(P.nac + 1, TPB);
+    // BCR: k_bcr_border already applied the camera / intrinsics step (one partial per BCR block)
+    const bool fused_upd = P.solver == 2;
+    const int nb_upd = fused_upd ? (P.nac + BCR_CAMS - 1) / BCR_CAMS : nblocks(P.nac + 1, TPB);
     static int ndummy = -1;
     if (ndummy < 0) {
         const char* e = getenv("MIBA_DUMMY_LAUNCHES");  // diagnostic: extra empty launches per iteration
         ndummy = e ? atoi(e) : 0;
     }
     for (int k = 0; k < ndummy; ++k) PL(K_DUMMY, k_dummy, dim3(1), dim3(64), 0, s, W.st);
-    PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.camdata, W.lin, W.rhs, W.delta,
-       W.part);
+    if (!fused_upd)
+        PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.camdata, W.lin, W.rhs,
+           W.delta, W.part);
     const int nb_bs = P.n_bs_chunks;
     if (P.n_ap > 0)
         PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,

@@ -539,7 +539,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     HIPCHECK(ctx, upload(ctx, B_ROWS, rows.data(), rows.size()));
     const int n_seg = (int)seg_cam.size();
     const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
-    const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, 1});
+    const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS, 1});
     HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
     // landmark sharding: envelope tile list of S, pack buffers, exchange scalars
     // envelope tiles of S: every solver reads only these; the per-iteration clear of S covers
@@ -872,7 +872,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         for (int i = 0; i < batch && launched <= max_iter + 1; ++i, ++launched) {
             HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
             HIPCHECK(ctx, launch_build(P, C, W, s, pf));
-            HIPCHECK(ctx, launch_factor(P, W, s, pf));
+            HIPCHECK(ctx, launch_factor(P, C, W, s, pf));
             HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
         }
         HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
