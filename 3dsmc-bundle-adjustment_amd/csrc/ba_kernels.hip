@@ -384,6 +384,76 @@ __device__ __forceinline__ void group_sum(double (&v)[NV]) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
 }
+// Point tail of the Schur preparation, from the point's sums acc = V packed (6) | e (3) | Kt (12):
+// gradient max-norm term, scaled + LM-damped V~, G = chol(V~)^-1, e~, K~, D~ -> rec[PDATA]; with
+// want_kk also the intrinsics Schur terms -Zk Zk^T (10 packed), -Zk ze (4) -> kk.
+__device__ __forceinline__ void point_tail(const DevProblem& P, const BaConsts& c, double radius,
+                                           const double* __restrict__ scale, int ap, const double* X,
+                                           const double* acc, bool want_kk, double* rec, double* kk, double& gmax,
+                                           double& bad) {
+    const double* V = acc;
+    const double* e = acc + 6;
+    const double* Kt = acc + 9;
+    // gradient max-norm contribution (points: x - (x + -g))
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gmax = fmax(gmax, fabs(X[i] - (X[i] + -e[i])));
+    const double* sp = scale + P.off_pt + 3 * ap;
+    const double* sk = scale + P.off_k;
+    const double s0 = sp[0], s1 = sp[1], s2 = sp[2];
+    // scaled, damped V  (Ceres: lm_diagonal = sqrt(clamp(diag(JtJ~)) / radius))
+    double v00 = s0 * V[0] * s0, v01 = s0 * V[1] * s1, v02 = s0 * V[2] * s2;
+    double v11 = s1 * V[3] * s1, v12 = s1 * V[4] * s2, v22 = s2 * V[5] * s2;
+    rec[21] = fmin(fmax(v00, c.min_diag), c.max_diag) / radius;  // D~ (model cost change, k_backsub_chunk)
+    rec[22] = fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
+    rec[23] = fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
+    v00 += rec[21];
+    v11 += rec[22];
+    v22 += rec[23];
+    // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rec[i] = 0.0;  // g00 g10 g11 g20 g21 g22
+    const bool pd = v00 > 0.0;
+    const double L00 = sqrt(v00);
+    const double L10 = v01 / L00, L20 = v02 / L00;
+    const double l11 = v11 - L10 * L10;
+    const double L11 = sqrt(l11);
+    const double L21 = (v12 - L20 * L10) / L11;
+    const double l22 = v22 - L20 * L20 - L21 * L21;
+    const double L22 = sqrt(l22);
+    if (pd && l11 > 0.0 && l22 > 0.0 && isfinite(l22)) {
+        const double i00 = 1 / L00, i11 = 1 / L11, i22 = 1 / L22;
+        rec[0] = i00;
+        rec[1] = -L10 * i00 * i11;
+        rec[2] = i11;
+        rec[4] = -L21 * i11 * i22;
+        rec[3] = -(L20 * i00 + L21 * rec[1]) * i22;
+        rec[5] = i22;
+    } else {
+        bad = 1.0;
+    }
+    const double* G = rec;
+    double* es = rec + 6;
+    double* Ks = rec + 9;
+    es[0] = s0 * e[0]; es[1] = s1 * e[1]; es[2] = s2 * e[2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        Ks[m * 3 + 0] = sk[m] * Kt[m * 3 + 0] * s0;
+        Ks[m * 3 + 1] = sk[m] * Kt[m * 3 + 1] * s1;
+        Ks[m * 3 + 2] = sk[m] * Kt[m * 3 + 2] * s2;
+    }
+    if (want_kk) {  // intrinsics Schur terms once per point: -Zk Zk^T (10 packed), -Zk ze (4)
+        double Zk[12], ze[3];
+        zk_ze(G, Ks, es, Zk, ze);
+        int qq = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int l = m; l < 4; ++l, ++qq)
+                kk[qq] = -(Zk[m * 3 + 0] * Zk[l * 3 + 0] + Zk[m * 3 + 1] * Zk[l * 3 + 1] + Zk[m * 3 + 2] * Zk[l * 3 + 2]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) kk[10 + m] = -(Zk[m * 3 + 0] * ze[0] + Zk[m * 3 + 1] * ze[1] + Zk[m * 3 + 2] * ze[2]);
+    }
+}
 template <int PP_LANES>
 __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c, const LmState* __restrict__ st, int mode,
                                                        const double* __restrict__ scale, double* __restrict__ cnp,
@@ -463,73 +533,12 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
                 if (i % PP_LANES == q) cnp[3 * ap + i] = v3[i];
         } else {
             group_sum<PP_LANES>(acc);
-            const double* V = acc;
-            const double* e = acc + 6;
-            const double* Kt = acc + 9;
-            // gradient max-norm contribution (points: x - (x + -g))
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gmax = fmax(gmax, fabs(X[i] - (X[i] + -e[i])));
-            const double* sp = scale + P.off_pt + 3 * ap;
-            const double* sk = scale + P.off_k;
-            const double s0 = sp[0], s1 = sp[1], s2 = sp[2];
-            // scaled, damped V  (Ceres: lm_diagonal = sqrt(clamp(diag(JtJ~)) / radius))
-            double v00 = s0 * V[0] * s0, v01 = s0 * V[1] * s1, v02 = s0 * V[2] * s2;
-            double v11 = s1 * V[3] * s1, v12 = s1 * V[4] * s2, v22 = s2 * V[5] * s2;
             double rec[PDATA];
-            rec[21] = fmin(fmax(v00, c.min_diag), c.max_diag) / radius;  // D~ (model cost change, k_backsub_chunk)
-            rec[22] = fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
-            rec[23] = fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
-            v00 += rec[21];
-            v11 += rec[22];
-            v22 += rec[23];
-            // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
-#pragma unroll
-            for (int i = 0; i < 6; ++i) rec[i] = 0.0;  // g00 g10 g11 g20 g21 g22
-            const bool pd = v00 > 0.0;
-            const double L00 = sqrt(v00);
-            const double L10 = v01 / L00, L20 = v02 / L00;
-            const double l11 = v11 - L10 * L10;
-            const double L11 = sqrt(l11);
-            const double L21 = (v12 - L20 * L10) / L11;
-            const double l22 = v22 - L20 * L20 - L21 * L21;
-            const double L22 = sqrt(l22);
-            if (pd && l11 > 0.0 && l22 > 0.0 && isfinite(l22)) {
-                const double i00 = 1 / L00, i11 = 1 / L11, i22 = 1 / L22;
-                rec[0] = i00;
-                rec[1] = -L10 * i00 * i11;
-                rec[2] = i11;
-                rec[4] = -L21 * i11 * i22;
-                rec[3] = -(L20 * i00 + L21 * rec[1]) * i22;
-                rec[5] = i22;
-            } else {
-                bad = 1.0;
-            }
-            const double* G = rec;
-            double* es = rec + 6;
-            double* Ks = rec + 9;
-            es[0] = s0 * e[0]; es[1] = s1 * e[1]; es[2] = s2 * e[2];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                Ks[m * 3 + 0] = sk[m] * Kt[m * 3 + 0] * s0;
-                Ks[m * 3 + 1] = sk[m] * Kt[m * 3 + 1] * s1;
-                Ks[m * 3 + 2] = sk[m] * Kt[m * 3 + 2] * s2;
-            }
+            point_tail(P, c, radius, scale, ap, X, acc, q == 0, rec, kk, gmax, bad);
             double* pd_out = pdata + (size_t)ap * PDATA;
 #pragma unroll
             for (int i = 0; i < PDATA; ++i)
                 if (i % PP_LANES == q) pd_out[i] = rec[i];
-            if (q == 0) {  // intrinsics Schur terms once per point: -Zk Zk^T (10 packed), -Zk ze (4)
-                double Zk[12], ze[3];
-                zk_ze(G, Ks, es, Zk, ze);
-                int qq = 0;
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-#pragma unroll
-                    for (int l = m; l < 4; ++l, ++qq)
-                        kk[qq] = -(Zk[m * 3 + 0] * Zk[l * 3 + 0] + Zk[m * 3 + 1] * Zk[l * 3 + 1] + Zk[m * 3 + 2] * Zk[l * 3 + 2]);
-#pragma unroll
-                for (int m = 0; m < 4; ++m) kk[10 + m] = -(Zk[m * 3 + 0] * ze[0] + Zk[m * 3 + 1] * ze[1] + Zk[m * 3 + 2] * ze[2]);
-            }
         }
     }
     if (mode == 0) return;
@@ -2001,6 +2010,9 @@ int pp_lanes() {
     return lanes;
 }
 
+// number of per-workgroup partials (PART_PT_*) the Schur preparation writes
+int pp_parts(const DevProblem& P) { return P.n_ap > 0 ? pp_blocks(P.n_ap) : 0; }
+
 static hipError_t launch_point_prep(const DevProblem& P, const BaConsts& c, int mode, DevWork& W, hipStream_t s, Prof* pf) {
     const int kid = mode == 0 ? K_POINT_COLNORM : K_POINT_PREP;
     const dim3 g(pp_blocks(P.n_ap)), b(PP_TPB);
@@ -2068,7 +2080,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     if (P.n_ap > 0)
         CK(launch_point_prep(P, c, 1, W, s, pf));
     PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin, W.scale,
-       W.S, W.rhs, W.chol_flag, P.n_ap > 0 ? pp_blocks(P.n_ap) : 0, W.part);
+       W.S, W.rhs, W.chol_flag, pp_parts(P), W.part);
     if (P.n_tiles > 0)
     {
         static int smode = -1;
@@ -2179,7 +2191,7 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
     if (P.n_ap > 0)
         PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part);
-    const int nb_pt = P.n_ap > 0 ? pp_blocks(P.n_ap) : 0;
+    const int nb_pt = pp_parts(P);
     if (!W.comm.on()) {
         PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
            W.chol_flag, W.scal, prm, W.lin, W.log);
