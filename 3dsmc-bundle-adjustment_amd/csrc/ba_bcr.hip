@@ -509,7 +509,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
                                                     const double* __restrict__ S, const double* __restrict__ rhs,
                                                     BcrWork Bw, int m, int nel, int* __restrict__ flag,
                                                     unsigned long long* __restrict__ stamps) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ElimLds& L = *reinterpret_cast<ElimLds*>(smem);
     const int nblk = Bw.nblk;
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
 // one per wave, MFMA operands loaded straight from X (L2-resident):
 //   t in [0,10) UL lower tiles, [10,20) UR lower tiles, [20,36) F, [36,40) rL, [40,44) rR
 __global__ __launch_bounds__(TPB_C) void k_bcr_contrib(const LmState* __restrict__ st, BcrWork Bw, int m) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int s = 1 << m;
     const int bi = (int)blockIdx.x / NCONTRIB_WG, r = (int)blockIdx.x % NCONTRIB_WG;
     const int i = s + 2 * s * bi;
@@ -705,7 +705,7 @@ template <bool STAMP>
 __global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ st, DevProblem P,
                                                     const double* __restrict__ S, BcrWork Bw, int m,
                                                     unsigned long long* __restrict__ stamps) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BackLds& L = *reinterpret_cast<BackLds*>(smem);
     const int s = 1 << m;
@@ -788,7 +788,7 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
                                                        const double* __restrict__ camdata,
                                                        const double* __restrict__ lin, double* __restrict__ delta,
                                                        double* __restrict__ part) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     __shared__ double red[20];
     __shared__ double yk[4];
     __shared__ double ybl[G_DOF];
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
                                                        const double* __restrict__ S, const double* __restrict__ rhs,
                                                        BcrWork Bw, int* __restrict__ flag,
                                                        unsigned long long* __restrict__ tl) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     TL(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     PersistLds& L = *reinterpret_cast<PersistLds*>(smem);
@@ -1242,7 +1242,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                                                      const double* __restrict__ S, const double* __restrict__ rhs,
                                                      BcrWork Bw, int* __restrict__ flag,
                                                      unsigned long long* __restrict__ tl) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     TLS(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nblk = Bw.nblk;

@@ -134,7 +134,13 @@ struct LmState {
     double radius, decrease_factor, x_cost, xnorm2, final_cost, gmax_ci, initial_cost;
     double msg_a, msg_b;
     int iter, n_succ, n_unsucc, n_invalid, step_ok, cur, need_lin, done, termination, msg;
+    // the next decision terminates at max_num_iterations before it looks at a step (Ceres checks the
+    // iteration count before ComputeTrustRegionStep): that iteration only re-linearises, so the step
+    // kernels (assembly, Schur, reduced solve, back-substitution) exit at once, like after `done`
+    int stop_next;
+    int n_decide;  // decisions taken (host progress word)
 };
+__device__ __forceinline__ bool skip_step(const LmState* st) { return st->done | st->stop_next; }
 // Camera / intrinsics step application (k_update_cams, or fused into k_bcr_border): delta = -s*y,
 // Sophus T*exp(delta) into the candidate slot, and the block's terms of the step scalars
 // acc = {|step|^2, model cost change 0.5 (g~ y + D~ y^2), candidate prior cost, |x_cand|^2}.
@@ -191,6 +197,7 @@ struct LmParams {
     double min_relative_decrease, max_radius, min_radius, function_tolerance, gradient_tolerance,
         parameter_tolerance;
     int max_iter, max_invalid;
+    unsigned* progress;  // host-mapped word: n_decide | done << 31 after every decision (nullptr: none)
 };
 enum LmMsg { MSG_NONE = 0, MSG_MAX_ITER, MSG_GRAD_TOL, MSG_MIN_RADIUS, MSG_PARAM_TOL, MSG_FUNC_TOL, MSG_INVALID,
              MSG_EVAL_FAIL };

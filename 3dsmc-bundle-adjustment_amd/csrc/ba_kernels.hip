@@ -103,6 +103,36 @@ __device__ __forceinline__ void block_sum_rs(double (&v)[NV], double* lds, doubl
     __syncthreads();
 }
 
+// NW-wave variants (k_final runs 16 waves); lds holds NW * NV doubles. Wave sums added in wave order.
+template <int NW, int NV>
+__device__ __forceinline__ void block_sum_nw(double (&v)[NV], double* lds, double* out) {
+    wave_sum<NV>(v);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        double a = lds[threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) a += lds[w * NV + threadIdx.x];
+        out[threadIdx.x] = a;
+    }
+    __syncthreads();
+}
+template <int NW>
+__device__ __forceinline__ double block_max_nw(double v, double* lds) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = lds[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) r = fmax(r, lds[w]);
+    __syncthreads();
+    return r;
+}
+
 __device__ __forceinline__ double block_max(double v, double* lds) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
@@ -583,7 +613,7 @@ __global__ void k_scale(DevProblem P, const double* __restrict__ camdata, const 
 __global__ void k_assemble(DevProblem P, BaConsts c, const LmState* __restrict__ st, const double* __restrict__ camdata,
                            const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
                            double* __restrict__ rhs) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     const double radius = st->radius;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const size_t ld = P.npad;
@@ -623,7 +653,7 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, con
                                                    const double* __restrict__ scale,
                                                    const double* __restrict__ pdata, double* __restrict__ S,
                                                    double* __restrict__ rhs) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int cur = st->cur;
     const int t = blockIdx.x * TPB + threadIdx.x;
     if (t >= P.n_ovf_obs) return;
@@ -738,7 +768,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
                                                     const double* __restrict__ pdata, double* __restrict__ S,
                                                     double* __restrict__ rhs, unsigned long long* __restrict__ stamps) {
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
-    if (st->done) return;
+    if (skip_step(st)) return;
     unsigned long long t_prev = 0, st_acc[4] = {0, 0, 0, 0};
 #define SCH_STAMP(k)                                          \
     do {                                                      \
@@ -935,7 +965,7 @@ __global__ __launch_bounds__(TPB) void k_chol(const LmState* __restrict__ st, do
                                               const int* __restrict__ fcol,
                                               const int* __restrict__ rptr, const int* __restrict__ rows,
                                               double* __restrict__ b, int* __restrict__ flag) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     __shared__ double Lkk[16][17];
     __shared__ double red[16][17];
     __shared__ int s_bad;
@@ -1152,7 +1182,7 @@ __global__ __launch_bounds__(TPB) void k_chol_band(const LmState* __restrict__ s
                                                    const int* __restrict__ fcol,
                                                    double* __restrict__ b, int* __restrict__ flag,
                                                    unsigned long long* __restrict__ stamps) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BandLds<W>& L = *reinterpret_cast<BandLds<W>*>(smem);
     int* fc_s = reinterpret_cast<int*>(smem + sizeof(BandLds<W>));
@@ -1462,7 +1492,7 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
                               const double* __restrict__ y, double* __restrict__ delta, double* __restrict__ part) {
     __shared__ double lds[4 * 4];
     __shared__ double out[4];
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int cur = st->cur;
     const double radius = st->radius;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1496,7 +1526,7 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
     __shared__ double dpl[BS_PTS][3];
     __shared__ double lds[4 * 5];
     __shared__ double out[5];
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int cur = st->cur;
     const int ch = blockIdx.x, tid = threadIdx.x;
     const int apb = P.bs_chunk[ch], ape = P.bs_chunk[ch + 1];
@@ -1607,7 +1637,7 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
 // Clear the envelope tiles of S (every solver reads only these; the rest stays zero).
 __global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st, const int2* __restrict__ tiles, int npad,
                                                   double* __restrict__ S) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int2 ij = tiles[blockIdx.x];
     S[(size_t)(16 * ij.x + (threadIdx.x >> 4)) * npad + 16 * ij.y + (threadIdx.x & 15)] = 0.0;
 }
@@ -1626,7 +1656,7 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
                                                       const double* __restrict__ part) {
     __shared__ double lds[4 * 14];
     __shared__ double kko[14];
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int2 ij = tiles[blockIdx.x];
     const int tid = threadIdx.x;
     const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
@@ -1689,37 +1719,39 @@ __device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, co
                                const double* __restrict__ scal, double* __restrict__ log);
 // scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]; then the LM decision (k_lm_decide's
 // body, fused: one launch less per iteration)
-__global__ __launch_bounds__(TPB) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
+// 16 waves: the ~2k back-substitution partials x 5 slots take 2 load rounds per thread instead of 8
+static constexpr int TPB_F = 1024, NW_F = TPB_F / 64;
+__global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                                int nblk_bs, const double* __restrict__ part,
                                                const int* __restrict__ chol_flag, double* __restrict__ scal,
                                                LmParams prm, const double* __restrict__ lin, double* __restrict__ log) {
-    __shared__ double lds[4 * 4];
+    __shared__ double lds[NW_F * 4];
     __shared__ double out[4];
-    __shared__ double red[4];
+    __shared__ double red[NW_F];
     if (st->done) return;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double gm = 0.0, bad = 0.0;
     const size_t stp = P.part_stride;
-    for (int i = threadIdx.x; i < nblk_upd; i += TPB) {
+    for (int i = threadIdx.x; i < nblk_upd; i += TPB_F) {
         acc[0] += part[PART_UPD_SN2 * stp + i];
         acc[1] += part[PART_UPD_MCC * stp + i];
         acc[2] += part[PART_UPD_COST * stp + i];
         acc[3] += part[PART_UPD_XN2 * stp + i];
     }
-    for (int i = threadIdx.x; i < nblk_bs; i += TPB) {
+    for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
         acc[0] += part[PART_BS_SN2 * stp + i];
         acc[1] += part[PART_BS_MCC * stp + i];
         acc[2] += part[PART_BS_COST * stp + i];
         acc[3] += part[PART_BS_XN2 * stp + i];
         bad = fmax(bad, part[PART_BS_BAD * stp + i]);
     }
-    for (int i = threadIdx.x; i < nblk_pt; i += TPB) {
+    for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
         gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
     }
-    block_sum<4>(acc, lds, out);
-    gm = block_max(gm, red);
-    bad = block_max(bad, red);
+    block_sum_nw<NW_F, 4>(acc, lds, out);
+    gm = block_max_nw<NW_F>(gm, red);
+    bad = block_max_nw<NW_F>(bad, red);
     if (threadIdx.x == 0) {
         scal[SC_XN2] = out[3];
         scal[SC_SN2] = out[0];
@@ -1737,7 +1769,7 @@ __global__ __launch_bounds__(TPB) void k_final(DevProblem P, LmState* __restrict
 __global__ __launch_bounds__(TPB) void k_env_pack(const LmState* __restrict__ st, const int2* __restrict__ tiles, int n_env,
                                                   int npad, double* __restrict__ S, double* __restrict__ rhs,
                                                   double* __restrict__ buf, int unpack) {
-    if (st->done) return;
+    if (skip_step(st)) return;
     const int t = blockIdx.x;
     if (t < n_env) {
         const int2 ij = tiles[t];
@@ -1862,8 +1894,21 @@ __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* 
 // One thread: Ceres 2.0 TrustRegionMinimizer::Minimize bookkeeping for the step whose
 // scalars k_final produced (model cost change, candidate cost, |step|, |x_cand|, flags).
 // Same decisions, in the same order, as oracle_solve() (oracle/ba_oracle.c).
+static __device__ void lm_decide_core(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
+                                      const double* __restrict__ scal, double* __restrict__ log);
 __device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
                                const double* __restrict__ scal, double* __restrict__ log) {
+    if (st->done) return;
+    lm_decide_core(st, prm, lin, scal, log);
+    LmState& S = *st;
+    S.n_decide += 1;
+    S.stop_next = !S.done && S.iter >= prm.max_iter;
+    if (prm.progress)
+        __hip_atomic_store(prm.progress, (unsigned)S.n_decide | (S.done ? 0x80000000u : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+static __device__ void lm_decide_core(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
+                                      const double* __restrict__ scal, double* __restrict__ log) {
     LmState S = *st;
     if (S.done) return;
     if (S.need_lin) {  // absorb the re-linearisation of the last accepted point
@@ -2193,7 +2238,7 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
            W.part);
     const int nb_pt = pp_parts(P);
     if (!W.comm.on()) {
-        PL(K_FINAL, k_final, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
+        PL(K_FINAL, k_final, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
            W.chol_flag, W.scal, prm, W.lin, W.log);
         return hipSuccess;
     }

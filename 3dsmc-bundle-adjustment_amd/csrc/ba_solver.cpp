@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ba.h"
@@ -70,6 +71,8 @@ struct ba_context {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    unsigned* hprog = nullptr;  // host-mapped LM progress word (LmParams::progress)
+    unsigned* dprog = nullptr;  // its device address
     DevBuf buf[B_COUNT];
     std::string err;
     // host-side structure of the last prepared problem
@@ -198,6 +201,8 @@ ba_context* ba_create(const ba_options* opts) {
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->hprog, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->dprog, ctx->hprog, 0);
     if (ctx->opts.profile_kernels) {
         for (int i = 0; i < 2 * Prof::MAXP && e == hipSuccess; ++i) e = hipEventCreate(&ctx->prof.ev[i]);
         ctx->prof_events = (e == hipSuccess);
@@ -222,6 +227,7 @@ void ba_destroy(ba_context* ctx) {
         if (e) hipEventDestroy(e);
     if (ctx->prof_events)
         for (int i = 0; i < 2 * Prof::MAXP; ++i) hipEventDestroy(ctx->prof.ev[i]);
+    if (ctx->hprog) hipHostFree(ctx->hprog);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -757,6 +763,7 @@ static LmState fresh_state(const ba_options& o, double radius) {
     st.n_succ = 1;  // iteration 0 counts as successful (Ceres convention)
     st.step_ok = 1;
     st.termination = -1;
+    st.stop_next = o.max_num_iterations <= 0;
     return st;
 }
 
@@ -849,7 +856,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     double kms0[K_COUNT];
     std::memcpy(kms0, ctx->k_ms, sizeof(kms0));
 
-    LmParams prm;
+    LmParams prm{};
     prm.min_relative_decrease = o.min_relative_decrease;
     prm.max_radius = o.max_trust_region_radius;
     prm.min_radius = o.min_trust_region_radius;
@@ -858,6 +865,8 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     prm.parameter_tolerance = o.parameter_tolerance;
     prm.max_iter = max_iter;
     prm.max_invalid = o.max_num_consecutive_invalid_steps;
+    prm.progress = ctx->dprog;
+    if (ctx->hprog) __atomic_store_n(ctx->hprog, 0u, __ATOMIC_RELEASE);
 
     // IterationZero: cost, gradient, column norms -> Jacobi scale, |x|
     HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
@@ -868,7 +877,30 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     int launched = 0;
     int batch = 2;
     LmState& S = h_state;
-    for (;;) {
+    if (!pf && ctx->hprog) {
+        // Unprofiled: keep LM_AHEAD iterations in flight and follow the device through the host-mapped
+        // progress word (n_decide | done << 31, written by every decision) instead of synchronising the
+        // stream per batch: the GPU never waits for the host, and at most LM_AHEAD - 1 iterations are
+        // enqueued past the termination (they exit at once).
+        constexpr int LM_AHEAD = 2;
+        volatile unsigned* hp = ctx->hprog;
+        for (;;) {
+            const unsigned w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
+            if ((w >> 31) || launched > max_iter + 1) break;
+            if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD) {
+                HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
+                HIPCHECK(ctx, launch_build(P, C, W, s, pf));
+                HIPCHECK(ctx, launch_factor(P, C, W, s, pf));
+                HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
+                ++launched;
+            } else {
+                std::this_thread::yield();
+            }
+        }
+        HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
+        HIPCHECK(ctx, hipStreamSynchronize(s));
+    }
+    for (; !S.done;) {
         for (int i = 0; i < batch && launched <= max_iter + 1; ++i, ++launched) {
             HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
             HIPCHECK(ctx, launch_build(P, C, W, s, pf));
