@@ -877,7 +877,9 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     int launched = 0;
     int batch = 2;
     LmState& S = h_state;
-    if (!pf && ctx->hprog) {
+    // (landmark shards keep the batch loop: every rank must enqueue the same number of iterations,
+    // since each one issues collectives, and the progress loop's count depends on host timing)
+    if (!pf && ctx->hprog && !W.comm.on()) {
         // Unprofiled: keep LM_AHEAD iterations in flight and follow the device through the host-mapped
         // progress word (n_decide | done << 31, written by every decision) instead of synchronising the
         // stream per batch: the GPU never waits for the host, and at most LM_AHEAD - 1 iterations are
