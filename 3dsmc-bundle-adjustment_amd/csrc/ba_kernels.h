@@ -271,6 +271,9 @@ struct Prof {
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
+// solve start: x and candidate slots <- prepared initial parameters, LM state <- st0
+hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
+                        const double* K0, int n_cams, int n_points, hipStream_t s);
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_factor(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf);
 // back-substitution, candidate evaluation, step scalars and the LM decision (k_final fuses k_lm_decide)

@@ -22,6 +22,7 @@
 // stored Jacobian blocks; DESIGN.md "Roofline").
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -2109,6 +2110,26 @@ hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevW
     const int nt = 6 * P.nac + 3 * P.n_ap + 4;
     PL(K_SCALE, k_scale, dim3(nblocks(nt, TPB)), dim3(TPB), 0, s, P, W.camdata, W.cnp, W.lin, jacobi, W.scale);
     return hipSuccess;
+}
+
+// Start of a solve: both parameter slots from the prepared initial values, and the fresh LM state
+// (one launch instead of six copies and a host-to-device state copy).
+__global__ __launch_bounds__(TPB) void k_reset(DevProblem P, LmState st0, LmState* __restrict__ st,
+                                               const double* __restrict__ cams0, const double* __restrict__ pts0,
+                                               const double* __restrict__ K0, int ncd, int npd) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    if (t < ncd) { const double v = cams0[t]; P.cams[0][t] = v; P.cams[1][t] = v; }
+    if (t < npd) { const double v = pts0[t]; P.pts[0][t] = v; P.pts[1][t] = v; }
+    if (t < 4) { const double v = K0[t]; P.K[0][t] = v; P.K[1][t] = v; }
+    if (t == 0) *st = st0;
+}
+
+hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
+                        const double* K0, int n_cams, int n_points, hipStream_t s) {
+    const int ncd = 7 * n_cams, npd = 3 * n_points;
+    hipLaunchKernelGGL(k_reset, dim3(nblocks(std::max({ncd, npd, 4}), TPB)), dim3(TPB), 0, s, P, st0, W.st, cams0, pts0,
+                       K0, ncd, npd);
+    return hipGetLastError();
 }
 
 hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {

@@ -831,26 +831,20 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     DevWork& W = ctx->W;
     const BaConsts& C = ctx->C;
     hipStream_t s = ctx->stream;
-    // start from the parameters of the last ba_prepare() (device-to-device)
-    HIPCHECK(ctx, hipMemcpyAsync(P.cams[0], ctx->buf[B_CAMS_INIT].p, sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(ctx, hipMemcpyAsync(P.cams[1], ctx->buf[B_CAMS_INIT].p, sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(ctx, hipMemcpyAsync(P.pts[0], ctx->buf[B_PTS_INIT].p, sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(ctx, hipMemcpyAsync(P.pts[1], ctx->buf[B_PTS_INIT].p, sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(ctx, hipMemcpyAsync(P.K[0], ctx->buf[B_K_INIT].p, sizeof(double) * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(ctx, hipMemcpyAsync(P.K[1], ctx->buf[B_K_INIT].p, sizeof(double) * 4, hipMemcpyDeviceToDevice, s));
     const int max_iter = std::max(o.max_num_iterations, 0);
     HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (max_iter + 2)));
     W.log = ctx->buf[B_LOG].as<double>();
     static thread_local LmState h_state;  // host staging (outlives the async copies)
     h_state = fresh_state(o, o.initial_trust_region_radius);
-    HIPCHECK(ctx, hipMemcpyAsync(W.st, &h_state, sizeof(LmState), hipMemcpyHostToDevice, s));
+    // start from the parameters of the last ba_prepare() (device-to-device) and a fresh state
+    HIPCHECK(ctx, launch_reset(P, W, h_state, ctx->buf[B_CAMS_INIT].as<double>(), ctx->buf[B_PTS_INIT].as<double>(),
+                               ctx->buf[B_K_INIT].as<double>(), p->n_cams, p->n_points, s));
     sum->num_obs_admissible = ctx->n_adm_all;
     sum->num_active_cams = P.nac;
     sum->num_active_points = P.n_ap;
     sum->reduced_system_size = P.n;
     sum->linear_solver = P.solver;
     sum->camera_band = P.cam_band;
-    HIPCHECK(ctx, hipStreamSynchronize(s));
     const double tl0 = now_ms();
     sum->time_setup_ms = tl0 - t0;
     double kms0[K_COUNT];
