@@ -469,6 +469,19 @@ __device__ void trsm_t_lanes(const double* L, const double* rd, double* Y) {
     __syncthreads();
 }
 
+// agent-scope (sc1) 8-byte payload store / load of the in-launch hand-offs (below)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void st_pub(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_pub(const double* p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Border rows B_i (4 x 60, S rows kb..kb+3 at the block's columns) -> LDS Bl[4][BB]
 // (zero past the last dof); one element per thread, issued with the block's other loads.
 __device__ __forceinline__ double border_load(const DevProblem& P, const double* __restrict__ S, int i, int e) {
@@ -489,7 +502,7 @@ __device__ __forceinline__ void border_partial(const double* Bl, const double* Y
         red[t] = acc;
     }
     __syncthreads();
-    if (t < 20) Bp[(size_t)i * 32 + t] = ((red[4 * t] + red[4 * t + 1]) + red[4 * t + 2]) + red[4 * t + 3];
+    if (t < 20) st_pub(Bp + (size_t)i * 32 + t, ((red[4 * t] + red[4 * t + 1]) + red[4 * t + 2]) + red[4 * t + 3]);
 }
 
 struct ElimLds {
@@ -777,25 +790,25 @@ __global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ 
 
 // ---- border: every workgroup sums the border partials in block order and solves the
 // 4x4 system C' y_k = b' (C' = S_kk - B^T V, b' = b_k - B^T u); workgroup i then writes
-// y_a = u - V y_k for the rows of block i into rhs (workgroup 0 also y_k).
+// y_a = u - V y_k for the rows of block i into rhs (workgroup 0 also y_k) and applies the camera
+// step of its cameras (was k_update_cams): lanes < BCR_CAMS, workgroup 0 also the intrinsics; one
+// partial per workgroup of the step scalars for k_final. PUB: inside k_bcr_split, after every
+// block's back-substitution flag, so Bp and Y are read with sc1 loads; bk = [b_k | S_kk packed].
 static constexpr int TPB_BD = 64;
-// Fused camera update (was k_update_cams): lanes < BCR_CAMS of workgroup i apply the step of the block's
-// cameras from the y rows it just produced, workgroup 0 also the intrinsics; one partial per workgroup
-// of the step scalars for k_final.
-__global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict__ st, DevProblem P,
-                                                       double* __restrict__ rhs, BcrWork Bw, int* __restrict__ flag,
-                                                       BaConsts c, const double* __restrict__ scale,
-                                                       const double* __restrict__ camdata,
-                                                       const double* __restrict__ lin, double* __restrict__ delta,
-                                                       double* __restrict__ part) {
-    if (skip_step(st)) return;
-    __shared__ double red[20];
-    __shared__ double yk[4];
-    __shared__ double ybl[G_DOF];
+template <bool PUB>
+__device__ __forceinline__ void border_apply(const LmState* __restrict__ st, const DevProblem& P, double* __restrict__ rhs,
+                                             const BcrWork& Bw, int* __restrict__ flag, const BaConsts& c,
+                                             const double* __restrict__ scale, const double* __restrict__ camdata,
+                                             const double* __restrict__ lin, double* __restrict__ delta,
+                                             double* __restrict__ part, int i, const double* bk, double* red,
+                                             double* yk, double* ybl) {
     const int tid = threadIdx.x;
     if (tid < 20) {
         double acc = 0.0;
-        for (int b = 0; b < Bw.nblk; ++b) acc += Bw.Bp[(size_t)b * 32 + tid];
+        for (int b = 0; b < Bw.nblk; ++b) {
+            const double* q = Bw.Bp + (size_t)b * 32 + tid;
+            acc += PUB ? ld_pub(q) : *q;
+        }
         red[tid] = acc;
     }
     __syncthreads();
@@ -804,11 +817,11 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
         int q = 0;
         for (int mm = 0; mm < 4; ++mm)
             for (int l = 0; l <= mm; ++l, ++q) {
-                const double v = Bw.bk[4 + q];
+                const double v = bk[4 + q];
                 Cm[mm * 4 + l] = v - red[mm * 5 + 1 + l];
                 Cm[l * 4 + mm] = v - red[l * 5 + 1 + mm];
             }
-        for (int mm = 0; mm < 4; ++mm) bp[mm] = Bw.bk[mm] - red[mm * 5];
+        for (int mm = 0; mm < 4; ++mm) bp[mm] = bk[mm] - red[mm * 5];
         bool bad = false;
         double Lm[16] = {0};
         for (int j = 0; j < 4; ++j) {
@@ -834,20 +847,23 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
             z[r] = v / Lm[r * 4 + r];
         }
         for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
-        if (bad && blockIdx.x == 0) *flag = 1;
+        if (bad && i == 0) *flag = 1;
     }
     __syncthreads();
-    const int i = blockIdx.x;
     const int b0 = i * G_DOF, nd = 6 * P.nac;
     if (tid < G_DOF && b0 + tid < nd) {
         const double* y = Bw.Y + (size_t)i * RSZ + tid * RC;
-        const double ya = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
+        double yv[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) yv[k] = PUB ? ld_pub(y + k) : y[k];
+        const double ya = yv[0] - (yv[1] * yk[0] + yv[2] * yk[1] + yv[3] * yk[2] + yv[4] * yk[3]);
         rhs[b0 + tid] = ya;
         ybl[tid] = ya;
     }
     if (i == 0 && tid < 4) rhs[P.kb + tid] = yk[tid];
-    if (i == 0 && tid == 0) Bw.flags[0] += 1;  // next call's epoch (k_bcr_persist)
+    if (i == 0 && tid == 0) Bw.flags[0] += 1;  // next call's epoch (persistent / split kernels)
     __syncthreads();
+    if (tid >= 64) return;  // the camera step is wave 0's
     const int cur = st->cur;
     const double radius = st->radius;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
@@ -867,6 +883,18 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
         part[PART_UPD_XN2 * P.part_stride + i] = acc[3];
     }
 }
+__global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict__ st, DevProblem P,
+                                                       double* __restrict__ rhs, BcrWork Bw, int* __restrict__ flag,
+                                                       BaConsts c, const double* __restrict__ scale,
+                                                       const double* __restrict__ camdata,
+                                                       const double* __restrict__ lin, double* __restrict__ delta,
+                                                       double* __restrict__ part) {
+    if (skip_step(st)) return;
+    __shared__ double red[20];
+    __shared__ double yk[4];
+    __shared__ double ybl[G_DOF];
+    border_apply<false>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, blockIdx.x, Bw.bk, red, yk, ybl);
+}
 
 // ---- persistent path: one resident workgroup per block for the whole solve -------------------
 // Workgroup i keeps D_i -> Cf_i and [A_l | A_r | R] -> [XL | XR | x] in LDS from its first load to
@@ -880,17 +908,6 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
 // behind which ONE lane stores the flag; ONE lane polls (relaxed, s_sleep), the others read after a
 // barrier. Flags hold the call epoch (flags[0] + 1; k_bcr_border advances flags[0]), so nothing is
 // reset per call. Every spin is bounded: a timeout raises chol_flag and the step is rejected.
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned gu32;
-
-__device__ __forceinline__ void st_pub(double* p, double v) {
-    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_pub(const double* p) {
-    return __longlong_as_double(
-        (long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 __device__ __forceinline__ void publish_flag(unsigned* f, unsigned epoch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
@@ -1146,6 +1163,7 @@ struct HLds {
     double Bl[4 * BB];
     double red[80];
     double yl[RSZ], yr[RSZ], yt[RSZ];
+    double bk[16], bred[20], byk[4], bybl[G_DOF];  // fused border: S_kk / b_k, sums, y_k, the block's y rows
     int ok;
     int pre;  // next panel's flags already set (prefetch)
 };
@@ -1166,6 +1184,26 @@ __device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok, const u
         *lds_ok = ok;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    return *lds_ok != 0;
+}
+// Wave 0 polls every block's flag (lane j: blocks j, j + 64, ...; relaxed, bounded); uniform result.
+// The payload behind these flags is read with sc1 loads only (ld_pub), so no acquire fence.
+__device__ bool wait_all_eq(const unsigned* f, int n, unsigned epoch, int* lds_ok) {
+    if (threadIdx.x < 64) {
+        int ok = 1;
+        for (int j = threadIdx.x; j < n && ok; j += 64) {
+            unsigned cnt = 0;
+            while (__hip_atomic_load((gu32*)const_cast<unsigned*>(f + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                   epoch) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++cnt > SPIN_LIMIT) { ok = 0; break; }
+            }
+        }
+        ok = __all(ok);
+        if (threadIdx.x == 0) *lds_ok = ok;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
     __syncthreads();
     return *lds_ok != 0;
 }
@@ -1239,9 +1277,13 @@ __device__ __forceinline__ HelperMap helper_map(int role, int wave, bool root) {
 
 template <bool STAMP, int NH>
 __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__ st, DevProblem P,
-                                                     const double* __restrict__ S, const double* __restrict__ rhs,
+                                                     const double* __restrict__ S, double* __restrict__ rhs,
                                                      BcrWork Bw, int* __restrict__ flag,
-                                                     unsigned long long* __restrict__ tl) {
+                                                     unsigned long long* __restrict__ tl, BaConsts c,
+                                                     const double* __restrict__ scale,
+                                                     const double* __restrict__ camdata,
+                                                     const double* __restrict__ lin, double* __restrict__ delta,
+                                                     double* __restrict__ part) {
     if (skip_step(st)) return;
     TLS(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1426,6 +1468,20 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const bool roleB = NH == 1 || role == 2;  // owns XR, the fill and the back-substitution
     if (root && roleA) return;                // the root has only the x columns (helper B)
     HLds& L = *reinterpret_cast<HLds*>(smem);
+    if (roleB && tid < 14) {  // border inputs [b_k | S_kk packed], read before the border overwrites rhs
+        int q = tid - 4, mm = 0;
+        while (q > mm) { q -= mm + 1; ++mm; }
+        L.bk[tid] = tid < 4 ? rhs[P.kb + tid] : S[(size_t)(P.kb + mm) * ld + P.kb + q];
+    }
+    // fused border (was k_bcr_border): after this block's back-substitution flag, wait for every
+    // block's, then solve the border redundantly and apply the block's camera step
+    auto border = [&]() {
+        if (!wait_all_eq(back_f, nblk, epoch, &L.ok)) {
+            if (tid == 0) *flag = 1;
+            return;
+        }
+        border_apply<true>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, i, L.bk, L.bred, L.byk, L.bybl);
+    };
     {
         const bool has_r0 = i + 1 < nblk;
         if (mi == 0) {
@@ -1725,6 +1781,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         border_partial(L.Bl, Yl, L.red, i, Bw.Bp);
         publish_flag(back_f + i, epoch);
         TLS(14);
+        border();
         return;
     }
 #pragma unroll
@@ -1806,6 +1863,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     border_partial(L.Bl, L.yt, L.red, i, Bw.Bp);
     publish_flag(back_f + i, epoch);
     TLS(14);
+    border();
 }
 #undef TLS
 static_assert(PANEL_DOUBLES <= BCR_BLOCK_DOUBLES, "published panels fit the block's workspace");
@@ -1835,14 +1893,13 @@ static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& 
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
     if (Bw.persist >= 2) {
+        // the border solve and the camera step run inside the split kernel (no k_bcr_border launch)
         if (Bw.persist == 3)
             BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 2>), dim3(3 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
-                Bw, W.chol_flag, stamps);
+                Bw, W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
         else
             BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 1>), dim3(2 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
-                Bw, W.chol_flag, stamps);
-        BPL(K_BCR_BORDER, k_bcr_border, dim3(nblk), dim3(TPB_BD), 0, s, W.st, P, W.rhs, Bw, W.chol_flag, c, W.scale,
-            W.camdata, W.lin, W.delta, W.part);
+                Bw, W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
         return hipSuccess;
     }
     if (Bw.persist) {
