@@ -795,22 +795,30 @@ __global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ 
 // partial per workgroup of the step scalars for k_final. PUB: inside k_bcr_split, after every
 // block's back-substitution flag, so Bp and Y are read with sc1 loads; bk = [b_k | S_kk packed].
 static constexpr int TPB_BD = 64;
+static constexpr int BP_CHUNK = 32;  // border partials staged in LDS per round (20 doubles per block)
 template <bool PUB>
 __device__ __forceinline__ void border_apply(const LmState* __restrict__ st, const DevProblem& P, double* __restrict__ rhs,
                                              const BcrWork& Bw, int* __restrict__ flag, const BaConsts& c,
                                              const double* __restrict__ scale, const double* __restrict__ camdata,
                                              const double* __restrict__ lin, double* __restrict__ delta,
                                              double* __restrict__ part, int i, const double* bk, double* red,
-                                             double* yk, double* ybl) {
+                                             double* yk, double* ybl, double* bpl) {
     const int tid = threadIdx.x;
-    if (tid < 20) {
-        double acc = 0.0;
-        for (int b = 0; b < Bw.nblk; ++b) {
-            const double* q = Bw.Bp + (size_t)b * 32 + tid;
-            acc += PUB ? ld_pub(q) : *q;
+    // sum of the blocks' border partials in block order: BP_CHUNK blocks' partials are loaded by all
+    // threads at once into LDS (one round trip), then lanes < 20 add them in order
+    double bsum = 0.0;
+    for (int b0 = 0; b0 < Bw.nblk; b0 += BP_CHUNK) {
+        const int nb = Bw.nblk - b0 < BP_CHUNK ? Bw.nblk - b0 : BP_CHUNK;
+        for (int e = tid; e < 20 * nb; e += blockDim.x) {
+            const double* q = Bw.Bp + (size_t)(b0 + e / 20) * 32 + e % 20;
+            bpl[e] = PUB ? ld_pub(q) : *q;
         }
-        red[tid] = acc;
+        __syncthreads();
+        if (tid < 20)
+            for (int b = 0; b < nb; ++b) bsum += bpl[20 * b + tid];
+        __syncthreads();
     }
+    if (tid < 20) red[tid] = bsum;
     __syncthreads();
     if (tid == 0) {
         double Cm[16], bp[4];
@@ -893,7 +901,9 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
     __shared__ double red[20];
     __shared__ double yk[4];
     __shared__ double ybl[G_DOF];
-    border_apply<false>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, blockIdx.x, Bw.bk, red, yk, ybl);
+    __shared__ double bpl[20 * BP_CHUNK];
+    border_apply<false>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, blockIdx.x, Bw.bk, red, yk, ybl,
+                        bpl);
 }
 
 // ---- persistent path: one resident workgroup per block for the whole solve -------------------
@@ -1164,6 +1174,7 @@ struct HLds {
     double red[80];
     double yl[RSZ], yr[RSZ], yt[RSZ];
     double bk[16], bred[20], byk[4], bybl[G_DOF];  // fused border: S_kk / b_k, sums, y_k, the block's y rows
+    double bpl[20 * 32];                            // fused border: staged partials (BP_CHUNK blocks)
     int ok;
     int pre;  // next panel's flags already set (prefetch)
 };
@@ -1480,7 +1491,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             if (tid == 0) *flag = 1;
             return;
         }
-        border_apply<true>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, i, L.bk, L.bred, L.byk, L.bybl);
+        border_apply<true>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, i, L.bk, L.bred, L.byk, L.bybl,
+                           L.bpl);
     };
     {
         const bool has_r0 = i + 1 < nblk;

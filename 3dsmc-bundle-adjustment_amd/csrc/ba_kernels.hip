@@ -1720,8 +1720,8 @@ __device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, co
                                const double* __restrict__ scal, double* __restrict__ log);
 // scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]; then the LM decision (k_lm_decide's
 // body, fused: one launch less per iteration)
-// 16 waves: the ~2k back-substitution partials x 5 slots take 2 load rounds per thread instead of 8
-static constexpr int TPB_F = 1024, NW_F = TPB_F / 64;
+// 4 waves (16 measured 1 us slower at C4: more waves to start and to reduce than loads saved)
+static constexpr int TPB_F = 256, NW_F = TPB_F / 64;
 __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                                int nblk_bs, const double* __restrict__ part,
                                                const int* __restrict__ chol_flag, double* __restrict__ scal,
