@@ -415,6 +415,64 @@ __device__ __forceinline__ void group_sum(double (&v)[NV]) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
 }
+// ---------------------------------------------------------------- envelope assembly
+// One workgroup per envelope tile of S (16x16, one element per thread): every element is written once —
+// the camera blocks s U s + D^2 (lower), the border s C s_k, the intrinsics block and the pad identity
+// (rank 0; the landmark shards of other ranks contribute zeros), zero elsewhere — and the diagonal tiles
+// write their 16 rows of rhs; resets the factorisation flag.
+__device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st, int t,
+                         const int2* __restrict__ tiles, const double* __restrict__ camdata,
+                         const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
+                         double* __restrict__ rhs, int* __restrict__ chol_flag) {
+    const int2 ij = tiles[t];
+    const int tid = threadIdx.x;
+    const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
+    const int nd = 6 * P.nac, kb = P.kb;
+    const double* sk = scale + P.off_k;
+    double v = 0.0;
+    if (P.rank == 0) {
+        const double radius = st->radius;
+        if (r < nd && col <= r && r / 6 == col / 6) {
+            const int ac = r / 6, i = col - 6 * ac, j = r - 6 * ac;
+            const int q = 6 * i - i * (i - 1) / 2 + (j - i);
+            const double* sc = scale + 6 * ac;
+            v = sc[i] * camdata[(size_t)ac * CAMDATA + q] * sc[j];
+            if (i == j) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
+        } else if (r >= kb && r < kb + 4 && col < nd) {
+            const int m = r - kb, ac = col / 6, i = col - 6 * ac;
+            v = scale[6 * ac + i] * camdata[(size_t)ac * CAMDATA + 21 + i * 4 + m] * sk[m];
+        } else if (r >= kb && r < kb + 4 && col >= kb && col <= r) {
+            const int m = col - kb, l = r - kb;
+            const int q = 4 * m - m * (m - 1) / 2 + (l - m);
+            v = sk[m] * lin[2 + q] * sk[l];
+            if (l == m) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
+        } else if (r == col && r >= P.n) {
+            v = 1.0;
+        }
+    }
+    S[(size_t)r * P.npad + col] = v;
+    if (ij.x == ij.y && tid < 16) {
+        const int rr = 16 * ij.x + tid;
+        double b = 0.0;
+        if (P.rank == 0) {
+            if (rr < nd) b = scale[rr] * camdata[(size_t)(rr / 6) * CAMDATA + 45 + rr % 6];
+            else if (rr < kb + 4) b = sk[rr - kb] * lin[12 + rr - kb];
+        }
+        rhs[rr] = b;
+    }
+    if (t == 0 && tid == 0) *chol_flag = 0;
+}
+// Standalone assembly (windows without active points; otherwise these tiles are extra workgroups of
+// k_point_prep, and k_schur_tile's last workgroup adds the points' intrinsics Schur terms).
+__global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                      const int2* __restrict__ tiles, const double* __restrict__ camdata,
+                                                      const double* __restrict__ lin, const double* __restrict__ scale,
+                                                      double* __restrict__ S, double* __restrict__ rhs,
+                                                      int* __restrict__ chol_flag) {
+    if (skip_step(st)) return;
+    env_tile(P, c, st, blockIdx.x, tiles, camdata, lin, scale, S, rhs, chol_flag);
+}
+
 // Point tail of the Schur preparation, from the point's sums acc = V packed (6) | e (3) | Kt (12):
 // gradient max-norm term, scaled + LM-damped V~, G = chol(V~)^-1, e~, K~, D~ -> rec[PDATA]; with
 // want_kk also the intrinsics Schur terms -Zk Zk^T (10 packed), -Zk ze (4) -> kk.
@@ -485,14 +543,23 @@ __device__ __forceinline__ void point_tail(const DevProblem& P, const BaConsts& 
         for (int m = 0; m < 4; ++m) kk[10 + m] = -(Zk[m * 3 + 0] * ze[0] + Zk[m * 3 + 1] * ze[1] + Zk[m * 3 + 2] * ze[2]);
     }
 }
+// Workgroups >= nb_pp assemble the envelope tiles of S (env_tile; independent of the point records),
+// so the assembly needs no launch of its own.
 template <int PP_LANES>
 __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c, const LmState* __restrict__ st, int mode,
                                                        const double* __restrict__ scale, double* __restrict__ cnp,
                                                        double* __restrict__ pdata, double* __restrict__ S,
-                                                       double* __restrict__ rhs, double* __restrict__ part) {
+                                                       double* __restrict__ rhs, double* __restrict__ part, int nb_pp,
+                                                       const int2* __restrict__ tiles,
+                                                       const double* __restrict__ camdata,
+                                                       const double* __restrict__ lin, int* __restrict__ chol_flag) {
     __shared__ double lds[4 * 14];
     __shared__ double out[14];
     __shared__ double red[4];
+    if ((int)blockIdx.x >= nb_pp) {
+        if (!skip_step(st)) env_tile(P, c, st, blockIdx.x - nb_pp, tiles, camdata, lin, scale, S, rhs, chol_flag);
+        return;
+    }
     if (st->done) return;
     const int cur = st->cur;
     const double radius = st->radius;
@@ -576,7 +643,7 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
     block_sum<14>(kk, lds, out);
     gmax = block_max(gmax, red);
     bad = block_max(bad, red);
-    // intrinsics terms: one partial per workgroup, summed in a fixed order by k_env_assemble (a
+    // intrinsics terms: one partial per workgroup, summed in a fixed order by k_schur_tile's last workgroup (a
     // same-address f64 atomic per workgroup serialises at ~45 ns each: 391 x 14 of them cost ~17 us)
     if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + blockIdx.x] = out[threadIdx.x];
     if (threadIdx.x == 0) {
@@ -767,9 +834,31 @@ template <bool STAMP>
 __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
-                                                    double* __restrict__ rhs, unsigned long long* __restrict__ stamps) {
+                                                    double* __restrict__ rhs, unsigned long long* __restrict__ stamps,
+                                                    int nblk_pt, const double* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     if (skip_step(st)) return;
+    if ((int)blockIdx.x == P.n_tiles) {
+        // last workgroup: S_kk += the points' intrinsics Schur terms (k_point_prep's per-workgroup partials,
+        // fixed order), rhs_k likewise. No tile writes S_kk or rhs_k.
+        double acc[14];
+#pragma unroll
+        for (int q = 0; q < 14; ++q) acc[q] = 0.0;
+        for (int i = threadIdx.x; i < nblk_pt; i += TPB)
+#pragma unroll
+            for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + i];
+        block_sum<14>(acc, Mt, Mt + 64);
+        const double* out = Mt + 64;
+        if (threadIdx.x < 10) {
+            int m = 0, q = threadIdx.x;
+            while (q >= 4 - m) { q -= 4 - m; ++m; }
+            const int l = m + q;  // packed (m, l), l >= m
+            S[(size_t)(P.kb + l) * P.npad + P.kb + m] += out[threadIdx.x];
+        } else if (threadIdx.x < 14) {
+            rhs[P.kb + threadIdx.x - 10] += out[threadIdx.x];
+        }
+        return;
+    }
     unsigned long long t_prev = 0, st_acc[4] = {0, 0, 0, 0};
 #define SCH_STAMP(k)                                          \
     do {                                                      \
@@ -1649,71 +1738,6 @@ __global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st
 // block and the pad identity (rank 0; the landmark shards of other ranks contribute zeros),
 // zero elsewhere — and the diagonal tiles write their 16 rows of rhs. Replaces k_env_zero +
 // k_assemble + the chol_flag memset (same values as k_assemble, element for element).
-__global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, const LmState* __restrict__ st,
-                                                      const int2* __restrict__ tiles, const double* __restrict__ camdata,
-                                                      const double* __restrict__ lin, const double* __restrict__ scale,
-                                                      double* __restrict__ S, double* __restrict__ rhs,
-                                                      int* __restrict__ chol_flag, int nblk_pt,
-                                                      const double* __restrict__ part) {
-    __shared__ double lds[4 * 14];
-    __shared__ double kko[14];
-    if (skip_step(st)) return;
-    const int2 ij = tiles[blockIdx.x];
-    const int tid = threadIdx.x;
-    const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
-    const int nd = 6 * P.nac, kb = P.kb;
-    // tiles meeting the intrinsics block (rows/cols kb..kb+3; it can straddle two tile rows) add the
-    // points' intrinsics Schur terms: k_point_prep's per-workgroup partials, summed in a fixed order
-    // (identical in every such tile). This was k_pp_reduce (one launch less per LM iteration).
-    const bool kk_tile = 16 * ij.x + 15 >= kb && 16 * ij.x < kb + 4 && 16 * ij.y + 15 >= kb && 16 * ij.y < kb + 4;
-    if (kk_tile) {  // uniform per workgroup
-        double acc[14];
-#pragma unroll
-        for (int q = 0; q < 14; ++q) acc[q] = 0.0;
-        for (int i = tid; i < nblk_pt; i += TPB)
-#pragma unroll
-            for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + i];
-        block_sum<14>(acc, lds, kko);
-    }
-    const double* sk = scale + P.off_k;
-    double v = 0.0;
-    if (P.rank == 0) {
-        const double radius = st->radius;
-        if (r < nd && col <= r && r / 6 == col / 6) {
-            const int ac = r / 6, i = col - 6 * ac, j = r - 6 * ac;
-            const int q = 6 * i - i * (i - 1) / 2 + (j - i);
-            const double* sc = scale + 6 * ac;
-            v = sc[i] * camdata[(size_t)ac * CAMDATA + q] * sc[j];
-            if (i == j) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
-        } else if (r >= kb && r < kb + 4 && col < nd) {
-            const int m = r - kb, ac = col / 6, i = col - 6 * ac;
-            v = scale[6 * ac + i] * camdata[(size_t)ac * CAMDATA + 21 + i * 4 + m] * sk[m];
-        } else if (r >= kb && r < kb + 4 && col >= kb && col <= r) {
-            const int m = col - kb, l = r - kb;
-            const int q = 4 * m - m * (m - 1) / 2 + (l - m);
-            v = sk[m] * lin[2 + q] * sk[l];
-            if (l == m) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
-        } else if (r == col && r >= P.n) {
-            v = 1.0;
-        }
-    }
-    if (kk_tile && r >= kb && r < kb + 4 && col >= kb && col <= r) {
-        const int m = col - kb, l = r - kb;
-        v += kko[4 * m - m * (m - 1) / 2 + (l - m)];
-    }
-    S[(size_t)r * P.npad + col] = v;
-    if (ij.x == ij.y && tid < 16) {
-        const int rr = 16 * ij.x + tid;
-        double b = 0.0;
-        if (P.rank == 0) {
-            if (rr < nd) b = scale[rr] * camdata[(size_t)(rr / 6) * CAMDATA + 45 + rr % 6];
-            else if (rr < kb + 4) b = sk[rr - kb] * lin[12 + rr - kb];
-        }
-        if (kk_tile && rr >= kb && rr < kb + 4) b += kko[10 + rr - kb];
-        rhs[rr] = b;
-    }
-    if (blockIdx.x == 0 && tid == 0) *chol_flag = 0;
-}
 
 // ---------------------------------------------------------------- final
 __device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
@@ -2061,11 +2085,16 @@ int pp_parts(const DevProblem& P) { return P.n_ap > 0 ? pp_blocks(P.n_ap) : 0; }
 
 static hipError_t launch_point_prep(const DevProblem& P, const BaConsts& c, int mode, DevWork& W, hipStream_t s, Prof* pf) {
     const int kid = mode == 0 ? K_POINT_COLNORM : K_POINT_PREP;
-    const dim3 g(pp_blocks(P.n_ap)), b(PP_TPB);
+    const int nb = pp_blocks(P.n_ap);
+    const int n_env = mode == 1 ? W.n_env : 0;  // mode 1: the envelope tiles of S ride along
+    const dim3 g(nb + n_env), b(PP_TPB);
     switch (pp_lanes()) {
-        case 1: PL(kid, k_point_prep<1>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part); break;
-        case 2: PL(kid, k_point_prep<2>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part); break;
-        default: PL(kid, k_point_prep<4>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part); break;
+        case 1: PL(kid, k_point_prep<1>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
+                   W.env_tile, W.camdata, W.lin, W.chol_flag); break;
+        case 2: PL(kid, k_point_prep<2>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
+                   W.env_tile, W.camdata, W.lin, W.chol_flag); break;
+        default: PL(kid, k_point_prep<4>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
+                    W.env_tile, W.camdata, W.lin, W.chol_flag); break;
     }
     return hipSuccess;
 }
@@ -2144,10 +2173,13 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     // point records + intrinsics Schur partials, then the envelope of S: clear + camera / intrinsics
     // blocks, LM diagonal, pad (rank 0 only), the points' intrinsics terms, rhs, chol_flag
     if (P.n_ap > 0)
-        CK(launch_point_prep(P, c, 1, W, s, pf));
-    PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin, W.scale,
-       W.S, W.rhs, W.chol_flag, pp_parts(P), W.part);
-    if (P.n_tiles > 0)
+        CK(launch_point_prep(P, c, 1, W, s, pf));  // + the envelope tiles
+    else
+        PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin,
+           W.scale, W.S, W.rhs, W.chol_flag);
+    // Schur tiles + one workgroup for the intrinsics Schur terms (when there are points)
+    const int n_sch = P.n_tiles + (P.n_ap > 0 ? 1 : 0);
+    if (n_sch > 0)
     {
         static int smode = -1;
         static unsigned long long* sst = nullptr;
@@ -2162,8 +2194,8 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                 CK(hipMalloc(&sst, sizeof(unsigned long long) * 4 * P.n_tiles));
                 scap = P.n_tiles;
             }
-            PL(K_SCHUR_TILE, k_schur_tile<true>, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
-               sst);
+            PL(K_SCHUR_TILE, k_schur_tile<true>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
+               sst, pp_parts(P), W.part);
             std::vector<unsigned long long> h((size_t)4 * P.n_tiles);
             CK(hipMemcpyAsync(h.data(), sst, sizeof(h[0]) * h.size(), hipMemcpyDeviceToHost, s));
             CK(hipStreamSynchronize(s));
@@ -2176,8 +2208,8 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             fprintf(stderr, "schur_tile %d tiles, mean cycles/tile: zero %.0f phaseA %.0f phaseB %.0f flush %.0f | max total %.0f\n",
                     P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
         } else {
-            PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(P.n_tiles), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
-               W.rhs, (unsigned long long*)nullptr);
+            PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
+               W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part);
         }
     }
     if (P.n_ovf_obs > 0)

@@ -400,7 +400,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         }
     };
     {
-        const int slots = schur_tile_slots();
+        const int slots = schur_tile_slots() - 1;  // one resident slot for the intrinsics-term workgroup
         int tile_pts = 128;
         if (slots > 0) tile_pts = std::max(CHUNK_PTS, (int)((cls[0].size() + slots - 1) / slots));
         const char* e = std::getenv("MIBA_TILE_PTS");
