@@ -415,19 +415,140 @@ __device__ __forceinline__ void group_sum(double (&v)[NV]) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
 }
+// Camera ac's value v (of CAMDATA) summed over its sub-segment partials, in sub-segment order.
+__device__ __forceinline__ double cam_sum(const DevProblem& P, const double* __restrict__ cpart, int ac, int v) {
+    const int2 r = P.ac_seg[ac];
+    double acc = 0.0;
+    for (int sg0 = r.x; sg0 < r.y; sg0 += 4) {  // 4 loads in flight, added in segment order
+        double t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = sg0 + k < r.y ? cpart[(size_t)(sg0 + k) * CAMDATA + v] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (sg0 + k < r.y) acc += t[k];
+    }
+    return acc;
+}
+// The camera's share of the gradient max-norm ||x - Plus(x, -g)||_inf (Ceres 2.0 trust_region_minimizer).
+__device__ __forceinline__ double cam_gmax(const DevProblem& P, int cur, int ac, const double* g) {
+    const double* x = P.cams[cur] + 7 * P.ac_cam[ac];
+    double ng[6], tp[7];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) ng[d] = -g[d];
+    se3_plus(x, ng, tp);
+    double gm = 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) gm = fmax(gm, fabs(x[j] - tp[j]));
+    return gm;
+}
+// Max-accumulate a non-negative double (its bit pattern orders like its value).
+__device__ __forceinline__ void atomic_max_nonneg(double* p, double v) {
+    atomicMax((unsigned long long*)p, (unsigned long long)__double_as_longlong(v));
+}
+// The intrinsics partials of all sub-segments in a fixed order (strided per thread, then block_sum).
+__device__ void intr_sums(const DevProblem& P, const double* __restrict__ seg_intr, double* lds, double* out) {
+    double acc[SEGINTR];
+#pragma unroll
+    for (int i = 0; i < SEGINTR; ++i) acc[i] = 0.0;
+    for (int sg = threadIdx.x; sg < P.n_seg; sg += TPB)
+#pragma unroll
+        for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)sg * SEGINTR + i];
+    block_sum<SEGINTR>(acc, lds, out);
+}
+// From the summed intrinsics partials out[SEGINTR] and the IntrinsicsPrior block (OptimizationUtils.cpp:
+// 117-125, squared loss): lin16[0] = cost, lin16[2..12) = Ukk packed (+ prior), lin16[12..16) = gk (+ prior);
+// returns the intrinsics' gradient max-norm term.
+__device__ double intr_lin(const DevProblem& P, const BaConsts& c, const double* K, const double* out, double* lin16) {
+    double pc = 0.0, gm = 0.0;
+    double gk[4];
+    for (int m = 0; m < 4; ++m) {
+        const double fk = c.sw_k * (P.prior[m] - K[m]);
+        pc += fk * fk;
+        gk[m] = out[10 + m] + (-c.sw_k) * fk;
+        gm = fmax(gm, fabs(K[m] - (K[m] + -gk[m])));
+    }
+    lin16[0] = out[14] + 0.5 * pc;
+    for (int q = 0; q < 10; ++q) lin16[2 + q] = out[q];
+    int q = 0;
+    for (int m = 0; m < 4; ++m)
+        for (int l = m; l < 4; ++l, ++q)
+            if (l == m) lin16[2 + q] += c.sw_k * c.sw_k;
+    for (int m = 0; m < 4; ++m) lin16[12 + m] = gk[m];
+    return gm;
+}
+
 // ---------------------------------------------------------------- envelope assembly
 // One workgroup per envelope tile of S (16x16, one element per thread): every element is written once —
 // the camera blocks s U s + D^2 (lower), the border s C s_k, the intrinsics block and the pad identity
 // (rank 0; the landmark shards of other ranks contribute zeros), zero elsewhere — and the diagonal tiles
 // write their 16 rows of rhs; resets the factorisation flag.
+// fin (unsharded LM loop): the camera-side sums are finished here instead of in k_cam_finalize. Each
+// tile sums the sub-segment partials of the (<= 4) cameras its elements need, in sub-segment order; the
+// diagonal tile holding a camera's first dof stores camdata and max-accumulates the camera's gradient
+// term into lin[1]; the intrinsics tiles sum the intrinsics partials and the diagonal one holding row kb
+// stores lin. Same values every iteration until the next linearisation. With stop (the terminal
+// stop_next iteration) only lin[0] / lin[1] are produced, for the decision.
 __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st, int t,
                          const int2* __restrict__ tiles, const double* __restrict__ camdata,
                          const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
-                         double* __restrict__ rhs, int* __restrict__ chol_flag) {
+                         double* __restrict__ rhs, int* __restrict__ chol_flag, int fin,
+                         const double* __restrict__ cpart, const double* __restrict__ seg_intr, double* camdata_w,
+                         double* lin_w) {
+    __shared__ double cds[4 * CAMDATA];
+    __shared__ double l16[LIN_N];
+    __shared__ double ilds[4 * SEGINTR];
+    __shared__ double io[SEGINTR];
     const int2 ij = tiles[t];
     const int tid = threadIdx.x;
     const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
     const int nd = 6 * P.nac, kb = P.kb;
+    const bool stop = st->stop_next;
+    int ac0 = 0;
+    const double* cd = camdata;  // camera values: row ac at cd + (ac - ac0) * CAMDATA
+    const double* linr = lin;
+    if (fin) {
+        const int r0 = 16 * ij.x, c0 = 16 * ij.y;
+        const bool diag = ij.x == ij.y;
+        const bool brd = r0 + 15 >= kb && r0 < kb + 4;  // tile holds intrinsics rows
+        // cameras this tile needs: of its rows (diagonal tiles: camera blocks + rhs), of its columns (border
+        // rows), else of rows and columns both (a camera block straddling two tile rows)
+        const int rlo = r0 / 6, rhi = r0 < nd ? min(r0 + 15, nd - 1) / 6 : -1;
+        const int clo = c0 / 6, chi = c0 < nd ? min(c0 + 15, nd - 1) / 6 : -1;
+        int lo = 0, hi = -1;
+        if (diag) { lo = rlo; hi = rhi; }
+        else if (brd) { lo = clo; hi = chi; }
+        else { lo = max(rlo, clo); hi = min(rhi, chi); }
+        if (hi < lo) { lo = 0; hi = -1; }
+        const int ncam = hi - lo + 1;
+        for (int e = tid; e < ncam * CAMDATA; e += TPB) cds[e] = cam_sum(P, cpart, lo + e / CAMDATA, e % CAMDATA);
+        const bool kk_any = brd && c0 + 15 >= kb && c0 < kb + 4;
+        if (kk_any) intr_sums(P, seg_intr, ilds, io);  // (barriers inside; uniform per tile)
+        __syncthreads();
+        const int cur = st->cur;
+        if (diag) {  // cameras whose first dof lies in this tile's rows
+            for (int e = tid; e < ncam * CAMDATA; e += TPB) {
+                const int ac = lo + e / CAMDATA;
+                if (6 * ac >= r0 && !stop) camdata_w[(size_t)ac * CAMDATA + e % CAMDATA] = cds[e];
+            }
+            if (tid < ncam && 6 * (lo + tid) >= r0)
+                atomic_max_nonneg(lin_w + 1, cam_gmax(P, cur, lo + tid, cds + tid * CAMDATA + 45));
+        }
+        if (kk_any) {
+            if (tid == 0) {
+                const double gm = intr_lin(P, c, P.K[cur], io, l16);
+                if (diag && r0 <= kb && kb < r0 + 16) {
+                    lin_w[0] = l16[0];
+                    for (int q = 2; q < LIN_N; ++q) lin_w[q] = l16[q];
+                    atomic_max_nonneg(lin_w + 1, gm);
+                }
+            }
+            __syncthreads();
+            linr = l16;
+        }
+        ac0 = lo;
+        cd = cds;
+    }
+    if (stop) return;
     const double* sk = scale + P.off_k;
     double v = 0.0;
     if (P.rank == 0) {
@@ -436,15 +557,15 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
             const int ac = r / 6, i = col - 6 * ac, j = r - 6 * ac;
             const int q = 6 * i - i * (i - 1) / 2 + (j - i);
             const double* sc = scale + 6 * ac;
-            v = sc[i] * camdata[(size_t)ac * CAMDATA + q] * sc[j];
+            v = sc[i] * cd[(size_t)(ac - ac0) * CAMDATA + q] * sc[j];
             if (i == j) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
         } else if (r >= kb && r < kb + 4 && col < nd) {
             const int m = r - kb, ac = col / 6, i = col - 6 * ac;
-            v = scale[6 * ac + i] * camdata[(size_t)ac * CAMDATA + 21 + i * 4 + m] * sk[m];
+            v = scale[6 * ac + i] * cd[(size_t)(ac - ac0) * CAMDATA + 21 + i * 4 + m] * sk[m];
         } else if (r >= kb && r < kb + 4 && col >= kb && col <= r) {
             const int m = col - kb, l = r - kb;
             const int q = 4 * m - m * (m - 1) / 2 + (l - m);
-            v = sk[m] * lin[2 + q] * sk[l];
+            v = sk[m] * linr[2 + q] * sk[l];
             if (l == m) v += fmin(fmax(v, c.min_diag), c.max_diag) / radius;
         } else if (r == col && r >= P.n) {
             v = 1.0;
@@ -455,8 +576,8 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
         const int rr = 16 * ij.x + tid;
         double b = 0.0;
         if (P.rank == 0) {
-            if (rr < nd) b = scale[rr] * camdata[(size_t)(rr / 6) * CAMDATA + 45 + rr % 6];
-            else if (rr < kb + 4) b = sk[rr - kb] * lin[12 + rr - kb];
+            if (rr < nd) b = scale[rr] * cd[(size_t)(rr / 6 - ac0) * CAMDATA + 45 + rr % 6];
+            else if (rr < kb + 4) b = sk[rr - kb] * linr[12 + rr - kb];
         }
         rhs[rr] = b;
     }
@@ -468,9 +589,13 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
                                                       const int2* __restrict__ tiles, const double* __restrict__ camdata,
                                                       const double* __restrict__ lin, const double* __restrict__ scale,
                                                       double* __restrict__ S, double* __restrict__ rhs,
-                                                      int* __restrict__ chol_flag) {
-    if (skip_step(st)) return;
-    env_tile(P, c, st, blockIdx.x, tiles, camdata, lin, scale, S, rhs, chol_flag);
+                                                      int* __restrict__ chol_flag, int fin,
+                                                      const double* __restrict__ cpart,
+                                                      const double* __restrict__ seg_intr, double* camdata_w,
+                                                      double* lin_w) {
+    if (st->done || (!fin && st->stop_next)) return;
+    env_tile(P, c, st, blockIdx.x, tiles, camdata, lin, scale, S, rhs, chol_flag, fin, cpart, seg_intr, camdata_w,
+             lin_w);
 }
 
 // Point tail of the Schur preparation, from the point's sums acc = V packed (6) | e (3) | Kt (12):
@@ -552,12 +677,17 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
                                                        double* __restrict__ rhs, double* __restrict__ part, int nb_pp,
                                                        const int2* __restrict__ tiles,
                                                        const double* __restrict__ camdata,
-                                                       const double* __restrict__ lin, int* __restrict__ chol_flag) {
+                                                       const double* __restrict__ lin, int* __restrict__ chol_flag,
+                                                       int fin, const double* __restrict__ cpart,
+                                                       const double* __restrict__ seg_intr, double* camdata_w,
+                                                       double* lin_w) {
     __shared__ double lds[4 * 14];
     __shared__ double out[14];
     __shared__ double red[4];
     if ((int)blockIdx.x >= nb_pp) {
-        if (!skip_step(st)) env_tile(P, c, st, blockIdx.x - nb_pp, tiles, camdata, lin, scale, S, rhs, chol_flag);
+        if (!st->done && (fin || !st->stop_next))
+            env_tile(P, c, st, blockIdx.x - nb_pp, tiles, camdata, lin, scale, S, rhs, chol_flag, fin, cpart, seg_intr,
+                     camdata_w, lin_w);
         return;
     }
     if (st->done) return;
@@ -2087,14 +2217,15 @@ static hipError_t launch_point_prep(const DevProblem& P, const BaConsts& c, int 
     const int kid = mode == 0 ? K_POINT_COLNORM : K_POINT_PREP;
     const int nb = pp_blocks(P.n_ap);
     const int n_env = mode == 1 ? W.n_env : 0;  // mode 1: the envelope tiles of S ride along
+    const int fin = W.comm.on() ? 0 : 1;         // unsharded: they also finish the camera-side sums
     const dim3 g(nb + n_env), b(PP_TPB);
     switch (pp_lanes()) {
         case 1: PL(kid, k_point_prep<1>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
-                   W.env_tile, W.camdata, W.lin, W.chol_flag); break;
+                   W.env_tile, W.camdata, W.lin, W.chol_flag, fin, W.camdata_part, W.seg_intr, W.camdata, W.lin); break;
         case 2: PL(kid, k_point_prep<2>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
-                   W.env_tile, W.camdata, W.lin, W.chol_flag); break;
+                   W.env_tile, W.camdata, W.lin, W.chol_flag, fin, W.camdata_part, W.seg_intr, W.camdata, W.lin); break;
         default: PL(kid, k_point_prep<4>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
-                    W.env_tile, W.camdata, W.lin, W.chol_flag); break;
+                    W.env_tile, W.camdata, W.lin, W.chol_flag, fin, W.camdata_part, W.seg_intr, W.camdata, W.lin); break;
     }
     return hipSuccess;
 }
@@ -2119,8 +2250,11 @@ hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, D
         CK(hipMemsetAsync(W.lin + 1, 0, sizeof(double), s));
     const size_t ncd = (size_t)P.nac * CAMDATA;
     if (!W.comm.on()) {  // camdata_loc == camdata unsharded
-        PL(K_LIN_FINALIZE, k_cam_finalize, dim3(P.nac + 1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part,
-           W.camdata_loc, W.seg_intr, W.lin, 0, (double*)nullptr);
+        // in the LM loop the envelope tiles (k_point_prep / k_env_assemble) finish the camera-side sums;
+        // iteration 0 needs them before the Jacobi scale and the initial state
+        if (!gated)
+            PL(K_LIN_FINALIZE, k_cam_finalize, dim3(P.nac + 1), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part,
+               W.camdata_loc, W.seg_intr, W.lin, 0, (double*)nullptr);
         return hipSuccess;
     }
     // sharded: one all-reduce of [camdata | intrinsics partials] between the local sums and
@@ -2176,7 +2310,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
         CK(launch_point_prep(P, c, 1, W, s, pf));  // + the envelope tiles
     else
         PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin,
-           W.scale, W.S, W.rhs, W.chol_flag);
+           W.scale, W.S, W.rhs, W.chol_flag, W.comm.on() ? 0 : 1, W.camdata_part, W.seg_intr, W.camdata, W.lin);
     // Schur tiles + one workgroup for the intrinsics Schur terms (when there are points)
     const int n_sch = P.n_tiles + (P.n_ap > 0 ? 1 : 0);
     if (n_sch > 0)
