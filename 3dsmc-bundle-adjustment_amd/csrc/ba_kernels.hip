@@ -3,19 +3,19 @@
 // One LM iteration of the reference's ceres::Solve (OptimizationUtils.cpp:300;
 // LM + SPARSE_SCHUR, BundleAdjustmentConfig.h:61-67) is, on the device:
 //
-//   k_cam_side      camera-major pass: per camera  U=Jc^T Jc, C=Jc^T Jk, g=Jc^T f
+//   k_cam_side      camera-major pass: per sub-segment  U=Jc^T Jc, C=Jc^T Jk, g=Jc^T f
 //                   (+ intrinsics JkJk, Jk^T f, cost)  [only after an accepted step]
-//   k_lin_finalize  reduce intrinsics partials, gradient max-norm of cams/intrinsics
-//   k_point_prep    point-major pass: per point V, e, K (scaled, LM-damped), V^-1,
-//                   intrinsics Schur term                           [every iteration]
-//   k_assemble      reduced camera system S = blocks(U + D^2, C, Ukk) and rhs
-//   k_obs_pairs     Schur scatter  S -= W V^-1 W^T, rhs -= W V^-1 e (global f64 atomics)
-//   k_chol          envelope-blocked Cholesky of S + forward/back solve (1 workgroup,
-//                   v_mfma_f64_16x16x4_f64 for the trailing 16x16 tile updates)
-//   k_update_cams   delta = -s*y, Sophus T*exp(delta), camera/intrinsics model-change terms
+//   k_point_prep    point-major pass: per point V, e, K (scaled, LM-damped), V^-1, intrinsics
+//                   Schur partials; extra workgroups assemble the envelope of S (camera blocks
+//                   U + D^2, border C, Ukk, rhs) and finish the camera-side sums  [every iteration]
+//   k_schur_tile    S -= W V^-1 W^T, rhs -= W V^-1 e on f64 MFMA (+ one workgroup: S_kk terms)
+//   k_obs_pairs     the same for overflow points (global f64 atomics)
+//   k_bcr_split     reduced camera system (ba_bcr.hip) + border solve + camera step;
+//                   k_chol_band / k_chol + k_update_cams for short or wide windows
 //   k_backsub_chunk point back-substitution, point model-change terms 0.5(e~^T y + y^T D~ y),
 //                   candidate cost at x + delta
-//   k_final         deterministic reduction of the per-block partials
+//   k_final         deterministic reduction of the per-block partials + the LM decision
+// (k_cam_finalize / k_lin_finalize: iteration 0 and landmark-sharded windows)
 //
 // The residual/Jacobian is never stored: it is recomputed from the 32-byte
 // observation record + the resident pose/point (cheaper than 304 B/obs of
