@@ -49,6 +49,11 @@ static constexpr int RSZ = BB * RC;
 static constexpr int NCONTRIB_WG = 11;  // 44 contribution tiles / 4 waves
 typedef double d4b __attribute__((ext_vector_type(4)));
 
+// chol_flag is raised by several workgroups at once: fetch-or, so a timeout is never overwritten
+__device__ __forceinline__ void raise_flag(int* flag, int bit) {
+    __hip_atomic_fetch_or(flag, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Diagnostic phase stamps (MIBA_BCR_STAMPS=1 launches the STAMP=true variants).
 __device__ __forceinline__ unsigned long long bcr_stamp() {
     unsigned long long t;
@@ -613,7 +618,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_elim(const LmState* __restrict__ 
         d4b none[NCT];
         potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, root ? L.X + 2 * BB : L.X, root ? RC : XC, bad, none, false);
     }
-    if (bad) *flag = 1;
+    if (bad) raise_flag(flag, FLAG_NOT_PD);
     BCR_STAMP(m, 2);
     if (root) {
         // compact the 8 solved columns (stride RC) next to the factor, backward solve
@@ -855,7 +860,7 @@ __device__ __forceinline__ void border_apply(const LmState* __restrict__ st, con
             z[r] = v / Lm[r * 4 + r];
         }
         for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
-        if (bad && i == 0) *flag = 1;
+        if (bad && i == 0) raise_flag(flag, FLAG_NOT_PD);
     }
     __syncthreads();
     const int b0 = i * G_DOF, nd = 6 * P.nac;
@@ -917,13 +922,16 @@ __global__ __launch_bounds__(TPB_BD) void k_bcr_border(const LmState* __restrict
 // (sc1) 8-byte accesses, every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier
 // behind which ONE lane stores the flag; ONE lane polls (relaxed, s_sleep), the others read after a
 // barrier. Flags hold the call epoch (flags[0] + 1; k_bcr_border advances flags[0]), so nothing is
-// reset per call. Every spin is bounded: a timeout raises chol_flag and the step is rejected.
+// reset per call. Every spin is bounded: a timeout raises FLAG_TIMEOUT in chol_flag, which ends the solve
+// with BA_E_INTERNAL (the context then falls back to the per-level launches).
 __device__ __forceinline__ void publish_flag(unsigned* f, unsigned epoch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store((gu32*)f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-static constexpr unsigned SPIN_LIMIT = 1u << 22;
+// polls before a hand-off wait gives up (bcr_set_spin_limit; tests force a tiny bound)
+__device__ unsigned g_spin_limit = 1u << 22;
+#define SPIN_LIMIT g_spin_limit
 // ONE lane polls fa then fb (either may be null); uniform result, false on timeout.
 __device__ bool wait_flags(const unsigned* fa, const unsigned* fb, unsigned epoch, int* lds_ok) {
     if (threadIdx.x == 0) {
@@ -1023,7 +1031,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
         const bool last = m == mi - 1 && !root;
         const bool has_r = i + 2 * s < nblk;  // right coupling at elimination level m + 1 = mi
         if (!wait_flags(a >= 0 ? elim_f + a : nullptr, b < nblk ? elim_f + b : nullptr, epoch, &L.ok)) {
-            if (tid == 0) *flag = 1;
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
         TL(2 + m);
@@ -1069,7 +1077,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
         potrf64_fwd_la<false>(L.T, L.rdiag, L.Wb, L.X + 2 * BB, RC, bad, cacc, false, pst);
     else
         potrf64_fwd_la<true>(L.T, L.rdiag, L.Wb, L.X, XC, bad, cacc, has_r, pst);
-    if (bad) *flag = 1;
+    if (bad) raise_flag(flag, FLAG_NOT_PD);
     TL(10);
     if (root) {
         double* Yl = L.yt;
@@ -1114,7 +1122,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
     TL(13);
     // ---- back-substitution: y_i = u - P y_{i-s} - Q y_{i+s}  (= Cf^-T (x_i - XL y_{i-s} - XR y_{i+s}))
     if (!wait_flags(back_f + (i - s), has_r ? back_f + (i + s) : nullptr, epoch, &L.ok)) {
-        if (tid == 0) *flag = 1;
+        if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
         return;
     }
     TL(12);
@@ -1336,7 +1344,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         for (int m = 0; m < mi; ++m) {
             const int s = 1 << m, a = i - s, b = i + s;
             if (!wait_flags(a >= 0 ? ur_f + a : nullptr, b < nblk ? ul_f + b : nullptr, epoch, &L.ok)) {
-                if (tid == 0) *flag = 1;
+                if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                 return;
             }
             double ua[NQ], ub[NQ];
@@ -1420,7 +1428,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 TLS(16 + 3 * kb);
             }
-            if (bad) *flag = 1;
+            if (bad) raise_flag(flag, FLAG_NOT_PD);
         } else if (wave <= 3) {
             for (int kb = 0; kb + wave <= 3 && kb < 3; ++kb) {
                 if (!spin_ge(0, kb + 1)) { ok = false; break; }
@@ -1471,7 +1479,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 }
             }
         }
-        if (!ok) *flag = 1;
+        if (!ok) raise_flag(flag, FLAG_TIMEOUT);
         return;
     }
     // ================= helpers: panel application, contributions, back-substitution
@@ -1488,7 +1496,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // block's, then solve the border redundantly and apply the block's camera step
     auto border = [&]() {
         if (!wait_all_eq(back_f, nblk, epoch, &L.ok)) {
-            if (tid == 0) *flag = 1;
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
         border_apply<true>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, i, L.bk, L.bred, L.byk, L.bybl,
@@ -1524,13 +1532,13 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         const unsigned* fa = a >= 0 ? ur_f + a : nullptr;
         const unsigned* fb = b < nblk ? ul_f + b : nullptr;
         if (!wait_flags(fa, fb, epoch, &L.ok)) {
-            if (tid == 0) *flag = 1;
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
         if (last && NH == 2) {
             const unsigned* ff = roleA ? (a >= 0 ? fill_f + a : nullptr) : (has_r ? fill_f + b : nullptr);
             if (!wait_flags(ff, nullptr, epoch, &L.ok)) {
-                if (tid == 0) *flag = 1;
+                if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                 return;
             }
         }
@@ -1646,7 +1654,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         if (!have) {
             const bool xl_now = xl_on && roleB && kb >= 2;
             if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok, xl_now ? xl_f + i : nullptr, 4 * epoch + kb - 2)) {
-                if (tid == 0) *flag = 1;
+                if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                 return;
             }
             issue(kb);
@@ -1817,7 +1825,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     if (NH == 2) {
         // last row block of the fill, then F = -XR^T XL; the back-substitution needs all of XL
         if (!wait_ge(xl_f + i, 4 * epoch + 3, &L.ok)) {
-            if (tid == 0) *flag = 1;
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
         for (int e = tid; e < 32 * BB; e += TPB_E) {
@@ -1842,7 +1850,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
     trsm_lower64_t(L.L, L.rdiag, L.X, XW, XC);
     if (!wait_flags(has_l ? back_f + (i - s_i) : nullptr, has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
-        if (tid == 0) *flag = 1;
+        if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
         return;
     }
     TLS(12);
@@ -1956,6 +1964,10 @@ static hipError_t bcr_persist_attr() {
         done = true;
     }
     return hipSuccess;
+}
+
+hipError_t bcr_set_spin_limit(unsigned limit) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &limit, sizeof(limit));
 }
 
 int bcr_persist_ok(int nblk) {

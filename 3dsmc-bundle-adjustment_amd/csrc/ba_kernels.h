@@ -200,7 +200,14 @@ struct LmParams {
     unsigned* progress;  // host-mapped word: n_decide | done << 31 after every decision (nullptr: none)
 };
 enum LmMsg { MSG_NONE = 0, MSG_MAX_ITER, MSG_GRAD_TOL, MSG_MIN_RADIUS, MSG_PARAM_TOL, MSG_FUNC_TOL, MSG_INVALID,
-             MSG_EVAL_FAIL };
+             MSG_EVAL_FAIL, MSG_TIMEOUT };
+// chol_flag bits: the reduced-system factorisation hit a non-positive pivot (a linear-solver failure,
+// Ceres' invalid step), or an inter-workgroup hand-off of the resident BCR kernels timed out (the
+// workgroups were not co-resident: a device-level failure that ends the solve with BA_E_INTERNAL)
+static constexpr int FLAG_NOT_PD = 1;
+static constexpr int FLAG_TIMEOUT = 2;
+// scal[SC_BAD] >= SC_BAD_TIMEOUT: some workgroup's hand-off timed out
+static constexpr double SC_BAD_TIMEOUT = 8.0;
 // per-iteration log row: cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius, accepted
 static constexpr int LOG_W = 8;
 
@@ -270,7 +277,9 @@ struct Prof {
 // fixed launch sequence the host can enqueue without reading anything back.
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf);
+// progress: the host-mapped LM progress word (LmParams::progress), published with the done bit when the
+// initial evaluation is non-finite (nullptr: none)
+hipError_t launch_init_state(const DevProblem& P, DevWork& W, unsigned* progress, hipStream_t s, Prof* pf);
 // solve start: x and candidate slots <- prepared initial parameters, LM state <- st0
 hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
                         const double* K0, int n_cams, int n_points, hipStream_t s);
@@ -284,6 +293,9 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, const 
 // 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);
+// spin bound of the resident BCR kernels' inter-workgroup waits (default 1 << 22 polls; tests force a
+// tiny bound to exercise the timeout path)
+hipError_t bcr_set_spin_limit(unsigned limit);
 // workgroups of k_schur_tile resident at once on the current device (CUs x blocks per CU)
 int schur_tile_slots();
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,

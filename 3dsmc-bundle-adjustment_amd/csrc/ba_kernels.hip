@@ -1913,7 +1913,8 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
         scal[SC_MCC] = out[1];
         scal[SC_CAND] = out[2];
         scal[SC_GMAX_PT] = gm;
-        scal[SC_BAD] = bad + (*chol_flag ? 4.0 : 0.0);
+        const int cf = *chol_flag;
+        scal[SC_BAD] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
         lm_decide_body(st, prm, lin, scal, log);
     }
 }
@@ -1974,9 +1975,12 @@ __global__ __launch_bounds__(TPB) void k_final_shard(DevProblem P, const LmState
     if (threadIdx.x == 0) {
         for (int i = 0; i < 4; ++i) red[i] = out[i];
         red[4] = gm;
-        red[5] = bad;
+        // the factorisation flag is identical on every rank (replicated reduced solve) except for a hand-off
+        // timeout, which is local: both ride the max all-reduce, so every rank takes the same decision
+        const int cf = *chol_flag;
+        red[5] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
         for (int i = 0; i < 4; ++i) red[6 + i] = out[4 + i];
-        red[10] = *chol_flag ? 4.0 : 0.0;
+        red[10] = 0.0;
     }
 }
 __global__ void k_combine(LmState* __restrict__ st, const double* __restrict__ red, double* __restrict__ scal,
@@ -2018,7 +2022,8 @@ __global__ __launch_bounds__(TPB) void k_xnorm_part(DevProblem P, const LmState*
 
 __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* __restrict__ lin,
                                                     LmState* __restrict__ st, double* __restrict__ log,
-                                                    const double* __restrict__ part, int nparts) {
+                                                    const double* __restrict__ part, int nparts,
+                                                    unsigned* progress) {
     __shared__ double lds[4];
     __shared__ double out[1];
     const int cur = st->cur;
@@ -2042,6 +2047,10 @@ __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* 
             st->done = 1;
             st->termination = 2;  // FAILURE
             st->msg = MSG_EVAL_FAIL;
+            // the host follows the progress word: publish the termination (no decision will run)
+            if (progress)
+                __hip_atomic_store(progress, (unsigned)st->n_decide | 0x80000000u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -2091,6 +2100,13 @@ static __device__ void lm_decide_core(LmState* __restrict__ st, const LmParams& 
     if (S.done) { *st = S; return; }
     S.iter += 1;
     double* lg = log + S.iter * LOG_W;
+    if (scal[SC_BAD] >= SC_BAD_TIMEOUT) {  // a BCR hand-off timed out: no valid step; end the solve loudly
+        S.n_unsucc += 1;
+        S.done = 1; S.termination = 2; S.msg = MSG_TIMEOUT;
+        lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
+        *st = S;
+        return;
+    }
     const double mcc = scal[SC_MCC];
     const bool lsf = scal[SC_BAD] >= 2.0;  // linear solver failure (point block or Cholesky not PD)
     const bool valid = !lsf && isfinite(mcc) && mcc > 0.0;
@@ -2295,10 +2311,10 @@ hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, con
     return hipGetLastError();
 }
 
-hipError_t launch_init_state(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
-    const int nparts = nblocks(std::max(P.nac, P.n_ap), TPB);
+hipError_t launch_init_state(const DevProblem& P, DevWork& W, unsigned* progress, hipStream_t s, Prof* pf) {
+    const int nparts = std::max(nblocks(std::max(P.nac, P.n_ap), TPB), 1);
     PL(K_XNORM, k_xnorm_part, dim3(nparts), dim3(TPB), 0, s, P, W.st, W.part);
-    PL(K_XNORM, k_xnorm_init, dim3(1), dim3(TPB), 0, s, P, W.lin, W.st, W.log, W.part, nparts);
+    PL(K_XNORM, k_xnorm_init, dim3(1), dim3(TPB), 0, s, P, W.lin, W.st, W.log, W.part, nparts, progress);
     if (W.comm.on()) COMM(&W.st->xnorm2, &W.st->xnorm2, 1, COMM_F64, COMM_SUM);  // points of all shards
     return hipSuccess;
 }

@@ -86,6 +86,8 @@ struct ba_context {
     int n_tiles = 0, n_ovf_obs = 0, n_tiled_pts = 0;
     int n_adm_all = 0;  // admissible observations over all landmark shards
     int prep_nc = -1, prep_np = -1, prep_no = -1;
+    int last_iter = -1;        // iterations of the last solve (ba_iteration_log rows - 1)
+    bool bcr_fallback = false;  // a resident BCR kernel timed out: per-level launches from then on
     // per-kernel profiling
     Prof prof;
     bool prof_events = false;
@@ -254,6 +256,29 @@ int32_t ba_comm_init(ba_context* ctx, int32_t nranks, int32_t rank, const uint8_
     return BA_OK;
 }
 
+int32_t ba_comm_init_host(ba_context* ctx, int32_t nranks, int32_t rank, ba_allreduce_fn fn, void* user) {
+    if (!ctx) return BA_E_INVALID;
+    if (comm_init_host(ctx->W.comm, nranks, rank, fn, user) != 0) {
+        ctx->err = comm_last_error();
+        return BA_E_INVALID;
+    }
+    ctx->prepared = false;  // the next solve re-prepares with the shard-global structure
+    return BA_OK;
+}
+
+int32_t ba_iteration_log(const ba_context* ctx, double* rows, int32_t max_rows) {
+    if (!ctx || ctx->last_iter < 0 || !ctx->W.log) return 0;
+    const int n = ctx->last_iter + 1;
+    if (rows && max_rows > 0) {
+        const int m = std::min(n, (int)max_rows);
+        if (hipSetDevice(ctx->device) != hipSuccess ||
+            hipMemcpy(rows, ctx->W.log, sizeof(double) * LOG_W * m, hipMemcpyDeviceToHost) != hipSuccess)
+            return 0;
+        for (int i = 0; i < m; ++i) rows[(size_t)i * LOG_W + 7] = 0.0;
+    }
+    return n;
+}
+
 int32_t ba_set_options(ba_context* ctx, const ba_options* opts) {
     if (!ctx || !opts) return BA_E_INVALID;
     if (opts->device >= 0 && opts->device != ctx->device) {
@@ -305,7 +330,6 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         ++cam_cnt[ci];
         ++pt_cnt[pi];
     }
-    if (!verdict[0] && n_adm == 0) { local_err = "no admissible observation (all depths <= 1e-15)"; verdict[0] = 1; }
     if (shard) {
         verdict[1] = nc;
         verdict[2] = -nc;
@@ -649,7 +673,7 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
         Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
         Bw.bk = Bw.rd + (size_t)64 * bcr_nblk;
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
-        Bw.persist = bcr_persist_ok(bcr_nblk);
+        Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
             else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
@@ -676,7 +700,9 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
     BaConsts& C = ctx->C;
     ctx->n_adm_all = n_adm_all;
-    const double N = (double)n_adm_all;  // all shards' admissible observations
+    // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
+    // and the window reduces to the IntrinsicsPrior block, :236-241)
+    const double N = (double)std::max(n_adm_all, 1);
     C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
     C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
     C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
@@ -776,6 +802,7 @@ static void format_message(const LmState& S, char* out, size_t n) {
         case MSG_FUNC_TOL: std::snprintf(out, n, "Function tolerance reached. |cost_change|/cost: %e <= %e", S.msg_a, S.msg_b); break;
         case MSG_INVALID: std::snprintf(out, n, "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d", (int)S.msg_a); break;
         case MSG_EVAL_FAIL: std::snprintf(out, n, "Residual and Jacobian evaluation failed."); break;
+        case MSG_TIMEOUT: std::snprintf(out, n, "Reduced camera solve failed: an inter-workgroup hand-off of the resident BCR kernel timed out."); break;
         default: std::snprintf(out, n, "unknown"); break;
     }
 }
@@ -789,10 +816,22 @@ static void print_row(int it, double cost, double dc, double g, double st, doubl
     std::fflush(stdout);
 }
 
+static int apply_spin_limit(ba_context* ctx) {
+    static unsigned applied = 0;
+    const char* e = std::getenv("MIBA_BCR_SPIN_LIMIT");  // tests: force the hand-off timeout path
+    const unsigned want = e ? (unsigned)std::strtoul(e, nullptr, 10) : (1u << 22);
+    if (want != applied) {
+        HIPCHECK(ctx, bcr_set_spin_limit(want));
+        applied = want;
+    }
+    return BA_OK;
+}
+
 extern "C" int32_t ba_prepare(ba_context* ctx, const ba_problem* p) {
     if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
     miba_maybe_dump_window(p, &ctx->opts);
     HIPCHECK(ctx, hipSetDevice(ctx->device));
+    if (int rc = apply_spin_limit(ctx)) return rc;
     int rc = prepare(ctx, p);
     if (rc) return rc;
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -807,6 +846,7 @@ extern "C" int32_t ba_solve(ba_context* ctx, ba_problem* p, ba_summary* sum) {
     miba_maybe_dump_window(p, &ctx->opts);
     const double t0 = now_ms();
     HIPCHECK(ctx, hipSetDevice(ctx->device));
+    if (int rc = apply_spin_limit(ctx)) return rc;
     int rc = prepare(ctx, p);
     if (rc) return rc;
     return solve_prepared(ctx, p, sum, t0);
@@ -865,44 +905,63 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     // IterationZero: cost, gradient, column norms -> Jacobi scale, |x|
     HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
     HIPCHECK(ctx, launch_scale(P, C, o.jacobi_scaling, W, s, pf));
-    HIPCHECK(ctx, launch_init_state(P, W, s, pf));
-    // LM iterations: fixed launch sequence, device-side decisions; the host only polls
-    // the state once per batch. Iterations enqueued after termination are no-ops.
+    HIPCHECK(ctx, launch_init_state(P, W, ctx->hprog ? ctx->dprog : nullptr, s, pf));
+    // LM iterations: fixed launch sequence, device-side decisions; the host follows the device.
+    // Iterations enqueued after the termination are no-ops (their kernels exit at once).
     int launched = 0;
     int batch = 2;
     LmState& S = h_state;
-    // (landmark shards keep the batch loop: every rank must enqueue the same number of iterations,
-    // since each one issues collectives, and the progress loop's count depends on host timing)
-    if (!pf && ctx->hprog && !W.comm.on()) {
+    const bool shard = W.comm.on();
+    auto launch_iter = [&]() -> int {
+        HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
+        HIPCHECK(ctx, launch_build(P, C, W, s, pf));
+        HIPCHECK(ctx, launch_factor(P, C, W, s, pf));
+        HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
+        ++launched;
+        return BA_OK;
+    };
+    if (!pf && ctx->hprog) {
         // Unprofiled: keep LM_AHEAD iterations in flight and follow the device through the host-mapped
-        // progress word (n_decide | done << 31, written by every decision) instead of synchronising the
-        // stream per batch: the GPU never waits for the host, and at most LM_AHEAD - 1 iterations are
-        // enqueued past the termination (they exit at once).
+        // progress word (n_decide | done << 31, written by every decision and by a failed initial
+        // evaluation) instead of synchronising the stream per batch: the GPU never waits for the host.
+        // When no launch is allowed the host also checks that the stream still runs: an idle or failed
+        // stream without a published decision (a device fault) ends the polling instead of spinning.
         constexpr int LM_AHEAD = 2;
         volatile unsigned* hp = ctx->hprog;
-        for (;;) {
-            const unsigned w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
+        unsigned w = 0;
+        for (unsigned spins = 0;;) {
+            w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
             if ((w >> 31) || launched > max_iter + 1) break;
             if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD) {
-                HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
-                HIPCHECK(ctx, launch_build(P, C, W, s, pf));
-                HIPCHECK(ctx, launch_factor(P, C, W, s, pf));
-                HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
-                ++launched;
+                if (int rc = launch_iter()) return rc;
+            } else if ((++spins & 255u) == 0) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q == hipSuccess) {  // idle: re-read the word once (it is written before the kernel ends)
+                    w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
+                    break;
+                }
+                if (q != hipErrorNotReady) HIPCHECK(ctx, q);
+                std::this_thread::yield();
             } else {
                 std::this_thread::yield();
             }
         }
+        // Landmark shards: every iteration issues collectives, so every rank must enqueue the same number
+        // of iterations. The decisions are identical on all ranks; the host has enqueued between d and
+        // d + LM_AHEAD - 1 iterations when it sees the terminating decision d: pad to d + LM_AHEAD - 1.
+        if (shard && (w >> 31)) {
+            const int target = std::min((int)(w & 0x7fffffffu) + LM_AHEAD - 1, max_iter + 2);
+            while (launched < target)
+                if (int rc = launch_iter()) return rc;
+        }
         HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
         HIPCHECK(ctx, hipStreamSynchronize(s));
     }
+    // profiled (HIP events around every launch) or no host-mapped word: batches of iterations, one
+    // stream synchronisation per batch (the same batch sizes on every landmark shard)
     for (; !S.done;) {
-        for (int i = 0; i < batch && launched <= max_iter + 1; ++i, ++launched) {
-            HIPCHECK(ctx, launch_linearize(P, C, 1, W, s, pf));
-            HIPCHECK(ctx, launch_build(P, C, W, s, pf));
-            HIPCHECK(ctx, launch_factor(P, C, W, s, pf));
-            HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
-        }
+        for (int i = 0; i < batch && launched <= max_iter + 1; ++i)
+            if (int rc = launch_iter()) return rc;
         HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
         HIPCHECK(ctx, hipStreamSynchronize(s));
         flush_prof(ctx);
@@ -919,6 +978,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     sum->num_unsuccessful_steps = S.n_unsucc;
     sum->num_iterations = S.iter;
     sum->termination_type = S.termination;
+    ctx->last_iter = S.iter;
     format_message(S, sum->message, sizeof(sum->message));
     if (o.minimizer_progress_to_stdout) {
         std::vector<double> lg((size_t)LOG_W * (S.iter + 1));
@@ -938,6 +998,19 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     const double t1 = now_ms();
     sum->time_lm_ms = t1 - tl0;
     sum->time_total_ms = t1 - t0;
+    if (S.msg == MSG_TIMEOUT) {
+        // loud failure: the resident BCR kernels' workgroups were not all co-resident (another context or
+        // process held CUs). The flags of the aborted hand-offs are stale: clear them, and run the
+        // per-level launches (no inter-workgroup waits) for every later solve of this context.
+        BcrWork& Bw = W.bcr;
+        if (P.solver == 2 && Bw.flags)
+            HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
+        HIPCHECK(ctx, hipStreamSynchronize(s));
+        Bw.persist = 0;
+        ctx->bcr_fallback = true;
+        ctx->err = std::string(sum->message) + " The context falls back to the per-level BCR launches.";
+        return BA_E_INTERNAL;
+    }
     auto dk = [&](int k) { return ctx->k_ms[k] - kms0[k]; };
     sum->time_linearize_ms = dk(K_CAM_SIDE) + dk(K_LIN_FINALIZE) + dk(K_POINT_COLNORM) + dk(K_SCALE);
     sum->time_schur_ms = dk(K_MEMSET_S) + dk(K_ASSEMBLE) + dk(K_POINT_PREP) + dk(K_SCHUR_TILE) + dk(K_OBS_PAIRS);

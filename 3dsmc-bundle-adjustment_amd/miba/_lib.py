@@ -16,10 +16,14 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libmiba.so")
 EXPORTS = (
     "ba_api_version", "ba_build_info", "ba_default_options", "ba_create", "ba_destroy", "ba_last_error", "ba_set_options",
     "ba_solve", "ba_prepare", "ba_solve_prepared", "ba_kernel_stats", "ba_reset_kernel_stats",
-    "ba_debug_linearize", "ba_debug_reduced_system", "ba_comm_unique_id", "ba_comm_init",
+    "ba_debug_linearize", "ba_debug_reduced_system", "ba_comm_unique_id", "ba_comm_init", "ba_comm_init_host",
+    "ba_iteration_log",
     "ba_problem_write", "ba_problem_read_dims", "ba_problem_read", "ba_bal_read_dims", "ba_bal_read", "ba_bal_write",
 )
 COMM_ID_BYTES = 128  # BA_COMM_ID_BYTES
+LOG_WIDTH = 8  # BA_LOG_WIDTH
+# ba_allreduce_fn: int32 (*)(void* buf, int64 count, int32 dtype, int32 op, void* user)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p)
 
 _lib = None
 
@@ -68,6 +72,10 @@ def lib():
     L.ba_comm_unique_id.restype = C.c_int32
     L.ba_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     L.ba_comm_init.restype = C.c_int32
+    L.ba_comm_init_host.argtypes = [C.c_void_p, C.c_int32, C.c_int32, ALLREDUCE_FN, C.c_void_p]
+    L.ba_comm_init_host.restype = C.c_int32
+    L.ba_iteration_log.argtypes = [C.c_void_p, dp, C.c_int32]
+    L.ba_iteration_log.restype = C.c_int32
     ip = C.POINTER(C.c_int32)
     L.ba_problem_write.argtypes = [C.c_char_p, C.POINTER(BaProblem), C.POINTER(BaOptions)]
     L.ba_problem_read_dims.argtypes = [C.c_char_p, ip, ip, ip]

@@ -41,3 +41,17 @@ def merge_points(prob: ProblemArrays, shard: ProblemArrays, ids: np.ndarray) -> 
     prob.points[ids] = shard.points
     prob.cams[:] = shard.cams
     prob.intr[:] = shard.intr
+
+
+def torch_allreduce(group=None):
+    """Host collective for ``Solver.comm_init_host`` over ``torch.distributed`` (e.g. the gloo backend):
+    reduces the staging array in place."""
+    import torch
+    import torch.distributed as dist
+
+    ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+    def allreduce(arr, op):
+        dist.all_reduce(torch.from_numpy(arr), op=ops[op], group=group)
+
+    return allreduce

@@ -87,6 +87,35 @@ class Solver:
             raise ValueError("unique id must be BA_COMM_ID_BYTES long")
         self._check(self._L.ba_comm_init(self._h, nranks, rank, uid), "ba_comm_init")
 
+    def comm_init_host(self, nranks: int, rank: int, allreduce) -> None:
+        """Make this solver one landmark shard over a host collective instead of RCCL (ba_comm_init_host).
+        ``allreduce(arr, op)`` reduces the numpy array ``arr`` (float64 or int32, a view of libmiba's
+        pinned staging buffer) in place across the ranks; op is "sum", "max" or "min"."""
+        ops = {0: "sum", 1: "max", 2: "min"}
+
+        def fn(buf, count, dtype, op, user):
+            try:
+                ct = C.c_double if dtype == 0 else C.c_int32
+                arr = np.ctypeslib.as_array((ct * int(count)).from_address(buf))
+                allreduce(arr, ops[int(op)])
+                return 0
+            except Exception as e:  # reported through ba_last_error
+                import sys
+                print(f"miba host all-reduce failed: {e!r}", file=sys.stderr)
+                return -1
+
+        self._allreduce_cb = _lib.ALLREDUCE_FN(fn)  # kept alive as long as the context
+        self._check(self._L.ba_comm_init_host(self._h, nranks, rank, self._allreduce_cb, None), "ba_comm_init_host")
+
+    def iteration_log(self) -> np.ndarray:
+        """Per-iteration log of the last solve (ba_iteration_log): rows 0..num_iterations of
+        cost, cost_change, |gradient|, |step|, tr_ratio, tr_radius, accepted (1/0/-1), 0."""
+        n = self._L.ba_iteration_log(self._h, None, 0)
+        rows = np.zeros((max(n, 0), _lib.LOG_WIDTH))
+        if n > 0:
+            self._L.ba_iteration_log(self._h, _dptr(rows), n)
+        return rows
+
     def set_options(self, **changes) -> None:
         for k, v in changes.items():
             setattr(self.options, k, v)

@@ -4,23 +4,30 @@
 Metric (BASELINE.json): "LM iterations/sec + ms/iter at (cams,points,obs)".
 A "step" is one Levenberg-Marquardt iteration of the reference's ceres::Solve
 (OptimizationUtils.cpp:300) over one resident synthetic window. Default
-workload: C4 = 200 cams / 100k points / 1M obs (BASELINE.json configs[3], the
-window the north_star's 1-GPU targets are stated on); --config C2 selects
-configs[1].
+workload: C4 = synthetic.make_config("C4"), 200 cams / 100k points / 1M obs
+(BASELINE.json configs[3], the window the north_star's 1-GPU targets are stated
+on and the window tests/test_converged_parity.py checks); --config C2 / C5
+select configs[1] / configs[4].
 
 Timed region: ba_solve_prepared() with max_num_iterations = K and the
 convergence tolerances disabled, so exactly K LM iterations run on a window
-already resident in HBM (ba_prepare() is outside the timed region).
+already resident in HBM (ba_prepare(), the host structure build + upload, is
+timed separately as setup_ms). Five timed runs after the warmup; value is the
+median (BASELINE.md's protocol).
 
---gpus N (torchrun, one rank per GPU): ONE window landmark-sharded across the N
-ranks (ba_comm_init): the same 200 cameras on every rank and a
-C4-size block of landmarks per rank (N x 100k points, N x 1M obs in total).
-Per iteration the ranks all-reduce (RCCL over xGMI) the camera-side partials,
-the packed envelope of the reduced camera system and the step scalars.
-Weak scaling: value = N x LM iterations/s = landmark-shard iterations per
-second (each GPU advances its C4-size shard by one LM iteration per step),
-timed over the max-over-ranks wall time. --shard runs the same sharded path
-with a 1-rank communicator (its overhead on one GPU).
+--gpus N (torchrun, one rank per GPU, RCCL over xGMI): strong scaling of ONE
+window: the BASELINE window's landmarks are split N ways (miba.shard.
+split_landmarks, balanced by observation count), every rank holds the cameras
+and its landmark block, and per LM iteration the ranks all-reduce the camera-side
+partials, the packed envelope of the reduced camera system and the step scalars
+(SURVEY §8e). value = LM iterations/s of the whole window over the max-over-ranks
+wall time. --weak instead gives every rank a full C4-size landmark block of one
+N-times larger window (same cameras), value = LM iterations/s of that window.
+
+--config C1 / C3 (TUM-size stand-ins, ≈10 / 50 keyframes): latency of the
+reference's per-frame call instead (main.cpp:163-168 re-optimises the same
+window every frame): ms per full ba_solve (prepare + LM to convergence, default
+tolerances) and per ba_solve_prepared re-solve of the resident window.
 """
 from __future__ import annotations
 
@@ -28,6 +35,7 @@ import argparse
 import glob
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -37,11 +45,13 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F64_MFMA_PEAK_TF = 78.6  # MI355X FP64 matrix spec (tools/mfma_f64_rate.hip measures ~73 TF/s sustained)
+TIMED_RUNS = 5
 
 # kernels whose bound is HBM bandwidth (per-observation passes) vs the f64 matrix cores
 HBM_KERNELS = {"cam_side", "cam_reduce", "point_colnorm", "point_prep", "backsub_eval", "lin_finalize", "scale", "assemble",
                "update_cams", "memset_S", "obs_pairs", "final", "xnorm", "comm"}
 JACOBIAN_PASS = "cam_side"  # the roofline.achieved basis (Jacobian pass, J kept in registers)
+NO_TOL = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0, minimizer_progress_to_stdout=0)
 
 
 def parse():
@@ -50,7 +60,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4", choices=["C1", "C2", "C3", "C4", "C5"])
-    ap.add_argument("--cpu-iters", type=int, default=24, help="LM iterations of the CPU oracle sample")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: a C4-size landmark block per rank")
+    ap.add_argument("--cpu-iters", type=int, default=4, help="LM iterations per timed run of the CPU oracle sample")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="timed runs of each CPU leg (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--shard", action="store_true", help="landmark-sharded path even on one GPU")
@@ -60,7 +72,7 @@ def parse():
     return ap.parse_args()
 
 
-PMC_ALIASES = {"bcr_persist": ("bcr_persist", "bcr_split")}  # profiler id -> kernel symbols it times
+PMC_ALIASES = {"bcr_persist": ("bcr_split", "bcr_persist")}  # profiler id -> kernel symbols it times
 
 
 def load_pmc_traffic(kernel: str, config: str):
@@ -90,13 +102,142 @@ def roofline_entry(k: dict, config: str) -> dict:
         e = {"bound": "mfma", "achieved": round(achieved, 4), "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
              "frac": round(achieved / F64_MFMA_PEAK_TF, 5)}
     e["traffic"] = load_pmc_traffic(k["name"], config)
-    e.update(kernel=k["name"], avg_launch_ms=round(avg_ms, 5), launches=k["launches"],
-             bytes_per_launch=k["bytes_per_launch"], flops_per_launch=k["flops_per_launch"])
+    e.update(kernel=("bcr_split" if k["name"] == "bcr_persist" else k["name"]), avg_launch_ms=round(avg_ms, 5),
+             launches=k["launches"], bytes_per_launch=k["bytes_per_launch"], flops_per_launch=k["flops_per_launch"])
     return e
+
+
+def host_info() -> dict:
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:
+        avail = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": avail,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(prob0, args, file_opts) -> dict:
+    """The oracle (CPU restatement of the Ceres 2.0 LM + SPARSE_SCHUR path, NOT Ceres) on a bounded sample
+    of the same window: --cpu-runs timed runs of --cpu-iters LM iterations each (median), at 1 thread (the
+    reference's num_threads default) and at the host threads this process may use."""
+    from oracle import oracle
+    info = host_info()
+    threads_all = max(1, min(int(os.environ.get("OMP_NUM_THREADS") or info["affinity_cpus"] or 1),
+                             info["affinity_cpus"] or 1, oracle.max_threads()))
+    o = oracle.default_options(max_num_iterations=args.cpu_iters, **NO_TOL)
+    if file_opts is not None:
+        for f in ("hub_p_repr", "hub_p_unpr", "weight_intrinsics", "weight_unpr"):
+            setattr(o, f, getattr(file_opts, f))
+    legs = {}
+    for threads in sorted({1, threads_all}):
+        oracle.config(threads=threads, profile=True)
+        its, setups = [], []
+        for _ in range(max(args.cpu_runs, 1)):
+            so = oracle.solve(prob0.copy(), o)
+            its.append(so["num_iterations"] / (so["time_lm_ms"] * 1e-3))
+            setups.append(so["time_setup_ms"])
+        legs[threads] = {"value": round(statistics.median(its), 4), "cores": threads,
+                         "setup_ms": round(statistics.median(setups), 2), "runs": [round(v, 4) for v in its]}
+    oracle.config(1, False)
+    one = legs[1]
+    out = {"value": one["value"], "unit": "LM iterations/s", "cores": 1, "kind": "port",
+           "sample": f"{args.config} window ({prob0.n_cams} cams / {prob0.n_points} points / {prob0.n_obs} obs): "
+                     f"median of {max(args.cpu_runs, 1)} runs x {args.cpu_iters} LM iterations of the f64 C oracle "
+                     f"(CPU restatement of the Ceres 2.0 LM + SPARSE_SCHUR path with a co-visibility profile "
+                     f"Cholesky of the reduced camera system, NOT Ceres; Ceres is not installable here)",
+           "setup_ms": one["setup_ms"], "runs": one["runs"], "host": info}
+    if threads_all > 1:
+        out["all_cores"] = legs[threads_all]
+    return out
+
+
+def time_runs(solver, prob0, steps, runs):
+    """ba_prepare (setup) + ba_solve_prepared of exactly `steps` iterations, `runs` times."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    el, setup, summ = [], [], None
+    solver.set_options(max_num_iterations=steps, profile_kernels=0)
+    for _ in range(runs):
+        prob = prob0.copy()
+        ts = time.perf_counter()
+        solver.prepare(prob)
+        setup.append((time.perf_counter() - ts) * 1e3)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        summ = solver.solve_prepared(prob)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        el.append(t1 - t0)
+    return el, setup, summ
+
+
+def latency_bench(args):
+    """TUM-size windows (C1 / C3 stand-ins): ms per full solve and per re-solve, GPU vs oracle."""
+    import torch
+    from miba import synthetic
+    from miba.solver import Solver
+    from oracle import oracle
+    torch.cuda.set_device(0)
+    prob0 = synthetic.make_config(args.config)
+    opts = dict(minimizer_progress_to_stdout=0)
+    with Solver(device=0, **opts) as s:
+        for _ in range(max(args.warmup, 1)):
+            s.solve(prob0.copy())
+        full, resolve, its = [], [], []
+        for _ in range(max(args.steps, 5)):
+            q = prob0.copy()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sm = s.solve(q)
+            full.append((time.perf_counter() - t0) * 1e3)
+            its.append(sm["num_iterations"])
+        q = prob0.copy()
+        s.prepare(q)
+        for _ in range(max(args.steps, 5)):
+            t0 = time.perf_counter()
+            s.solve_prepared(q)
+            resolve.append((time.perf_counter() - t0) * 1e3)
+    oracle.config(1, True)
+    cpu = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        so = oracle.solve(prob0.copy())
+        cpu.append((time.perf_counter() - t0) * 1e3)
+    oracle.config(1, False)
+    med = statistics.median
+    out = {"metric": "ms per windowOptimize solve (prepare + LM to convergence)", "value": round(med(full), 4),
+           "unit": "ms", "n_gpus": 1, "steps": len(full), "warmup": args.warmup, "ms_per_step": round(med(full), 4),
+           "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": f"{args.config} TUM-size stand-in: {prob0.n_cams} cams / {prob0.n_points} points / "
+                                  f"{prob0.n_obs} obs (synthetic.make_config; real TUM windows need the dataset and "
+                                  f"the OpenCV/OpenGV front-end, absent offline)", "cams": prob0.n_cams,
+                      "points": prob0.n_points, "obs": prob0.n_obs, "parallelism": "single"},
+           "lm_iterations": its[0], "ms_per_resolve_prepared": round(med(resolve), 4),
+           "ms_per_lm_iteration": round(med(full) / max(its[0], 1), 4),
+           "cpu_baseline": {"value": round(med(cpu), 3), "unit": "ms", "cores": 1, "kind": "port",
+                            "sample": f"oracle full solve of the same window ({so['num_iterations']} LM iterations), "
+                                      f"median of 3", "host": host_info()}}
+    print(json.dumps(out), flush=True)
 
 
 def main():
     args = parse()
+    if args.config in ("C1", "C3") and not args.problem:
+        return latency_bench(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -110,25 +251,27 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world)
 
-    from miba import synthetic
+    from miba import shard, synthetic
     from miba.solver import Solver
 
     sharded = world > 1 or args.shard
     file_opts = None
     if args.problem:
-        from miba import problem_io, shard
+        from miba import problem_io
         whole, file_opts = problem_io.load(args.problem)
-        prob = shard.split_landmarks(whole, world, rank)[0] if world > 1 else whole
         args.config = "file"
+    elif args.weak:
+        whole = None
+        prob = synthetic.make_landmark_shard(args.config, rank)  # shard 0 == the single-GPU window's cameras
     else:
-        prob = synthetic.make_landmark_shard(args.config, rank)  # shard 0 == the single-GPU window
+        whole = synthetic.make_config(args.config)
+    if whole is not None:
+        prob = shard.split_landmarks(whole, world, rank)[0] if world > 1 else whole
     prob0 = prob.copy()
 
-    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0,
-                  minimizer_progress_to_stdout=0)
     prof = 0 if args.no_profile else 1
     solver = Solver(file_opts, device=local_rank, profile_kernels=prof, max_num_iterations=max(args.warmup, 1),
-                    **no_tol)
+                    **NO_TOL)
     if sharded:
         box = [Solver.comm_unique_id() if rank == 0 else None]
         if world > 1:
@@ -137,11 +280,12 @@ def main():
     # warmup (untimed, unprofiled: first launches load the code objects)
     if args.warmup > 0:
         solver.set_options(max_num_iterations=args.warmup, profile_kernels=0)
+        prob = prob0.copy()
         solver.prepare(prob)
         solver.solve_prepared(prob)
-        prob = prob0.copy()
     # breakdown run: every kernel launch timed (per-iteration breakdown, dominant kernel)
     solver.set_options(max_num_iterations=5, profile_kernels=prof, profile_mask=0)
+    prob = prob0.copy()
     solver.prepare(prob)
     solver.reset_kernel_stats()
     wsumm = solver.solve_prepared(prob)
@@ -149,19 +293,8 @@ def main():
     names = [k["name"] for k in wstats]
     live = [k for k in wstats if k["launches"] > 0]
     dom = max(live, key=lambda k: k["total_ms"])["name"] if live else None
-    # timed run (no HIP events: event records between dependent launches cost ~5-10 us each)
-    prob = prob0.copy()
-    solver.set_options(max_num_iterations=args.steps, profile_kernels=0)
-    solver.prepare(prob)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    summ = solver.solve_prepared(prob)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
+    # timed runs (no HIP events: event records between dependent launches cost ~5-10 us each)
+    els, setups, summ = time_runs(solver, prob0, args.steps, TIMED_RUNS)
     # the same K-step region again with HIP events around the dominant kernel and the
     # Jacobian pass only: their average launch durations for the roofline
     stats = []
@@ -175,8 +308,8 @@ def main():
         solver.reset_kernel_stats()
         solver.solve_prepared(prob0.copy())
         stats = solver.kernel_stats()
-    elapsed = t1 - t0
     iters = summ["num_iterations"]
+    elapsed = statistics.median(els)
     t = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device="cuda")
     if world > 1:
         tmax = t.clone()
@@ -189,56 +322,48 @@ def main():
         elapsed_max = elapsed
 
     if rank == 0:
-        value = world * iters / elapsed_max
+        value = iters / elapsed_max
         ms_per_step = elapsed_max * 1e3 / max(iters, 1)
         kern = [k for k in stats if k["launches"] > 0]
         roofs = {k["name"]: roofline_entry(k, args.config) for k in kern}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            from oracle import oracle
-            q = prob0.copy()
-            o = oracle.default_options(max_num_iterations=args.cpu_iters, **no_tol)
-            if file_opts is not None:
-                for f in ("hub_p_repr", "hub_p_unpr", "weight_intrinsics", "weight_unpr"):
-                    setattr(o, f, getattr(file_opts, f))
-            tc0 = time.perf_counter()
-            so = oracle.solve(q, o)
-            tc1 = time.perf_counter()
-            cpu = {"value": round(so["num_iterations"] / (so["time_lm_ms"] * 1e-3), 4),
-                   "unit": "LM iterations/s", "cores": 1, "kind": "port",
-                   "sample": f"{args.config} window ({prob0.n_cams} cams / {prob0.n_points} points / {prob0.n_obs} obs), "
-                             f"{so['num_iterations']} LM iterations of the f64 C oracle (CPU restatement of the "
-                             f"Ceres 2.0 LM path, not Ceres; single thread), wall {tc1 - tc0:.1f}s incl. setup"}
+            cpu = cpu_baseline(prob0, args, file_opts)
         wit = max(wsumm["num_iterations"], 1)
-        phases = {k["name"]: round(k["total_ms"] / wit, 4) for k in live}  # warmup run, every kernel timed
+        phases = {k["name"]: round(k["total_ms"] / wit, 4) for k in live}  # breakdown run, every kernel timed
+        n_cams = prob0.n_cams
+        n_pts = whole.n_points if whole is not None else world * prob0.n_points
+        n_obs = whole.n_obs if whole is not None else world * prob0.n_obs
         if args.problem:
-            workload = (f"{os.path.basename(args.problem)}: {prob0.n_cams} cams / {world}x~{prob0.n_points} points / "
-                        f"{world}x~{prob0.n_obs} obs, one window from file"
-                        + (f", landmark-sharded across {world} GPUs" if sharded else ""))
-            par = f"landmark-shard{world}" if sharded else "single"
-        elif sharded:
-            workload = (f"{args.config} landmark shards: {prob0.n_cams} cams / {world}x{prob0.n_points} points / "
-                        f"{world}x{prob0.n_obs} obs, one window landmark-sharded across {world} GPU(s) "
-                        f"(RCCL all-reduce of the reduced camera system per LM iteration)")
-            par = f"landmark-shard{world}"
+            workload = f"{os.path.basename(args.problem)}: {n_cams} cams / {n_pts} points / {n_obs} obs, one window"
         else:
-            workload = f"{args.config}: {prob0.n_cams} cams / {prob0.n_points} points / {prob0.n_obs} obs, one window"
-            par = "single"
+            workload = f"{args.config}: {n_cams} cams / {n_pts} points / {n_obs} obs, one window"
+        if world > 1 and not args.weak:
+            workload += f", landmark-sharded across {world} GPUs (strong scaling, RCCL all-reduce per LM iteration)"
+        elif args.weak:
+            workload = (f"{args.config} landmark blocks: {n_cams} cams / {world}x{prob0.n_points} points / "
+                        f"{world}x{prob0.n_obs} obs, one window with a C4-size landmark block per GPU (weak scaling, "
+                        f"RCCL all-reduce per LM iteration)")
+        elif sharded:
+            workload += ", landmark-sharded path with a 1-rank RCCL communicator"
         out = {
             "metric": "LM iterations/sec",
             "value": round(value, 3),
-            "unit": "LM iterations/s" if world == 1 else "landmark-shard LM iterations/s",
+            "unit": "LM iterations/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "file" if args.problem else "synthetic",
-            "config": {"workload": workload, "cams": prob0.n_cams, "points": world * prob0.n_points,
-                       "obs": world * prob0.n_obs, "parallelism": par},
+            "config": {"workload": workload, "cams": n_cams, "points": n_pts, "obs": n_obs,
+                       "parallelism": f"landmark-shard{world}" if sharded else "single"},
+            "setup_ms": round(statistics.median(setups), 3),
+            "timed_runs": {"n": len(els), "ms_per_step": [round(e * 1e3 / max(iters, 1), 4) for e in els],
+                           "statistic": "median"},
             "roofline": roofs.get(dom),
             "roofline_source": "libmiba HIP events (solver stream) around every launch of the dominant kernel and of "
                                "the Jacobian pass, over a repeat of the timed K-step region",

@@ -178,6 +178,27 @@ int32_t ba_solve_prepared(ba_context* ctx, ba_problem* prob, ba_summary* summary
 int32_t ba_comm_unique_id(uint8_t id[BA_COMM_ID_BYTES]);
 int32_t ba_comm_init(ba_context* ctx, int32_t nranks, int32_t rank, const uint8_t id[BA_COMM_ID_BYTES]);
 
+/* The same landmark sharding over a caller-supplied host collective instead of RCCL (e.g. MPI,
+ * or torch.distributed gloo in the multi-rank tests, where several ranks share one GPU and RCCL
+ * refuses duplicate devices). fn reduces `count` elements of the host buffer `buf` in place across
+ * the ranks and returns 0 on success (dtype BA_DTYPE_*, op BA_OP_*); libmiba calls it on the
+ * thread running ba_solve, at the same points of the LM iteration as the RCCL collectives, with
+ * the device data staged through pinned memory. Local (not collective): every rank calls it once. */
+#define BA_DTYPE_F64 0
+#define BA_DTYPE_I32 1
+#define BA_OP_SUM 0
+#define BA_OP_MAX 1
+#define BA_OP_MIN 2
+typedef int32_t (*ba_allreduce_fn)(void* buf, int64_t count, int32_t dtype, int32_t op, void* user);
+int32_t ba_comm_init_host(ba_context* ctx, int32_t nranks, int32_t rank, ba_allreduce_fn fn, void* user);
+
+/* Per-iteration log of the last solve, the rows Ceres prints with minimizer_progress_to_stdout
+ * (iteration 0 .. num_iterations): cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius,
+ * accepted (1 = successful step, 0 = unsuccessful / invalid, -1 = the step that met a tolerance),
+ * 0. Returns the number of rows available (at most max_rows are written; rows may be NULL). */
+#define BA_LOG_WIDTH 8
+int32_t ba_iteration_log(const ba_context* ctx, double* rows, int32_t max_rows);
+
 /* Per-kernel device timing (requires ba_options.profile_kernels = 1).
  * bytes_per_launch is the ALGORITHMIC traffic model of DESIGN.md §Roofline
  * for the last prepared window (compulsory bytes, each input/output once). */

@@ -31,6 +31,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../include/ba.h"
 
@@ -144,6 +147,44 @@ static void se3_plus(const double* T, const double* d, double* out) {
     out[0] = nx; out[1] = ny; out[2] = nz; out[3] = nw;
 }
 
+
+/* ------------------------------------------------------------------ */
+/* execution knobs of the restatement (not of the reference): OpenMP threads and the
+ * storage of the reduced camera system. threads = 1 and profile = 0 (full lower
+ * triangle, dense Cholesky) is the checker configuration; the CPU baseline leg runs
+ * the profile (skyline) storage — the Ceres SPARSE_SCHUR stand-in, whose fill stays
+ * inside the co-visibility envelope — at 1 and at all host threads.             */
+static int g_threads = 1;
+static int g_profile = 0;
+
+EXPORT void oracle_config(int32_t threads, int32_t profile) {
+    g_threads = threads < 1 ? 1 : threads;
+#ifndef _OPENMP
+    g_threads = 1;
+#endif
+    g_profile = profile ? 1 : 0;
+}
+EXPORT int32_t oracle_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+static inline int tid(void) {
+#ifdef _OPENMP
+    return omp_get_thread_num();
+#else
+    return 0;
+#endif
+}
+/* contiguous chunk [lo, hi) of n items for thread t of T */
+static inline void chunk(int n, int t, int T, int* lo, int* hi) {
+    *lo = (int)((long long)n * t / T);
+    *hi = (int)((long long)n * (t + 1) / T);
+}
+
 /* ------------------------------------------------------------------ */
 /* problem bookkeeping                                                  */
 typedef struct {
@@ -157,11 +198,18 @@ typedef struct {
     int n_act_pts;
     int* pt_ptr;     /* CSR over admissible obs by point */
     int* pt_obs;     /* admissible indices */
+    int max_m;       /* max admissible observations of one point */
     double sw_r, sw_d, sw_k; /* sqrt weights */
+    /* lower profile of the reduced system S (n x n): row i holds columns [fc[i], i]
+     * at a[rp[i] + j - fc[i]]; the 4 intrinsics rows are last and full (arrowhead border) */
+    int* fc;
+    size_t* rp;
+    size_t nnz;
 } orc_t;
 
 static void orc_free(orc_t* c) {
     free(c->adm); free(c->cam_ac); free(c->pt_active); free(c->pt_ptr); free(c->pt_obs);
+    free(c->fc); free(c->rp);
 }
 
 static int orc_init(orc_t* c, const ba_problem* p, const ba_options* o) {
@@ -192,11 +240,41 @@ static int orc_init(orc_t* c, const ba_problem* p, const ba_options* o) {
         c->cam_ac[i] = (cam_has[i] && i != p->fixed_cam) ? c->nac++ : -1;
     free(cam_has);
     c->n = 6 * c->nac + 4;
-    for (int i = 0; i < p->n_points; ++i) { c->pt_ptr[i + 1] += c->pt_ptr[i]; c->n_act_pts += c->pt_active[i]; }
+    for (int i = 0; i < p->n_points; ++i) {
+        c->n_act_pts += c->pt_active[i];
+        const int m = c->pt_ptr[i + 1];
+        if (m > c->max_m) c->max_m = m;
+        c->pt_ptr[i + 1] += c->pt_ptr[i];
+    }
     int* fill = (int*)malloc(sizeof(int) * (p->n_points + 1));
     memcpy(fill, c->pt_ptr, sizeof(int) * (p->n_points + 1));
     for (int a = 0; a < c->n_adm; ++a) c->pt_obs[fill[p->obs_pt[c->adm[a]]]++] = a;
     free(fill);
+    /* profile of S: first co-visible active camera of every active camera */
+    int* fcam = (int*)malloc(sizeof(int) * (c->nac + 1));
+    for (int a = 0; a < c->nac; ++a) fcam[a] = a;
+    for (int pi = 0; pi < p->n_points; ++pi) {
+        int lo = c->nac;
+        for (int q = c->pt_ptr[pi]; q < c->pt_ptr[pi + 1]; ++q) {
+            const int ac = c->cam_ac[p->obs_cam[c->adm[c->pt_obs[q]]]];
+            if (ac >= 0 && ac < lo) lo = ac;
+        }
+        for (int q = c->pt_ptr[pi]; q < c->pt_ptr[pi + 1]; ++q) {
+            const int ac = c->cam_ac[p->obs_cam[c->adm[c->pt_obs[q]]]];
+            if (ac >= 0 && lo < fcam[ac]) fcam[ac] = lo;
+        }
+    }
+    c->fc = (int*)malloc(sizeof(int) * (c->n + 1));
+    c->rp = (size_t*)malloc(sizeof(size_t) * (c->n + 1));
+    size_t off = 0;
+    for (int r = 0; r < c->n; ++r) {
+        c->fc[r] = (g_profile && r < 6 * c->nac) ? 6 * fcam[r / 6] : 0;
+        c->rp[r] = off;
+        off += (size_t)(r - c->fc[r] + 1);
+    }
+    c->rp[c->n] = off;
+    c->nnz = off;
+    free(fcam);
     const double N = (double)c->n_adm;
     c->sw_r = sqrt(1.0 / N);                 /* ReprojectionConstraint weight 1/N (:280) */
     c->sw_d = sqrt(o->weight_unpr / N);      /* DepthPrior weight WEIGHT_UNPR/N (:290) */
@@ -282,22 +360,36 @@ static int lin_alloc(lin_t* L, int n) {
 }
 static void lin_free(lin_t* L) { free(L->f); free(L->jc); free(L->jp); free(L->jk); }
 
-/* Evaluate cost (and Jacobians if L != NULL). Returns 0 ok, -1 non-finite. */
+/* Evaluate cost (and Jacobians if L != NULL). Returns 0 ok, -1 non-finite.
+ * Per-thread partial costs over contiguous observation ranges, summed in thread order. */
 static int evaluate(const orc_t* c, const double* cams, const double* pts, const double* K, lin_t* L,
                     double* cost_out) {
     const ba_problem* p = c->p;
+    const int T = g_threads;
+    double part[T];
+    int badv[T];
+#pragma omp parallel num_threads(T)
+    {
+        const int t = tid();
+        int lo, hi;
+        chunk(c->n_adm, t, T, &lo, &hi);
+        double cost = 0, f[3];
+        int bad = 0;
+        for (int a = lo; a < hi && !bad; ++a) {
+            const int k = c->adm[a];
+            double cb;
+            bad = eval_obs(c, cams + 7 * p->obs_cam[k], pts + 3 * p->obs_pt[k], K, p->obs_uv[2 * k],
+                           p->obs_uv[2 * k + 1], p->obs_depth[k], L ? L->f + 3 * a : f,
+                           L ? L->jc + 18 * a : NULL, L ? L->jp + 9 * a : NULL, L ? L->jk + 8 * a : NULL, &cb);
+            cost += cb;
+        }
+        part[t] = cost;
+        badv[t] = bad;
+    }
     double cost = 0;
-    double f[3], jc[18], jp[9], jk[8];
-    for (int a = 0; a < c->n_adm; ++a) {
-        const int k = c->adm[a];
-        double cb;
-        int st = eval_obs(c, cams + 7 * p->obs_cam[k], pts + 3 * p->obs_pt[k], K, p->obs_uv[2 * k],
-                          p->obs_uv[2 * k + 1], p->obs_depth[k], L ? L->f + 3 * a : f,
-                          L ? L->jc + 18 * a : NULL, L ? L->jp + 9 * a : NULL, L ? L->jk + 8 * a : NULL,
-                          &cb);
-        (void)jc; (void)jp; (void)jk;
-        if (st) return -1;
-        cost += cb;
+    for (int t = 0; t < T; ++t) {
+        if (badv[t]) return -1;
+        cost += part[t];
     }
     /* IntrinsicsPrior (:117-125), squared loss */
     double ck = 0;
@@ -318,44 +410,64 @@ static inline int off_pt(const orc_t* c, int pi) { return 6 * c->nac + 3 * pi; }
 static inline int off_k(const orc_t* c) { return 6 * c->nac + 3 * c->p->n_points; }
 static inline int nloc(const orc_t* c) { return 6 * c->nac + 3 * c->p->n_points + 4; }
 
-/* squared column norms of the (robustified) Jacobian, Ceres SparseMatrix::SquaredColumnNorm */
-static void col_norms(const orc_t* c, const lin_t* L, double* cn) {
+/* Squared column norms of the (robustified) Jacobian (Ceres SparseMatrix::SquaredColumnNorm)
+ * and the gradient g = J^T f (local coords, unscaled), point-major: each point's entries
+ * are owned by one thread, the camera / intrinsics entries are per-thread partials summed
+ * in thread order. Either output may be NULL. */
+static void colnorm_grad(const orc_t* c, const lin_t* L, double* cn, double* g) {
     const ba_problem* p = c->p;
-    memset(cn, 0, sizeof(double) * nloc(c));
-    for (int a = 0; a < c->n_adm; ++a) {
-        const int k = c->adm[a];
-        const int ac = c->cam_ac[p->obs_cam[k]];
-        const double* jc = L->jc + 18 * a;
-        const double* jp = L->jp + 9 * a;
-        const double* jk = L->jk + 8 * a;
-        for (int r = 0; r < 3; ++r) {
-            if (ac >= 0)
-                for (int d = 0; d < 6; ++d) cn[6 * ac + d] += jc[r * 6 + d] * jc[r * 6 + d];
-            for (int i = 0; i < 3; ++i) cn[off_pt(c, p->obs_pt[k]) + i] += jp[r * 3 + i] * jp[r * 3 + i];
-        }
-        for (int r = 0; r < 2; ++r)
-            for (int i = 0; i < 4; ++i) cn[off_k(c) + i] += jk[r * 4 + i] * jk[r * 4 + i];
+    const int T = g_threads, nf = 6 * c->nac + 4;
+    double* pc = (double*)calloc((size_t)T * 2 * nf + 1, sizeof(double)); /* [t][cn | g] camera + intr */
+    if (cn) memset(cn, 0, sizeof(double) * nloc(c));
+    if (g) memset(g, 0, sizeof(double) * nloc(c));
+#pragma omp parallel num_threads(T)
+    {
+        const int t = tid();
+        double* mc = pc + (size_t)t * 2 * nf;
+        double* mg = mc + nf;
+        int lo, hi;
+        chunk(p->n_points, t, T, &lo, &hi);
+        for (int pi = lo; pi < hi; ++pi)
+            for (int q = c->pt_ptr[pi]; q < c->pt_ptr[pi + 1]; ++q) {
+                const int a = c->pt_obs[q];
+                const int ac = c->cam_ac[p->obs_cam[c->adm[a]]];
+                const double* jc = L->jc + 18 * a;
+                const double* jp = L->jp + 9 * a;
+                const double* jk = L->jk + 8 * a;
+                const double* f = L->f + 3 * a;
+                const int op = off_pt(c, pi);
+                for (int r = 0; r < 3; ++r) {
+                    if (ac >= 0)
+                        for (int d = 0; d < 6; ++d) {
+                            mc[6 * ac + d] += jc[r * 6 + d] * jc[r * 6 + d];
+                            mg[6 * ac + d] += jc[r * 6 + d] * f[r];
+                        }
+                    for (int i = 0; i < 3; ++i) {
+                        if (cn) cn[op + i] += jp[r * 3 + i] * jp[r * 3 + i];
+                        if (g) g[op + i] += jp[r * 3 + i] * f[r];
+                    }
+                }
+                for (int r = 0; r < 2; ++r)
+                    for (int i = 0; i < 4; ++i) {
+                        mc[6 * c->nac + i] += jk[r * 4 + i] * jk[r * 4 + i];
+                        mg[6 * c->nac + i] += jk[r * 4 + i] * f[r];
+                    }
+            }
     }
-    for (int i = 0; i < 4; ++i) cn[off_k(c) + i] += c->sw_k * c->sw_k; /* prior: J = -sqrt(w) I */
-}
-
-/* gradient g = J^T f (local coords, unscaled) */
-static void gradient(const orc_t* c, const lin_t* L, double* g) {
-    const ba_problem* p = c->p;
-    memset(g, 0, sizeof(double) * nloc(c));
-    for (int a = 0; a < c->n_adm; ++a) {
-        const int k = c->adm[a];
-        const int ac = c->cam_ac[p->obs_cam[k]];
-        const double* f = L->f + 3 * a;
-        for (int r = 0; r < 3; ++r) {
-            if (ac >= 0)
-                for (int d = 0; d < 6; ++d) g[6 * ac + d] += L->jc[18 * a + r * 6 + d] * f[r];
-            for (int i = 0; i < 3; ++i) g[off_pt(c, p->obs_pt[k]) + i] += L->jp[9 * a + r * 3 + i] * f[r];
+    const int ok = off_k(c);
+    for (int t = 0; t < T; ++t) {
+        const double* mc = pc + (size_t)t * 2 * nf;
+        for (int j = 0; j < nf; ++j) {
+            const int dst = j < 6 * c->nac ? j : ok + (j - 6 * c->nac);
+            if (cn) cn[dst] += mc[j];
+            if (g) g[dst] += mc[nf + j];
         }
-        for (int r = 0; r < 2; ++r)
-            for (int i = 0; i < 4; ++i) g[off_k(c) + i] += L->jk[8 * a + r * 4 + i] * f[r];
     }
-    for (int i = 0; i < 4; ++i) g[off_k(c) + i] += -c->sw_k * L->fk[i];
+    for (int i = 0; i < 4; ++i) {
+        if (cn) cn[ok + i] += c->sw_k * c->sw_k; /* prior: J = -sqrt(w) I */
+        if (g) g[ok + i] += -c->sw_k * L->fk[i];
+    }
+    free(pc);
 }
 
 /* 3x3 SPD inverse via Cholesky; returns -1 if not PD */
@@ -387,18 +499,18 @@ static int inv3_spd(const double V[9], double Vi[9]) {
     return 0;
 }
 
-/* Build (part of) the Jacobi-scaled, LM-damped reduced camera system over the
- * points in [pb, pe) (their observations' camera terms included). The prior and
- * the damping of cameras/intrinsics are added when with_global != 0.
- * S: n*n dense full symmetric (accumulated, caller zeroes), rhs: n.
- * Per point it also stores Vinv (9) and e (3) and Kt (12) for back-substitution
- * if the arrays are non-NULL.  Schur elimination of every point block
- * (Ceres SchurEliminator semantics: E-block = point, F-blocks = poses + intrinsics). */
-static int build_reduced(const orc_t* c, const lin_t* L, const double* scale, const double* D2,
-                         int pb, int pe, int with_global, double* S, double* rhs, double* Vinv_all,
-                         double* e_all, double* Kt_all) {
+/* element (r, cc), cc <= r, of the packed lower profile */
+#define SP(a, r, cc) ((a)[c->rp[(r)] + (size_t)((cc) - c->fc[(r)])])
+
+/* Schur elimination of the points in [pb, pe) into the packed lower profile Sa and rhs
+ * (accumulated): the observations' camera / intrinsics (F-block) terms plus, per point,
+ * -W V~^-1 W^T (Ceres SchurEliminator semantics: E-block = point, F-blocks = poses +
+ * intrinsics). W / Y / rowb are per-thread scratch of c->max_m observations. Per point
+ * it also stores Vinv (9), e (3) and Kt (12) for the back-substitution when non-NULL. */
+static int eliminate_points(const orc_t* c, const lin_t* L, const double* scale, const double* D2, int pb, int pe,
+                            double* Sa, double* rhs, double* Vinv_all, double* e_all, double* Kt_all, double* W,
+                            double* Y, int* rowb) {
     const ba_problem* p = c->p;
-    const int n = c->n;
     const int kb = 6 * c->nac; /* intrinsics rows */
     const double* sk = scale + off_k(c);
     double Vt[9], Vi[9], Kt[12];
@@ -409,6 +521,7 @@ static int build_reduced(const orc_t* c, const lin_t* L, const double* scale, co
         memset(Vt, 0, sizeof(Vt));
         memset(Kt, 0, sizeof(Kt));
         double e[3] = {0, 0, 0};
+        int nw = 0;
         for (int q = c->pt_ptr[pi]; q < c->pt_ptr[pi + 1]; ++q) {
             const int a = c->pt_obs[q];
             const int k = c->adm[a];
@@ -427,29 +540,25 @@ static int build_reduced(const orc_t* c, const lin_t* L, const double* scale, co
                 for (int j = 0; j < 3; ++j) Kt[i * 3 + j] += Jk[i] * Jp[j] + Jk[4 + i] * Jp[3 + j];
             /* camera-side (F-block) terms of this observation */
             for (int i = 0; i < 4; ++i) {
-                for (int j = 0; j <= i; ++j) {
-                    const double v = Jk[i] * Jk[j] + Jk[4 + i] * Jk[4 + j];
-                    S[(kb + i) * n + kb + j] += v;
-                    if (i != j) S[(kb + j) * n + kb + i] += v;
-                }
+                for (int j = 0; j <= i; ++j) SP(Sa, kb + i, kb + j) += Jk[i] * Jk[j] + Jk[4 + i] * Jk[4 + j];
                 rhs[kb + i] += Jk[i] * f[0] + Jk[4 + i] * f[1];
             }
-            if (ac >= 0) {
-                const double* sc = scale + 6 * ac;
-                for (int r = 0; r < 3; ++r)
-                    for (int d = 0; d < 6; ++d) Jc[r * 6 + d] = L->jc[18 * a + r * 6 + d] * sc[d];
-                const int cb = 6 * ac;
-                for (int i = 0; i < 6; ++i) {
-                    for (int j = 0; j < 6; ++j)
-                        S[(cb + i) * n + cb + j] += Jc[i] * Jc[j] + Jc[6 + i] * Jc[6 + j] + Jc[12 + i] * Jc[12 + j];
-                    for (int j = 0; j < 4; ++j) {
-                        const double v = Jc[i] * Jk[j] + Jc[6 + i] * Jk[4 + j];
-                        S[(cb + i) * n + kb + j] += v;
-                        S[(kb + j) * n + cb + i] += v;
-                    }
-                    rhs[cb + i] += Jc[i] * f[0] + Jc[6 + i] * f[1] + Jc[12 + i] * f[2];
-                }
+            if (ac < 0) continue;
+            const double* sc = scale + 6 * ac;
+            for (int r = 0; r < 3; ++r)
+                for (int d = 0; d < 6; ++d) Jc[r * 6 + d] = L->jc[18 * a + r * 6 + d] * sc[d];
+            const int cb = 6 * ac;
+            for (int i = 0; i < 6; ++i) {
+                for (int j = 0; j <= i; ++j)
+                    SP(Sa, cb + i, cb + j) += Jc[i] * Jc[j] + Jc[6 + i] * Jc[6 + j] + Jc[12 + i] * Jc[12 + j];
+                for (int j = 0; j < 4; ++j) SP(Sa, kb + j, cb + i) += Jc[i] * Jk[j] + Jc[6 + i] * Jk[4 + j];
+                rhs[cb + i] += Jc[i] * f[0] + Jc[6 + i] * f[1] + Jc[12 + i] * f[2];
             }
+            /* W = Jc^T Jp (6x3) of this observation */
+            for (int d = 0; d < 6; ++d)
+                for (int i = 0; i < 3; ++i)
+                    W[18 * nw + d * 3 + i] = Jc[d] * Jp[i] + Jc[6 + d] * Jp[3 + i] + Jc[12 + d] * Jp[6 + i];
+            rowb[nw++] = cb;
         }
         /* LM damping of the E block */
         for (int i = 0; i < 3; ++i) Vt[i * 4] += D2[off_pt(c, pi) + i];
@@ -457,28 +566,6 @@ static int build_reduced(const orc_t* c, const lin_t* L, const double* scale, co
         if (Vinv_all) memcpy(Vinv_all + 9 * pi, Vi, sizeof(Vi));
         if (e_all) memcpy(e_all + 3 * pi, e, sizeof(e));
         if (Kt_all) memcpy(Kt_all + 12 * pi, Kt, sizeof(Kt));
-        /* gather F_j: for each obs with active cam, W = Jc^T Jp (6x3); plus Kt (4x3) */
-        const int m = c->pt_ptr[pi + 1] - c->pt_ptr[pi];
-        double* W = (double*)malloc(sizeof(double) * 18 * (m + 1));
-        double* Y = (double*)malloc(sizeof(double) * 18 * (m + 1));
-        int* rowb = (int*)malloc(sizeof(int) * (m + 1));
-        int nw = 0;
-        for (int q = c->pt_ptr[pi]; q < c->pt_ptr[pi + 1]; ++q) {
-            const int a = c->pt_obs[q];
-            const int k = c->adm[a];
-            const int ac = c->cam_ac[p->obs_cam[k]];
-            if (ac < 0) continue;
-            const double* sc = scale + 6 * ac;
-            double Jc[18], Jp[9];
-            for (int r = 0; r < 3; ++r) {
-                for (int d = 0; d < 6; ++d) Jc[r * 6 + d] = L->jc[18 * a + r * 6 + d] * sc[d];
-                for (int i = 0; i < 3; ++i) Jp[r * 3 + i] = L->jp[9 * a + r * 3 + i] * sp[i];
-            }
-            for (int d = 0; d < 6; ++d)
-                for (int i = 0; i < 3; ++i)
-                    W[18 * nw + d * 3 + i] = Jc[d] * Jp[i] + Jc[6 + d] * Jp[3 + i] + Jc[12 + d] * Jp[6 + i];
-            rowb[nw++] = 6 * ac;
-        }
         /* Y = W Vi */
         for (int w = 0; w < nw; ++w)
             for (int d = 0; d < 6; ++d)
@@ -491,71 +578,115 @@ static int build_reduced(const orc_t* c, const lin_t* L, const double* scale, co
             for (int j = 0; j < 3; ++j)
                 YK[i * 3 + j] = Kt[i * 3 + 0] * Vi[j] + Kt[i * 3 + 1] * Vi[3 + j] + Kt[i * 3 + 2] * Vi[6 + j];
         for (int a = 0; a < nw; ++a) {
-            for (int b = 0; b < nw; ++b)
+            /* lower part only: blocks (a, b) with rowb[b] < rowb[a], and the lower half of equal rows */
+            for (int b = 0; b < nw; ++b) {
+                if (rowb[b] > rowb[a]) continue;
                 for (int d = 0; d < 6; ++d)
-                    for (int d2 = 0; d2 < 6; ++d2)
-                        S[(rowb[a] + d) * n + rowb[b] + d2] -=
-                            Y[18 * a + d * 3 + 0] * W[18 * b + d2 * 3 + 0] +
-                            Y[18 * a + d * 3 + 1] * W[18 * b + d2 * 3 + 1] +
-                            Y[18 * a + d * 3 + 2] * W[18 * b + d2 * 3 + 2];
+                    for (int d2 = 0; d2 < 6; ++d2) {
+                        if (rowb[b] == rowb[a] && d2 > d) continue;
+                        SP(Sa, rowb[a] + d, rowb[b] + d2) -= Y[18 * a + d * 3 + 0] * W[18 * b + d2 * 3 + 0] +
+                                                             Y[18 * a + d * 3 + 1] * W[18 * b + d2 * 3 + 1] +
+                                                             Y[18 * a + d * 3 + 2] * W[18 * b + d2 * 3 + 2];
+                    }
+            }
             for (int d = 0; d < 6; ++d) {
-                for (int j = 0; j < 4; ++j) {
-                    const double v = Y[18 * a + d * 3 + 0] * Kt[j * 3 + 0] + Y[18 * a + d * 3 + 1] * Kt[j * 3 + 1] +
-                                     Y[18 * a + d * 3 + 2] * Kt[j * 3 + 2];
-                    S[(rowb[a] + d) * n + kb + j] -= v;
-                    S[(kb + j) * n + rowb[a] + d] -= v;
-                }
+                for (int j = 0; j < 4; ++j)
+                    SP(Sa, kb + j, rowb[a] + d) -= Y[18 * a + d * 3 + 0] * Kt[j * 3 + 0] +
+                                                   Y[18 * a + d * 3 + 1] * Kt[j * 3 + 1] +
+                                                   Y[18 * a + d * 3 + 2] * Kt[j * 3 + 2];
                 rhs[rowb[a] + d] -= Y[18 * a + d * 3 + 0] * e[0] + Y[18 * a + d * 3 + 1] * e[1] +
                                     Y[18 * a + d * 3 + 2] * e[2];
             }
         }
         for (int i = 0; i < 4; ++i) {
-            for (int j = 0; j < 4; ++j)
-                S[(kb + i) * n + kb + j] -=
+            for (int j = 0; j <= i; ++j)
+                SP(Sa, kb + i, kb + j) -=
                     YK[i * 3 + 0] * Kt[j * 3 + 0] + YK[i * 3 + 1] * Kt[j * 3 + 1] + YK[i * 3 + 2] * Kt[j * 3 + 2];
             rhs[kb + i] -= YK[i * 3 + 0] * e[0] + YK[i * 3 + 1] * e[1] + YK[i * 3 + 2] * e[2];
         }
-        free(W); free(Y); free(rowb);
-    }
-    if (with_global) {
-        /* IntrinsicsPrior block: J = -sqrt(w) I (scaled), residual fk */
-        for (int i = 0; i < 4; ++i) {
-            S[(kb + i) * n + kb + i] += c->sw_k * c->sw_k * sk[i] * sk[i];
-            rhs[kb + i] += -c->sw_k * sk[i] * L->fk[i];
-        }
-        for (int ac = 0; ac < c->nac; ++ac)
-            for (int d = 0; d < 6; ++d) S[(6 * ac + d) * n + 6 * ac + d] += D2[6 * ac + d];
-        for (int i = 0; i < 4; ++i) S[(kb + i) * n + kb + i] += D2[off_k(c) + i];
     }
     return bad ? -1 : 0;
 }
 
-/* dense Cholesky S = L L^T in place (lower), then solve for x: returns -1 if not PD */
-static int chol_solve(double* S, int n, double* b) {
-    for (int j = 0; j < n; ++j) {
-        double d = S[j * n + j];
-        for (int k = 0; k < j; ++k) d -= S[j * n + k] * S[j * n + k];
-        if (!(d > 0) || !isfinite(d)) return -1;
-        d = sqrt(d);
-        S[j * n + j] = d;
-        const double id = 1.0 / d;
-        for (int i = j + 1; i < n; ++i) {
-            double s = S[i * n + j];
-            const double* ri = S + i * n;
-            const double* rj = S + j * n;
-            for (int k = 0; k < j; ++k) s -= ri[k] * rj[k];
-            S[i * n + j] = s * id;
+/* Build (part of) the Jacobi-scaled, LM-damped reduced camera system over the points
+ * in [pb, pe): Sa (packed lower profile, c->nnz) and rhs (n) are overwritten. Threads
+ * take contiguous point ranges into private copies, summed in thread order. The prior
+ * and the damping of cameras / intrinsics are added when with_global != 0. */
+static int build_reduced(const orc_t* c, const lin_t* L, const double* scale, const double* D2, int pb, int pe,
+                         int with_global, double* Sa, double* rhs, double* Vinv_all, double* e_all, double* Kt_all) {
+    const int T = g_threads, n = c->n;
+    const size_t m = (size_t)c->max_m + 1, slab = c->nnz + (size_t)n;
+    double* priv = (double*)calloc((size_t)T * slab, sizeof(double));
+    double* scr = (double*)malloc(sizeof(double) * 36 * m * T);
+    int* rowb = (int*)malloc(sizeof(int) * m * T);
+    int badv[T];
+#pragma omp parallel num_threads(T)
+    {
+        const int t = tid();
+        int lo, hi;
+        chunk(pe - pb, t, T, &lo, &hi);
+        double* Sp = priv + (size_t)t * slab;
+        badv[t] = eliminate_points(c, L, scale, D2, pb + lo, pb + hi, Sp, Sp + c->nnz, Vinv_all, e_all, Kt_all,
+                                   scr + 36 * m * t, scr + 36 * m * t + 18 * m, rowb + m * t);
+    }
+    memcpy(Sa, priv, sizeof(double) * c->nnz);
+    memcpy(rhs, priv + c->nnz, sizeof(double) * n);
+    int bad = badv[0];
+    for (int t = 1; t < T; ++t) {
+        const double* Sp = priv + (size_t)t * slab;
+        for (size_t i = 0; i < c->nnz; ++i) Sa[i] += Sp[i];
+        for (int i = 0; i < n; ++i) rhs[i] += Sp[c->nnz + i];
+        bad |= badv[t];
+    }
+    free(priv); free(scr); free(rowb);
+    if (with_global) {
+        const int kb = 6 * c->nac;
+        const double* sk = scale + off_k(c);
+        /* IntrinsicsPrior block: J = -sqrt(w) I (scaled), residual fk */
+        for (int i = 0; i < 4; ++i) {
+            SP(Sa, kb + i, kb + i) += c->sw_k * c->sw_k * sk[i] * sk[i];
+            rhs[kb + i] += -c->sw_k * sk[i] * L->fk[i];
+        }
+        for (int ac = 0; ac < c->nac; ++ac)
+            for (int d = 0; d < 6; ++d) SP(Sa, 6 * ac + d, 6 * ac + d) += D2[6 * ac + d];
+        for (int i = 0; i < 4; ++i) SP(Sa, kb + i, kb + i) += D2[off_k(c) + i];
+    }
+    return bad ? -1 : 0;
+}
+
+/* Row-oriented profile (skyline) Cholesky S = L L^T in place, then L L^T x = b.
+ * Fill stays inside the profile; with fc == 0 it is the dense Cholesky.
+ * Returns -1 if S is not positive definite. */
+static int chol_solve(const orc_t* c, double* a, double* b) {
+    const int n = c->n;
+    for (int i = 0; i < n; ++i) {
+        const int fi = c->fc[i];
+        double* ri = a + c->rp[i] - fi; /* ri[j] = L(i, j), j in [fi, i] */
+        for (int j = fi; j <= i; ++j) {
+            const int fj = c->fc[j];
+            const double* rj = a + c->rp[j] - fj;
+            double s = ri[j];
+            for (int k = fi > fj ? fi : fj; k < j; ++k) s -= ri[k] * rj[k];
+            if (j < i) {
+                ri[j] = s / rj[j];
+            } else {
+                if (!(s > 0) || !isfinite(s)) return -1;
+                ri[i] = sqrt(s);
+            }
         }
     }
     for (int i = 0; i < n; ++i) { /* L z = b */
+        const int fi = c->fc[i];
+        const double* ri = a + c->rp[i] - fi;
         double s = b[i];
-        for (int k = 0; k < i; ++k) s -= S[i * n + k] * b[k];
-        b[i] = s / S[i * n + i];
+        for (int k = fi; k < i; ++k) s -= ri[k] * b[k];
+        b[i] = s / ri[i];
     }
     for (int i = n - 1; i >= 0; --i) { /* L^T x = z */
-        double s = b[i];
-        for (int k = i + 1; k < n; ++k) s -= S[k * n + i] * b[k];
-        b[i] = s / S[i * n + i];
+        const int fi = c->fc[i];
+        const double* ri = a + c->rp[i] - fi;
+        b[i] /= ri[i];
+        for (int k = fi; k < i; ++k) b[k] -= ri[k] * b[i];
     }
     return 0;
 }
@@ -617,15 +748,16 @@ static int compute_step(const orc_t* c, const lin_t* L, const double* scale, con
                         double* step) {
     const int n = c->n;
     const int nl = nloc(c);
+    const ba_problem* p = c->p;
     double* D2 = (double*)malloc(sizeof(double) * nl);
     for (int i = 0; i < nl; ++i) D2[i] = diag[i] / radius; /* lm_diagonal = sqrt(diag / radius) */
-    double* S = (double*)calloc((size_t)n * n, sizeof(double));
-    double* rhs = (double*)calloc(n, sizeof(double));
-    double* Vinv = (double*)malloc(sizeof(double) * 9 * (c->p->n_points + 1));
-    double* e = (double*)malloc(sizeof(double) * 3 * (c->p->n_points + 1));
-    double* Kt = (double*)malloc(sizeof(double) * 12 * (c->p->n_points + 1));
-    int st = build_reduced(c, L, scale, D2, 0, c->p->n_points, 1, S, rhs, Vinv, e, Kt);
-    if (!st) st = chol_solve(S, n, rhs);
+    double* Sa = (double*)malloc(sizeof(double) * (c->nnz + 1));
+    double* rhs = (double*)malloc(sizeof(double) * n);
+    double* Vinv = (double*)malloc(sizeof(double) * 9 * (p->n_points + 1));
+    double* e = (double*)malloc(sizeof(double) * 3 * (p->n_points + 1));
+    double* Kt = (double*)malloc(sizeof(double) * 12 * (p->n_points + 1));
+    int st = build_reduced(c, L, scale, D2, 0, p->n_points, 1, Sa, rhs, Vinv, e, Kt);
+    if (!st) st = chol_solve(c, Sa, rhs);
     if (!st) {
         /* F-part of y */
         memset(step, 0, sizeof(double) * nl);
@@ -633,9 +765,7 @@ static int compute_step(const orc_t* c, const lin_t* L, const double* scale, con
             for (int d = 0; d < 6; ++d) step[6 * ac + d] = rhs[6 * ac + d];
         for (int i = 0; i < 4; ++i) step[off_k(c) + i] = rhs[6 * c->nac + i];
         /* back-substitute points: y_p = Vinv (e - W^T y_c - Kt^T y_k) */
-        const ba_problem* p = c->p;
-        const double* sk = scale + off_k(c);
-        (void)sk;
+#pragma omp parallel for num_threads(g_threads) schedule(static)
         for (int pi = 0; pi < p->n_points; ++pi) {
             if (!c->pt_active[pi]) continue;
             const double* sp = scale + off_pt(c, pi);
@@ -671,29 +801,41 @@ static int compute_step(const orc_t* c, const lin_t* L, const double* scale, con
             step[i] = -step[i];
         }
     }
-    free(D2); free(S); free(rhs); free(Vinv); free(e); free(Kt);
+    free(D2); free(Sa); free(rhs); free(Vinv); free(e); free(Kt);
     return st;
 }
 
-/* model_cost_change = -(J delta)^T (f + J delta / 2)  (ComputeTrustRegionStep) */
+/* model_cost_change = -(J delta)^T (f + J delta / 2)  (ComputeTrustRegionStep);
+ * per-thread partials over contiguous observation ranges, summed in thread order */
 static double model_cost_change(const orc_t* c, const lin_t* L, const double* delta) {
     const ba_problem* p = c->p;
-    double m = 0;
-    for (int a = 0; a < c->n_adm; ++a) {
-        const int k = c->adm[a];
-        const int ac = c->cam_ac[p->obs_cam[k]];
-        const double* dp = delta + off_pt(c, p->obs_pt[k]);
-        const double* dk = delta + off_k(c);
-        for (int r = 0; r < 3; ++r) {
-            double jd = 0;
-            if (ac >= 0)
-                for (int d = 0; d < 6; ++d) jd += L->jc[18 * a + r * 6 + d] * delta[6 * ac + d];
-            for (int i = 0; i < 3; ++i) jd += L->jp[9 * a + r * 3 + i] * dp[i];
-            if (r < 2)
-                for (int i = 0; i < 4; ++i) jd += L->jk[8 * a + r * 4 + i] * dk[i];
-            m += -jd * (L->f[3 * a + r] + jd / 2.0);
+    const int T = g_threads;
+    double part[T];
+#pragma omp parallel num_threads(T)
+    {
+        const int t = tid();
+        int lo, hi;
+        chunk(c->n_adm, t, T, &lo, &hi);
+        double m = 0;
+        for (int a = lo; a < hi; ++a) {
+            const int k = c->adm[a];
+            const int ac = c->cam_ac[p->obs_cam[k]];
+            const double* dp = delta + off_pt(c, p->obs_pt[k]);
+            const double* dk = delta + off_k(c);
+            for (int r = 0; r < 3; ++r) {
+                double jd = 0;
+                if (ac >= 0)
+                    for (int d = 0; d < 6; ++d) jd += L->jc[18 * a + r * 6 + d] * delta[6 * ac + d];
+                for (int i = 0; i < 3; ++i) jd += L->jp[9 * a + r * 3 + i] * dp[i];
+                if (r < 2)
+                    for (int i = 0; i < 4; ++i) jd += L->jk[8 * a + r * 4 + i] * dk[i];
+                m += -jd * (L->f[3 * a + r] + jd / 2.0);
+            }
         }
+        part[t] = m;
     }
+    double m = 0;
+    for (int t = 0; t < T; ++t) m += part[t];
     for (int i = 0; i < 4; ++i) {
         const double jd = -c->sw_k * delta[off_k(c) + i];
         m += -jd * (L->fk[i] + jd / 2.0);
@@ -710,8 +852,23 @@ static void print_row(int it, double cost, double dc, double g, double st, doubl
            t_it, t_tot);
 }
 
+/* Per-iteration trace row (same layout as libmiba's device iteration log, ba_iteration_log):
+ * cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius, accepted (1 / 0 / -1 = the
+ * terminating tolerance step), 0 */
+#define TRACE_W 8
+typedef struct {
+    double* rows;
+    int max_rows;
+} trace_t;
+static void trace_row(trace_t* tr, int it, double cost, double dc, double g, double st, double rho, double rad,
+                      double acc) {
+    if (!tr || !tr->rows || it >= tr->max_rows) return;
+    double* r = tr->rows + (size_t)it * TRACE_W;
+    r[0] = cost; r[1] = dc; r[2] = g; r[3] = st; r[4] = rho; r[5] = rad; r[6] = acc; r[7] = 0;
+}
+
 /* The Ceres 2.0 TrustRegionMinimizer::Minimize loop with LM strategy. */
-EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
+static int solve_impl(ba_problem* p, const ba_options* opt, ba_summary* sum, trace_t* tr) {
     const double t0 = now_ms();
     memset(sum, 0, sizeof(*sum));
     orc_t c;
@@ -747,14 +904,10 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
         sum->initial_cost = NAN; sum->final_cost = NAN;
         goto done;
     }
-    col_norms(&c, &L, cn);
+    colnorm_grad(&c, &L, cn, g);
     for (int i = 0; i < nl; ++i) scale[i] = opt->jacobi_scaling ? 1.0 / (1.0 + sqrt(cn[i])) : 1.0;
-    gradient(&c, &L, g);
     double gmax = grad_max_norm(&c, &x, g);
-    double gnorm = 0;
-    (void)gnorm;
     sum->initial_cost = x_cost;
-    double min_cost = x_cost;
     double final_cost = x_cost; /* SetSummaryFinalCost: min over iteration costs */
     double radius = opt->initial_trust_region_radius;
     double decrease_factor = 2.0;
@@ -763,6 +916,7 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
     int iter = 0, n_succ = 1, n_unsucc = 0, n_invalid = 0;
     int step_ok = 1; /* iteration 0 counts as successful */
     if (progress) { print_header(); print_row(0, x_cost, 0, gmax, 0, 0, radius, 0, 0); }
+    trace_row(tr, 0, x_cost, 0, gmax, 0, 0, radius, 1);
     for (;;) {
         /* FinalizeIterationAndCheckIfMinimizerCanContinue */
         if (iter >= opt->max_num_iterations) {
@@ -802,6 +956,7 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
                 sum->termination_type = BA_FAILURE;
                 snprintf(sum->message, sizeof(sum->message), "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d", opt->max_num_consecutive_invalid_steps);
                 ++n_unsucc;
+                trace_row(tr, iter, x_cost, 0, gmax, 0, 0, radius, 0);
                 break;
             }
             radius = radius / decrease_factor; /* LM StepIsInvalid == StepRejected */
@@ -810,6 +965,7 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
             step_ok = 0;
             ++n_unsucc;
             if (progress) print_row(iter, x_cost, 0, gmax, 0, 0, radius, 0, now_ms() - tl0);
+            trace_row(tr, iter, x_cost, 0, gmax, 0, 0, radius, 0);
             continue;
         }
         n_invalid = 0;
@@ -827,17 +983,19 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
                 for (int j = 0; j < 3; ++j) { const double d = x.pts[3 * i + j] - xc.pts[3 * i + j]; sn2 += d * d; }
         for (int j = 0; j < 4; ++j) { const double d = x.K[j] - xc.K[j]; sn2 += d * d; }
         const double step_norm = sqrt(sn2);
+        const double cost_change = x_cost - cand_cost;
         if (step_norm <= opt->parameter_tolerance * (xnorm + opt->parameter_tolerance)) {
             sum->termination_type = BA_CONVERGENCE;
             snprintf(sum->message, sizeof(sum->message), "Parameter tolerance reached. Relative step_norm: %e <= %e.", step_norm / (xnorm + opt->parameter_tolerance), opt->parameter_tolerance);
             /* the iteration is not finalized (returns before FinalizeIteration) */
+            trace_row(tr, iter, cand_cost, cost_change, gmax, step_norm, 0, radius, -1);
             break;
         }
         /* FunctionToleranceReached */
-        const double cost_change = x_cost - cand_cost;
         if (fabs(cost_change) <= opt->function_tolerance * x_cost) {
             sum->termination_type = BA_CONVERGENCE;
             snprintf(sum->message, sizeof(sum->message), "Function tolerance reached. |cost_change|/cost: %e <= %e", fabs(cost_change) / x_cost, opt->function_tolerance);
+            trace_row(tr, iter, cand_cost, cost_change, gmax, step_norm, 0, radius, -1);
             break;
         }
         /* IsStepSuccessful (monotonic: relative decrease vs model) */
@@ -855,8 +1013,7 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
                 break;
             }
             x_cost = ncost;
-            col_norms(&c, &L, cn);
-            gradient(&c, &L, g);
+            colnorm_grad(&c, &L, cn, g);
             gmax = grad_max_norm(&c, &x, g);
             /* LevenbergMarquardtStrategy::StepAccepted */
             radius = radius / fmax(1.0 / 3.0, 1.0 - pow(2.0 * rho - 1.0, 3));
@@ -865,9 +1022,9 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
             reuse_diag = 0;
             step_ok = 1;
             ++n_succ;
-            if (x_cost < min_cost) min_cost = x_cost;
             final_cost = fmin(final_cost, x_cost);
             if (progress) print_row(iter, x_cost, cost_change, gmax, step_norm, rho, radius, 0, now_ms() - tl0);
+            trace_row(tr, iter, x_cost, cost_change, gmax, step_norm, rho, radius, 1);
         } else {
             /* HandleUnsuccessfulStep: iteration cost reported = candidate cost */
             radius = radius / decrease_factor;
@@ -877,6 +1034,7 @@ EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
             ++n_unsucc;
             final_cost = fmin(final_cost, cand_cost);
             if (progress) print_row(iter, cand_cost, cost_change, gmax, step_norm, rho, radius, 0, now_ms() - tl0);
+            trace_row(tr, iter, cand_cost, cost_change, gmax, step_norm, rho, radius, 0);
         }
     }
     sum->final_cost = final_cost;
@@ -892,6 +1050,18 @@ done:
     lin_free(&L);
     orc_free(&c);
     return ret;
+}
+
+EXPORT int oracle_solve(ba_problem* p, const ba_options* opt, ba_summary* sum) {
+    return solve_impl(p, opt, sum, NULL);
+}
+
+/* oracle_solve plus the per-iteration trace (TRACE_W doubles per row, rows 0..num_iterations) */
+EXPORT int oracle_solve_trace(ba_problem* p, const ba_options* opt, ba_summary* sum, double* rows,
+                              int32_t max_rows) {
+    trace_t tr = {rows, max_rows};
+    if (rows && max_rows > 0) memset(rows, 0, sizeof(double) * TRACE_W * (size_t)max_rows);
+    return solve_impl(p, opt, sum, &tr);
 }
 
 /* Per-observation residuals/Jacobians in the ORIGINAL obs order (same layout
@@ -940,7 +1110,8 @@ EXPORT int oracle_reduced_system(const ba_problem* p, const ba_options* opt, dou
     double* cn = (double*)malloc(sizeof(double) * nl);
     double* scale = (double*)malloc(sizeof(double) * nl);
     double* D2 = (double*)malloc(sizeof(double) * nl);
-    col_norms(&c, &L, cn);
+    double* Sa = (double*)malloc(sizeof(double) * (c.nnz + 1));
+    colnorm_grad(&c, &L, cn, NULL);
     if (radius <= 0) radius = opt->initial_trust_region_radius;
     for (int i = 0; i < nl; ++i) {
         scale[i] = opt->jacobi_scaling ? 1.0 / (1.0 + sqrt(cn[i])) : 1.0;
@@ -948,9 +1119,17 @@ EXPORT int oracle_reduced_system(const ba_problem* p, const ba_options* opt, dou
         D2[i] = fmin(fmax(v, opt->min_lm_diagonal), opt->max_lm_diagonal) / radius;
     }
     memset(S, 0, sizeof(double) * (size_t)c.n * c.n);
-    memset(rhs, 0, sizeof(double) * c.n);
-    if (!st) st = build_reduced(&c, &L, scale, D2, pt_begin, pt_end, with_global, S, rhs, NULL, NULL, NULL);
-    free(cn); free(scale); free(D2);
+    if (!st) st = build_reduced(&c, &L, scale, D2, pt_begin, pt_end, with_global, Sa, rhs, NULL, NULL, NULL);
+    if (!st) {
+        const orc_t* cc = &c;
+        for (int r = 0; r < cc->n; ++r)
+            for (int j = cc->fc[r]; j <= r; ++j) {
+                const double v = Sa[cc->rp[r] + (size_t)(j - cc->fc[r])];
+                S[(size_t)r * cc->n + j] = v;
+                S[(size_t)j * cc->n + r] = v;
+            }
+    }
+    free(cn); free(scale); free(D2); free(Sa);
     lin_free(&L);
     orc_free(&c);
     return st ? BA_E_INVALID : 0;

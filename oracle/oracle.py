@@ -49,6 +49,11 @@ def lib():
                                             C.c_int32, C.c_int32, C.POINTER(C.c_int32), dp, dp]
         L.oracle_reduced_system.restype = C.c_int
         L.oracle_se3_plus.argtypes = [dp, dp, dp]
+        L.oracle_solve_trace.argtypes = [C.POINTER(BaProblem), C.POINTER(BaOptions), C.POINTER(BaSummary), dp,
+                                         C.c_int32]
+        L.oracle_solve_trace.restype = C.c_int
+        L.oracle_config.argtypes = [C.c_int32, C.c_int32]
+        L.oracle_max_threads.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -75,6 +80,35 @@ def solve(prob: ProblemArrays, opts: BaOptions | None = None) -> dict:
     if rc != 0:
         raise RuntimeError(f"oracle_solve failed: {rc}")
     return s.as_dict()
+
+
+TRACE_W = 8  # cost, cost_change, |gradient|, |step|, tr_ratio, tr_radius, accepted (1/0/-1), 0
+
+
+def solve_trace(prob: ProblemArrays, opts: BaOptions | None = None):
+    """solve() plus the per-iteration trace, rows 0..num_iterations (same layout as
+    libmiba's ba_iteration_log)."""
+    opts = opts or default_options()
+    s = BaSummary()
+    ps = prob.struct()
+    rows = max(int(opts.max_num_iterations), 0) + 2
+    tr = np.zeros((rows, TRACE_W))
+    rc = lib().oracle_solve_trace(C.byref(ps), C.byref(opts), C.byref(s), _dptr(tr), rows)
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_trace failed: {rc}")
+    d = s.as_dict()
+    return d, tr[: d["num_iterations"] + 1].copy()
+
+
+def config(threads: int = 1, profile: bool = False) -> None:
+    """Execution knobs of the restatement: OpenMP threads (1 = fixed summation order, the
+    checker) and the reduced-system storage (False = dense lower triangle, the checker;
+    True = the co-visibility profile, the SPARSE_SCHUR stand-in timed as the CPU baseline)."""
+    lib().oracle_config(int(threads), int(bool(profile)))
+
+
+def max_threads() -> int:
+    return int(lib().oracle_max_threads())
 
 
 def linearize(prob: ProblemArrays, opts: BaOptions | None = None):
