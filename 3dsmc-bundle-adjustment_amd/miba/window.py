@@ -90,20 +90,26 @@ def window_optimize(kf_i: int, kf_f: int, keyframes: list, landmarks: dict, intr
             uv.append((px, py))
             depth.append(d)
     summary = None
-    if obs_cam:
-        prob = ProblemArrays(np.array(cams), np.array(pts).reshape(-1, 3), np.array(intr_opt, dtype=np.float64),
-                             np.array(intr_init, dtype=np.float64), np.array(obs_cam), np.array(obs_pt),
-                             np.array(uv), np.array(depth), fixed_cam=0)
-        summary = solve(prob)  # :300
+    try:
+        # :300 — solved even when no observation is admissible: the IntrinsicsPrior block (:236-241) is always
+        # added, so Ceres still pulls intr_opt toward intr_init (the poses have no residual and stay put)
+        prob = ProblemArrays(np.array(cams), np.array(pts, dtype=np.float64).reshape(-1, 3),
+                             np.array(intr_opt, dtype=np.float64), np.array(intr_init, dtype=np.float64),
+                             np.array(obs_cam, dtype=np.int32), np.array(obs_pt, dtype=np.int32),
+                             np.array(uv, dtype=np.float64).reshape(-1, 2), np.array(depth, dtype=np.float64),
+                             fixed_cam=0)
+        summary = solve(prob)
         intr_opt[:] = prob.intr
         for k, lid in enumerate(ids):
             landmarks[lid] = prob.points[k].copy()
         for kf_n in range(kf_i, kf_f + 1):
             keyframes[kf_n].T_w_c = prob.cams[kf_n - kf_i].copy()
-    for kf_n in range(kf_i, kf_f + 1):  # :303-307
-        keyframes[kf_n].T_w_c = se3_mul(T0, keyframes[kf_n].T_w_c)
-    for lid in ids:  # :308-310
-        landmarks[lid] = se3_act(T0, landmarks[lid])
+    finally:
+        # :303-310 map back — also when the solve raised, so the caller's window is never left re-anchored
+        for kf_n in range(kf_i, kf_f + 1):
+            keyframes[kf_n].T_w_c = se3_mul(T0, keyframes[kf_n].T_w_c)
+        for lid in ids:
+            landmarks[lid] = se3_act(T0, landmarks[lid])
     return summary
 
 

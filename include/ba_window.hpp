@@ -163,10 +163,12 @@ bool windowOptimize(int kf_i, int kf_f, KeyFrames& keyframes, Map3D& map, const 
     }
     ba_problem prob = w.view();
     ba_summary summary{};
-    const int32_t rc = prob.n_obs > 0 ? solve(&prob, &summary) : BA_OK;  // :300
+    // :300 — solved even when no observation is admissible: the IntrinsicsPrior block (:236-241) is always
+    // added, so Ceres still pulls intrinsics_optimized toward intrinsics_initial (poses have no residual)
+    const int32_t rc = solve(&prob, &summary);
     if (status) *status = rc;
     if (summary_out) *summary_out = summary;
-    if (rc == BA_OK && prob.n_obs > 0) {
+    if (rc == BA_OK) {
         for (int i = 0; i < 4; ++i) intrinsics_optimized[i] = w.intr[i];
         for (size_t k = 0; k < w.landmark_ids.size(); ++k) {
             double* X = map.at(w.landmark_ids[k]).point.data();

@@ -1,0 +1,85 @@
+"""Edge cases of the C-ABI on the GPU: a non-finite initial evaluation (Ceres FAILURE with
+"Residual and Jacobian evaluation failed.", rc 0, no hang of the progress-word loop), windows
+without any admissible observation (only the IntrinsicsPrior block, OptimizationUtils.cpp:236-241,
+solved like Ceres), and a forced inter-workgroup hand-off timeout of the resident BCR kernel
+(loud BA_E_INTERNAL, then a per-level-launch fallback that still matches the oracle)."""
+import numpy as np
+import pytest
+
+from miba import synthetic
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _solver(**kw):
+    from miba.solver import Solver
+    return Solver(device=0, minimizer_progress_to_stdout=0, **kw)
+
+
+@pytest.mark.parametrize("bad", ["nan_point", "inf_depth_point_on_camera"])
+def test_non_finite_initial_evaluation_fails_like_ceres(bad):
+    p = synthetic.make_problem(n_cams=10, n_points=300, obs_per_point=(2, 3), seed=1)
+    if bad == "nan_point":
+        p.points[17] = np.nan
+    else:  # a point at a camera centre: z = 0, the projection divides by zero
+        k = int(np.nonzero(p.obs_pt == 5)[0][0])
+        p.points[5] = p.cams[p.obs_cam[k], 4:7]
+    q = p.copy()
+    with _solver() as s:
+        sg = s.solve(p)  # must return (rc 0), not spin
+        # the context stays usable afterwards
+        ok = synthetic.make_problem(n_cams=10, n_points=300, obs_per_point=(2, 3), seed=1)
+        so_ok = oracle.solve(ok.copy())
+        sg_ok = s.solve(ok)
+    so = oracle.solve(q)
+    assert so["termination"] == "FAILURE"
+    assert sg["termination"] == "FAILURE", sg
+    assert sg["message"] == "Residual and Jacobian evaluation failed.", sg["message"]
+    assert sg["num_iterations"] == 0
+    assert abs(sg_ok["final_cost"] - so_ok["final_cost"]) <= 1e-6 * so_ok["final_cost"]
+
+
+@pytest.mark.parametrize("kind", ["all_depths_zero", "no_observations"])
+def test_window_without_admissible_observations_solves_the_prior(kind):
+    p = synthetic.make_problem(n_cams=8, n_points=100, obs_per_point=(2, 4), seed=9)
+    if kind == "all_depths_zero":
+        p.obs_depth[:] = np.where(np.arange(p.n_obs) % 2 == 0, 0.0, -np.inf)
+    else:
+        from miba.capi import ProblemArrays
+        p = ProblemArrays(p.cams, p.points[:0], p.intr, p.intr_prior, p.obs_cam[:0], p.obs_pt[:0], p.obs_uv[:0],
+                          p.obs_depth[:0], p.fixed_cam)
+    p.intr[:] = p.intr_prior + np.array([4.0, -3.0, 2.0, -1.0])  # intrinsics_optimized != intrinsics_initial
+    q = p.copy()
+    cams0 = p.cams.copy()
+    with _solver() as s:
+        sg = s.solve(p)
+    so = oracle.solve(q)
+    assert sg["num_obs_admissible"] == 0 and sg["num_active_cams"] == 0 and sg["reduced_system_size"] == 4
+    assert sg["termination"] == so["termination"], (sg, so)
+    assert sg["num_iterations"] == so["num_iterations"]
+    assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-12 * so["initial_cost"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["initial_cost"], (sg, so)
+    np.testing.assert_allclose(p.intr, q.intr, rtol=1e-10)
+    assert np.max(np.abs(p.intr - p.intr_prior)) < 1e-2  # pulled onto the prior
+    np.testing.assert_array_equal(p.cams, cams0)  # no residual on any pose
+
+
+def test_bcr_handoff_timeout_is_loud_then_falls_back(monkeypatch):
+    from miba.solver import MibaError
+    p = synthetic.make_config("C2")
+    with _solver(max_num_iterations=5) as s:
+        monkeypatch.setenv("MIBA_BCR_SPIN_LIMIT", "1")
+        with pytest.raises(MibaError, match="timed out"):
+            s.solve(p.copy())
+        monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
+        q = p.copy()
+        sg = s.solve(q)  # per-level launches from now on
+    assert sg["linear_solver"] == 2
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=5))
+    assert sg["num_iterations"] == so["num_iterations"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sg, so)
+    # a fresh context uses the resident kernels again (the spin limit is back to its default)
+    with _solver(max_num_iterations=5) as s2:
+        sg2 = s2.solve(p.copy())
+    assert abs(sg2["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]

@@ -184,3 +184,72 @@ def test_lm_reaches_scipy_minimum_quadratic_regime():
     r = least_squares(fun, z0, method="lm", xtol=1e-15, ftol=1e-15, gtol=1e-15, max_nfev=20000)
     c_scipy = 0.5 * np.sum(r.fun ** 2)
     assert abs(s["final_cost"] - c_scipy) <= 1e-6 * c_scipy, (s, c_scipy)
+
+
+
+def test_lm_minimum_certified_by_scipy_huber_regime():
+    """Independent minimiser cross-check in the regime every real window runs in: the default Huber
+    a = 1e-3 with w = 1/N puts most residual blocks in the linear zone, where both LM and
+    scipy converge only linearly, so the check is a certificate at the oracle's minimum: an objective
+    written independently with numpy (refmath) equals the oracle's final cost there, and neither
+    scipy least_squares(loss="huber", f_scale=a) nor L-BFGS-B started from it lowers the cost by more
+    than 1e-6 relative. scipy's huber applies 0.5 a^2 rho(z / a^2) to each residual z = r^2; with one
+    residual per block (the block norm) that is 0.5 * Ceres HuberLoss(a)(|f_b|^2), the reference's
+    objective (OptimizationUtils.cpp:223-226, 279-294). Each IntrinsicsPrior row r (squared loss,
+    :237-241) enters as k^2 copies of r / k, inside Huber's quadratic zone (|r| / k < a), where they sum
+    to exactly 0.5 r^2."""
+    from scipy.optimize import least_squares, minimize
+    from refmath import plus_pose as pp, quat_R
+    p = small_problem(seed=11, n_cams=3, n_points=15, obs_per_point=(2, 3))
+    a = 1e-3
+    o = oracle.default_options(max_num_iterations=3000, function_tolerance=1e-15, parameter_tolerance=1e-15,
+                               gradient_tolerance=1e-16)
+    q = p.copy()
+    s = oracle.solve(q, o)
+    adm = np.nonzero(p.obs_depth > 1e-15)[0]
+    N = len(adm)
+    cams_act = [c for c in range(p.n_cams) if c != p.fixed_cam]
+    oc, op, uv, dep = p.obs_cam[adm], p.obs_pt[adm], p.obs_uv[adm], p.obs_depth[adm]
+    nz = 6 * len(cams_act) + 3 * p.n_points + 4
+    KSPLIT = 10
+
+    def unpack(z):  # local perturbation of the oracle's solution q
+        cams = q.cams.copy()
+        for i, c in enumerate(cams_act):
+            cams[c] = pp(q.cams[c], z[6 * i:6 * i + 6])
+        off = 6 * len(cams_act)
+        return cams, q.points + z[off:off + 3 * p.n_points].reshape(-1, 3), q.intr + z[off + 3 * p.n_points:]
+
+    def blocks(z):  # (|f_repr|^2, |f_depth|^2) per observation, prior residual
+        cams, pts, K = unpack(z)
+        R = np.array([quat_R(c[:4]) for c in cams])[oc]
+        pc = np.einsum("nji,nj->ni", R, pts[op] - cams[oc, 4:7])
+        u = (K[0] * pc[:, 0] + K[2] * pc[:, 2]) / pc[:, 2]
+        v = (K[1] * pc[:, 1] + K[3] * pc[:, 2]) / pc[:, 2]
+        return ((u - uv[:, 0]) ** 2 + (v - uv[:, 1]) ** 2) / N, 10 / N * (dep - pc[:, 2]) ** 2, \
+            np.sqrt(1e-6) * (p.intr_prior - K)
+
+    def rho(x):
+        return np.where(x > a * a, 2 * a * np.sqrt(x) - a * a, x)
+
+    def F(z):
+        sr, sd, fk = blocks(z)
+        return 0.5 * np.sum(rho(sr)) + 0.5 * np.sum(rho(sd)) + 0.5 * np.sum(fk ** 2)
+
+    def fun(z):
+        sr, sd, fk = blocks(z)
+        return np.r_[np.sqrt(sr), np.sqrt(sd), np.repeat(fk / KSPLIT, KSPLIT * KSPLIT)]
+
+    z0 = np.zeros(nz)
+    sr, sd, fk = blocks(z0)
+    assert np.mean(np.r_[sr, sd] > a * a) > 0.5  # the Huber linear zone dominates
+    assert np.all(np.abs(fk) / KSPLIT < a)
+    assert abs(F(z0) - s["final_cost"]) <= 1e-12 * s["final_cost"]
+    r = least_squares(fun, z0, method="trf", loss="huber", f_scale=a, xtol=1e-15, ftol=1e-15, gtol=1e-15,
+                      max_nfev=2000)
+    assert F(r.x) >= s["final_cost"] * (1 - 1e-6), (F(r.x), s["final_cost"])
+    m = minimize(F, z0, method="L-BFGS-B", options=dict(maxiter=5000, ftol=1e-16, gtol=1e-14, maxcor=50))
+    assert m.fun >= s["final_cost"] * (1 - 1e-6), (m.fun, s["final_cost"])
+    # the reference's own stopping rule (function_tolerance 1e-6 per step) ends close to that minimum
+    sd_ = oracle.solve(p.copy())
+    assert s["final_cost"] <= sd_["final_cost"] <= s["final_cost"] * (1 + 1e-3)

@@ -118,3 +118,52 @@ def test_cpp_adapter_on_gpu_matches_oracle(adapter_bin, tmp_path):
         np.testing.assert_allclose(K_g, K_c, atol=1e-3)
         for kc, kg in zip(kfs_c, kfs_g):
             np.testing.assert_allclose(kg.T_w_c[4:], kc.T_w_c[4:], atol=1e-5)
+
+
+def _tiny_window(depth):
+    rng = np.random.default_rng(7)
+    kfs, lms = [], {}
+    for l in range(6):
+        lms[l] = np.array([0.1 * l - 0.2, 0.05 * l, 2.0 + 0.1 * l])
+    for k in range(3):
+        T = np.array([0, 0, 0, 1.0, 0.01 * k, 0.0, 0.0])
+        kp = rng.uniform(100, 500, (6, 2)).astype(np.float32)
+        loc = np.zeros((6, 3))
+        loc[:, 2] = depth
+        kfs.append(window.KeyFrame(T, kp, loc, {i: i for i in range(6)}))
+    return kfs, lms
+
+
+def test_all_inadmissible_window_solves_the_intrinsics_prior():
+    """Every depth <= 1e-15: Ceres still solves the IntrinsicsPrior block (OptimizationUtils.cpp:236-241),
+    pulling intrinsics_optimized toward intrinsics_initial; poses and landmarks are untouched."""
+    kfs, lms = _tiny_window(0.0)
+    T_before = [kf.T_w_c.copy() for kf in kfs]
+    L_before = {k: v.copy() for k, v in lms.items()}
+    K0 = np.array([525.0, 525.0, 319.5, 239.5])
+    K = K0 + np.array([3.0, -2.0, 1.5, 0.5])
+    summ = window.window_optimize(0, 2, kfs, lms, K0, K, lambda p: oracle.solve(p))
+    assert summ["num_obs_admissible"] == 0 and summ["num_active_cams"] == 0
+    assert summ["termination"] == "CONVERGENCE"
+    assert np.all(np.abs(K - K0) < 1e-3 * np.abs(np.array([3.0, 2.0, 1.5, 0.5])))  # a quadratic: one step
+    for kf, T in zip(kfs, T_before):
+        np.testing.assert_allclose(kf.T_w_c, T, atol=1e-15)
+    for k in lms:
+        np.testing.assert_allclose(lms[k], L_before[k], atol=1e-15)
+
+
+def test_map_back_runs_when_the_solve_raises():
+    kfs, lms = _tiny_window(2.0)
+    kfs[0].T_w_c = np.array([0, 0, np.sin(0.1), np.cos(0.1), 0.3, -0.2, 0.1])
+    T_before = [kf.T_w_c.copy() for kf in kfs]
+    L_before = {k: v.copy() for k, v in lms.items()}
+
+    def boom(p):
+        raise RuntimeError("device lost")
+
+    with pytest.raises(RuntimeError):
+        window.window_optimize(0, 2, kfs, lms, np.ones(4), np.ones(4), boom)
+    for kf, T in zip(kfs, T_before):
+        np.testing.assert_allclose(kf.T_w_c, T, atol=1e-12)
+    for k in lms:
+        np.testing.assert_allclose(lms[k], L_before[k], atol=1e-12)
