@@ -17,6 +17,9 @@ static constexpr int PDATA = 24;
 static constexpr int TILE_WIN = 12;    // cameras per tile window
 static constexpr int CHUNK_PTS = 32;   // points per Schur chunk (K = 3 * CHUNK_PTS of the MFMA product)
 static constexpr int CHUNK_OBS = 256;
+// deterministic mode: per-tile Schur slab, rows of M' (80) x the window's camera dofs (6 * TILE_WIN)
+static constexpr int SCH_TBUF_LD = 6 * TILE_WIN;
+static constexpr int SCH_TBUF = 80 * SCH_TBUF_LD;
 static constexpr int SUBSEG_OBS = 1024;  // observations per camera-side sub-segment (one workgroup)
 static constexpr int BS_PTS = 64;     // points per back-substitution chunk
 static constexpr int BS_OBS = 512;    // observations per back-substitution chunk (a single point may exceed)
@@ -241,6 +244,10 @@ struct DevWork {
     double* env_glob;
     double* red;           // [32]: 0..3 local sums, 4..5 local maxima, 6..9 replicated sums, 10 chol flag,
                            //       16..19 global sums, 20..21 global maxima
+    // deterministic mode (ba_options.deterministic): per-tile Schur slabs + each active camera's tile range;
+    // nullptr: the tiles flush with f64 atomics
+    double* det_tbuf = nullptr;
+    const int2* det_trange = nullptr;
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)

@@ -957,6 +957,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 typedef double d4 __attribute__((ext_vector_type(4)));
 static constexpr int SCH_K = 3 * CHUNK_PTS;   // K extent of one chunk
 static constexpr int SCH_LDM = 80;            // rows of M' (6 * TILE_WIN + 5 <= 80)
+static_assert(SCH_LDM * 6 * TILE_WIN == SCH_TBUF, "deterministic slab geometry");
 static_assert(6 * TILE_WIN + 5 <= SCH_LDM, "M' rows exceed 5 MFMA tiles");
 static_assert(CHUNK_OBS <= TPB, "phase A: one observation per thread");
 
@@ -965,7 +966,8 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
                                                     double* __restrict__ rhs, unsigned long long* __restrict__ stamps,
-                                                    int nblk_pt, const double* __restrict__ part) {
+                                                    int nblk_pt, const double* __restrict__ part,
+                                                    double* __restrict__ tbuf) {
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     if (skip_step(st)) return;
     if ((int)blockIdx.x == P.n_tiles) {
@@ -1161,6 +1163,10 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             const int r1 = 16 * tib[t] + kq + 4 * g;
             if (r1 < r2 || r1 > er) continue;
             const double v = -acc[t][g];
+            if (tbuf) {  // deterministic mode: the tile's own slab, summed in tile order by k_schur_gather
+                tbuf[(size_t)tile * SCH_TBUF + r1 * SCH_TBUF_LD + r2] = v;
+                continue;
+            }
             if (r1 < kr) atomicAdd(&S[(size_t)(6 * base + r1) * ld + g2], v);
             else if (r1 < er) atomicAdd(&S[(size_t)(P.kb + r1 - kr) * ld + g2], v);
             else atomicAdd(&rhs[g2], v);
@@ -1173,6 +1179,114 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             for (int k = 0; k < 4; ++k) stamps[(size_t)blockIdx.x * 4 + k] = st_acc[k];
     }
 #undef SCH_STAMP
+}
+
+// Deterministic mode (ba_options.deterministic): every Schur tile wrote its flush into its own slab
+// tbuf[tile] (rows: 6 span camera dofs | 4 intrinsics | rhs; columns: 6 span camera dofs) instead of
+// f64 atomics into S. One workgroup per envelope tile of S sums, per element, the slabs of the tiles whose
+// camera window covers it, in increasing tile order: bitwise reproducible S / rhs.
+// trange[a] = [first tile with base >= a - (TILE_WIN - 1), first tile with base > a) (bases non-decreasing).
+__global__ __launch_bounds__(TPB) void k_schur_gather(DevProblem P, const LmState* __restrict__ st,
+                                                      const int2* __restrict__ tiles, const double* __restrict__ tbuf,
+                                                      const int2* __restrict__ trange, double* __restrict__ S,
+                                                      double* __restrict__ rhs) {
+    if (skip_step(st)) return;
+    const int2 ij = tiles[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
+    const int nd = 6 * P.nac, kb = P.kb;
+    if (col < nd && col <= r && (r < nd || (r >= kb && r < kb + 4))) {
+        const int b = col / 6;
+        const bool cam_row = r < nd;
+        const int a = cam_row ? r / 6 : b;
+        const int t0 = trange[a].x, t1 = trange[b].y;
+        double acc = 0.0;
+        for (int t = t0; t < t1; ++t) {
+            const int bs = P.tile_base[t], sp = P.tile_span[t];
+            if (bs > b || bs + sp <= a) continue;
+            const int r1 = cam_row ? r - 6 * bs : 6 * sp + (r - kb);
+            acc += tbuf[(size_t)t * SCH_TBUF + r1 * SCH_TBUF_LD + (col - 6 * bs)];
+        }
+        S[(size_t)r * P.npad + col] += acc;
+    }
+    if (ij.x == ij.y && tid < 16) {
+        const int rr = 16 * ij.x + tid;
+        if (rr < nd) {
+            const int a = rr / 6;
+            double acc = 0.0;
+            for (int t = trange[a].x; t < trange[a].y; ++t) {
+                const int bs = P.tile_base[t], sp = P.tile_span[t];
+                if (bs > a || bs + sp <= a) continue;
+                acc += tbuf[(size_t)t * SCH_TBUF + (6 * sp + 4) * SCH_TBUF_LD + (rr - 6 * bs)];
+            }
+            rhs[rr] += acc;
+        }
+    }
+}
+
+// Deterministic overflow Schur terms (k_obs_pairs without atomics): ONE workgroup walks the overflow
+// observations in their fixed order; every thread evaluates the (few) Jacobians itself, and each element
+// of S / rhs is always updated by the same thread (S camera block element (e2, d) by thread 6 d + e2, rhs
+// by 36 + d, border row m by 42 + 4 d + m), so the sums run in program order without barriers or atomics.
+// Overflow points (spanning > TILE_WIN cameras or linking a camera twice) are rare; this path is for the
+// reproducibility mode, not for speed.
+__global__ __launch_bounds__(128) void k_obs_pairs_det(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                       const double* __restrict__ scale,
+                                                       const double* __restrict__ pdata, double* __restrict__ S,
+                                                       double* __restrict__ rhs) {
+    if (skip_step(st)) return;
+    const int cur = st->cur;
+    const int tid = threadIdx.x;
+    const size_t ld = P.npad;
+    const int kb = P.kb;
+    const double* K = P.K[cur];
+    auto wt = [&](int q, int ca, const double* sp, const double* X, double W[18]) {
+        const double2 uv = P.po_uv[q];
+        ObsEval ev;
+        double jc[18], jp[9], jk[8];
+        lin_obs(c, P.cams[cur] + 7 * P.po_cam[q], X, K, uv.x, uv.y, P.po_depth[q], ev, jc, jp, jk);
+        w_tilde(jc, jp, scale + 6 * ca, sp, W);
+    };
+    for (int i = 0; i < P.n_ovf_obs; ++i) {
+        const int a = P.ovf_obs[i];
+        const int ca = P.po_ac[a];
+        if (ca < 0) continue;
+        const int ap = P.po_ap[a];
+        const double* pd = pdata + (size_t)ap * PDATA;
+        const double* sp = scale + P.off_pt + 3 * ap;
+        const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
+        double Vf[9], Wa[18], Y[18];
+        vinv_from_g(pd, Vf);
+        wt(a, ca, sp, X, Wa);
+#pragma unroll
+        for (int d = 0; d < 6; ++d)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                Y[d * 3 + j] = Wa[d * 3 + 0] * Vf[0 * 3 + j] + Wa[d * 3 + 1] * Vf[1 * 3 + j] + Wa[d * 3 + 2] * Vf[2 * 3 + j];
+        if (tid >= 36 && tid < 42) {
+            const int d = tid - 36;
+            rhs[6 * ca + d] -= Y[d * 3 + 0] * pd[6] + Y[d * 3 + 1] * pd[7] + Y[d * 3 + 2] * pd[8];
+        } else if (tid >= 42 && tid < 66) {
+            const int d = (tid - 42) >> 2, m = (tid - 42) & 3;
+            S[(size_t)(kb + m) * ld + 6 * ca + d] -=
+                Y[d * 3 + 0] * pd[9 + m * 3 + 0] + Y[d * 3 + 1] * pd[9 + m * 3 + 1] + Y[d * 3 + 2] * pd[9 + m * 3 + 2];
+        }
+        for (int b = P.pt_ptr[ap]; b < P.pt_ptr[ap + 1]; ++b) {
+            const int cb = P.po_ac[b];
+            if (cb < ca || (cb == ca && b < a) || tid >= 36) continue;
+            double W[18];
+            wt(b, cb, sp, X, W);
+            const int d = tid / 6, e2 = tid % 6;
+            if (cb > ca) {
+                S[(size_t)(6 * cb + e2) * ld + 6 * ca + d] -=
+                    Y[d * 3 + 0] * W[e2 * 3 + 0] + Y[d * 3 + 1] * W[e2 * 3 + 1] + Y[d * 3 + 2] * W[e2 * 3 + 2];
+            } else if (e2 >= d) {
+                double m = Y[d * 3 + 0] * W[e2 * 3 + 0] + Y[d * 3 + 1] * W[e2 * 3 + 1] + Y[d * 3 + 2] * W[e2 * 3 + 2];
+                if (b != a) m += Y[e2 * 3 + 0] * W[d * 3 + 0] + Y[e2 * 3 + 1] * W[d * 3 + 1] + Y[e2 * 3 + 2] * W[d * 3 + 2];
+                S[(size_t)(6 * ca + e2) * ld + 6 * ca + d] -= m;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------- Cholesky
@@ -2345,7 +2459,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                 scap = P.n_tiles;
             }
             PL(K_SCHUR_TILE, k_schur_tile<true>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
-               sst, pp_parts(P), W.part);
+               sst, pp_parts(P), W.part, W.det_tbuf);
             std::vector<unsigned long long> h((size_t)4 * P.n_tiles);
             CK(hipMemcpyAsync(h.data(), sst, sizeof(h[0]) * h.size(), hipMemcpyDeviceToHost, s));
             CK(hipStreamSynchronize(s));
@@ -2359,12 +2473,19 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                     P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
         } else {
             PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
-               W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part);
+               W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf);
         }
+        if (W.det_tbuf && P.n_tiles > 0)
+            PL(K_SCHUR_TILE, k_schur_gather, dim3(W.n_env), dim3(TPB), 0, s, P, W.st, W.env_tile, W.det_tbuf,
+               W.det_trange, W.S, W.rhs);
     }
-    if (P.n_ovf_obs > 0)
-        PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata,
-           W.S, W.rhs);
+    if (P.n_ovf_obs > 0) {
+        if (W.det_tbuf)
+            PL(K_OBS_PAIRS, k_obs_pairs_det, dim3(1), dim3(128), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs);
+        else
+            PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale,
+               W.pdata, W.S, W.rhs);
+    }
     if (W.comm.on()) {  // S = sum over the landmark shards: envelope tiles + rhs
         const size_t ne = (size_t)W.n_env * 256 + P.npad;
         PL(K_COMM, k_env_pack, dim3(W.n_env + 1), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs,

@@ -60,7 +60,7 @@ enum BufId {
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
     B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_ENV_GLOB, B_RED, B_PREP, B_BS_CHUNK, B_AC_SEG, B_CAMPART, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
-    B_DBG0, B_DBG1, B_DBG2, B_DBG3,
+    B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_DET_TRANGE,
     B_COUNT
 };
 
@@ -87,6 +87,17 @@ struct ba_context {
     int n_adm_all = 0;  // admissible observations over all landmark shards
     int prep_nc = -1, prep_np = -1, prep_no = -1;
     int last_iter = -1;        // iterations of the last solve (ba_iteration_log rows - 1)
+    // shard_min_obs: a window below the threshold is gathered onto every rank and solved there alone; the
+    // communicator is parked meanwhile (restored by the next prepare), the rank's points are the slice
+    // [gather_off, gather_off + its n_points) of the gathered window
+    Comm comm_parked;
+    int gather_off = 0;
+    int dev_np = 0;  // points on the device (the gathered window's when gathered)
+    struct Gathered {
+        std::vector<double> cams, pts, uv, dep;
+        std::vector<int> oc, op;
+        double intr[4], prior[4];
+    } gw;
     bool bcr_fallback = false;  // a resident BCR kernel timed out: per-level launches from then on
     // per-kernel profiling
     Prof prof;
@@ -131,21 +142,24 @@ static hipError_t upload(ba_context* ctx, int id, const T* src, size_t n) {
     return e;
 }
 
-// Host-side all-reduce of a small int32 array across the landmark shards (prepare time).
-static int host_allreduce_i32(ba_context* ctx, int* v, size_t n, CommOp op) {
+// Host-side all-reduce of a small array across the landmark shards (prepare time).
+template <class T>
+static int host_allreduce(ba_context* ctx, T* v, size_t n, CommOp op) {
     if (!ctx->W.comm.on() || n == 0) return BA_OK;
-    if (ctx->buf[B_PREP].ensure(sizeof(int) * n) != hipSuccess) { ctx->err = "prepare scratch allocation failed"; return BA_E_NOMEM; }
-    int* d = ctx->buf[B_PREP].as<int>();
+    if (ctx->buf[B_PREP].ensure(sizeof(T) * n) != hipSuccess) { ctx->err = "prepare scratch allocation failed"; return BA_E_NOMEM; }
+    T* d = ctx->buf[B_PREP].as<T>();
     hipStream_t s = ctx->stream;
-    if (hipMemcpyAsync(d, v, sizeof(int) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-        comm_allreduce(ctx->W.comm, d, d, n, COMM_I32, op, s) != hipSuccess ||
-        hipMemcpyAsync(v, d, sizeof(int) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    const CommType t = sizeof(T) == 8 ? COMM_F64 : COMM_I32;
+    if (hipMemcpyAsync(d, v, sizeof(T) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        comm_allreduce(ctx->W.comm, d, d, n, t, op, s) != hipSuccess ||
+        hipMemcpyAsync(v, d, sizeof(T) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         ctx->err = std::string("landmark-shard all-reduce failed: ") + comm_last_error();
         return BA_E_COMM;
     }
     return BA_OK;
 }
+static int host_allreduce_i32(ba_context* ctx, int* v, size_t n, CommOp op) { return host_allreduce(ctx, v, n, op); }
 
 extern "C" {
 
@@ -178,6 +192,7 @@ void ba_default_options(ba_options* o) {
     o->parameter_tolerance = 1e-8;
     o->device = -1;
     o->deterministic = 0;
+    o->shard_min_obs = 262144;
 }
 
 ba_context* ba_create(const ba_options* opts) {
@@ -224,6 +239,7 @@ void ba_destroy(ba_context* ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     comm_destroy(ctx->W.comm);
+    comm_destroy(ctx->comm_parked);
     for (auto& b : ctx->buf) b.release();
     for (auto& e : ctx->ev)
         if (e) hipEventDestroy(e);
@@ -248,6 +264,7 @@ int32_t ba_comm_unique_id(uint8_t id[BA_COMM_ID_BYTES]) {
 int32_t ba_comm_init(ba_context* ctx, int32_t nranks, int32_t rank, const uint8_t id[BA_COMM_ID_BYTES]) {
     if (!ctx || !id) return BA_E_INVALID;
     if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice failed"; return BA_E_DEVICE; }
+    comm_destroy(ctx->comm_parked);
     if (comm_init(ctx->W.comm, nranks, rank, id) != 0) {
         ctx->err = comm_last_error();
         return nranks < 1 || rank < 0 || rank >= nranks ? BA_E_INVALID : BA_E_COMM;
@@ -258,6 +275,7 @@ int32_t ba_comm_init(ba_context* ctx, int32_t nranks, int32_t rank, const uint8_
 
 int32_t ba_comm_init_host(ba_context* ctx, int32_t nranks, int32_t rank, ba_allreduce_fn fn, void* user) {
     if (!ctx) return BA_E_INVALID;
+    comm_destroy(ctx->comm_parked);
     if (comm_init_host(ctx->W.comm, nranks, rank, fn, user) != 0) {
         ctx->err = comm_last_error();
         return BA_E_INVALID;
@@ -304,7 +322,96 @@ int32_t ba_set_options(ba_context* ctx, const ba_options* opts) {
 // ---------------------------------------------------------------------------
 // Problem preparation: admissibility (countConstraints :184-213, skip :265-268),
 // active parameter blocks, point-major / camera-major orderings, envelope of S.
+static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det);
+
+// Landmark shards of a window too small to pay for the per-iteration exchange (admissible observations
+// over all shards < ba_options.shard_min_obs): gather every shard onto every rank (SUM all-reduces of
+// zero-padded slices, once per ba_prepare) and solve the whole window on each rank without collectives,
+// in deterministic mode so that all ranks compute bitwise the same cameras; each rank keeps its slice.
+// Returns 1 when the window was prepared gathered, 0 when it stays sharded, < 0 on error.
+static int prepare_gathered(ba_context* ctx, const ba_problem* p) {
+    Comm& comm = ctx->W.comm;
+    const int R = comm.nranks, me = comm.rank;
+    // agreement first (every rank reaches the same branch): local validity and admissible count
+    int v[2] = {0, 0};
+    bool ok = p && p->n_cams >= 0 && p->n_points >= 0 && p->n_obs >= 0 && p->intr && p->intr_prior &&
+              (!p->n_cams || p->cams) && (!p->n_points || p->points) &&
+              (!p->n_obs || (p->obs_cam && p->obs_pt && p->obs_uv && p->obs_depth));
+    for (int k = 0; ok && k < p->n_obs; ++k) {
+        if (p->obs_cam[k] < 0 || p->obs_cam[k] >= p->n_cams || p->obs_pt[k] < 0 || p->obs_pt[k] >= p->n_points) ok = false;
+        else if (p->obs_depth[k] > 1e-15) ++v[1];
+    }
+    v[0] = ok ? 0 : 1;
+    if (int rc = host_allreduce_i32(ctx, v, 2, COMM_SUM)) return rc;
+    if (v[0] != 0 || v[1] >= ctx->opts.shard_min_obs) return 0;  // invalid (prepare_core reports it) or large
+    std::vector<int> cnt(2 * (size_t)R, 0);
+    cnt[2 * me] = p->n_points;
+    cnt[2 * me + 1] = p->n_obs;
+    if (int rc = host_allreduce_i32(ctx, cnt.data(), cnt.size(), COMM_SUM)) return rc;
+    int np = 0, no = 0, poff = 0, ooff = 0;
+    for (int r = 0; r < R; ++r) {
+        if (r == me) { poff = np; ooff = no; }
+        np += cnt[2 * r];
+        no += cnt[2 * r + 1];
+    }
+    auto& g = ctx->gw;
+    g.cams.assign(p->cams, p->cams + 7 * (size_t)p->n_cams);  // replicated on every rank
+    std::memcpy(g.intr, p->intr, sizeof(g.intr));
+    std::memcpy(g.prior, p->intr_prior, sizeof(g.prior));
+    g.pts.assign(3 * (size_t)np, 0.0);
+    g.uv.assign(2 * (size_t)no, 0.0);
+    g.dep.assign(no, 0.0);
+    g.oc.assign(no, 0);
+    g.op.assign(no, 0);
+    std::copy(p->points, p->points + 3 * (size_t)p->n_points, g.pts.begin() + 3 * (size_t)poff);
+    std::copy(p->obs_uv, p->obs_uv + 2 * (size_t)p->n_obs, g.uv.begin() + 2 * (size_t)ooff);
+    std::copy(p->obs_depth, p->obs_depth + p->n_obs, g.dep.begin() + ooff);
+    std::copy(p->obs_cam, p->obs_cam + p->n_obs, g.oc.begin() + ooff);
+    for (int k = 0; k < p->n_obs; ++k) g.op[ooff + k] = p->obs_pt[k] + poff;
+    int rc = host_allreduce(ctx, g.pts.data(), g.pts.size(), COMM_SUM);
+    if (!rc) rc = host_allreduce(ctx, g.uv.data(), g.uv.size(), COMM_SUM);
+    if (!rc) rc = host_allreduce(ctx, g.dep.data(), g.dep.size(), COMM_SUM);
+    if (!rc) rc = host_allreduce_i32(ctx, g.oc.data(), g.oc.size(), COMM_SUM);
+    if (!rc) rc = host_allreduce_i32(ctx, g.op.data(), g.op.size(), COMM_SUM);
+    if (rc) return rc;
+    ba_problem full{};
+    full.n_cams = p->n_cams;
+    full.n_points = np;
+    full.n_obs = no;
+    full.fixed_cam = p->fixed_cam;
+    full.cams = g.cams.data();
+    full.points = g.pts.data();
+    full.intr = g.intr;
+    full.intr_prior = g.prior;
+    full.obs_cam = g.oc.data();
+    full.obs_pt = g.op.data();
+    full.obs_uv = g.uv.data();
+    full.obs_depth = g.dep.data();
+    ctx->comm_parked = comm;  // no collective while this window is solved
+    comm = Comm{};
+    rc = prepare_core(ctx, &full, true);
+    if (rc) return rc;
+    ctx->gather_off = poff;
+    ctx->dev_np = np;
+    ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;  // the caller's shard
+    return 1;
+}
+
 static int prepare(ba_context* ctx, const ba_problem* p) {
+    if (ctx->comm_parked.on()) {  // the last window ran gathered: the communicator is back for this one
+        ctx->W.comm = ctx->comm_parked;
+        ctx->comm_parked = Comm{};
+    }
+    ctx->gather_off = 0;
+    ctx->dev_np = p && p->n_points > 0 ? p->n_points : 0;
+    if (ctx->W.comm.on() && ctx->opts.shard_min_obs > 0) {
+        const int rc = prepare_gathered(ctx, p);
+        if (rc != 0) return rc < 0 ? rc : BA_OK;
+    }
+    return prepare_core(ctx, p, false);
+}
+
+static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     const ba_options& o = ctx->opts;
     const bool shard = ctx->W.comm.on();
     // validation: with landmark shards every rank must reach the same verdict before any
@@ -698,6 +805,21 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     W.scal = ctx->buf[B_SCAL].as<double>(); W.chol_flag = ctx->buf[B_FLAG].as<int>();
     W.fcol = ctx->buf[B_FCOL].as<int>(); W.rptr = ctx->buf[B_RPTR].as<int>(); W.rows = ctx->buf[B_ROWS].as<int>();
     W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
+    // deterministic mode: the Schur tiles write per-tile slabs, summed in tile order per element of S
+    W.det_tbuf = nullptr;
+    W.det_trange = nullptr;
+    if ((o.deterministic || force_det) && P.n_tiles > 0) {
+        HIPCHECK(ctx, ctx->buf[B_DET_TBUF].ensure(sizeof(double) * SCH_TBUF * (size_t)P.n_tiles));
+        std::vector<int2> trange(std::max(nac, 1));
+        for (int a = 0, lo = 0, hi = 0; a < nac; ++a) {
+            while (lo < P.n_tiles && tile_base[lo] < a - (TILE_WIN - 1)) ++lo;
+            while (hi < P.n_tiles && tile_base[hi] <= a) ++hi;
+            trange[a] = make_int2(lo, std::max(lo, hi));
+        }
+        HIPCHECK(ctx, upload(ctx, B_DET_TRANGE, trange.data(), trange.size()));
+        W.det_tbuf = ctx->buf[B_DET_TBUF].as<double>();
+        W.det_trange = ctx->buf[B_DET_TRANGE].as<int2>();
+    }
     BaConsts& C = ctx->C;
     ctx->n_adm_all = n_adm_all;
     // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
@@ -878,7 +1000,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     h_state = fresh_state(o, o.initial_trust_region_radius);
     // start from the parameters of the last ba_prepare() (device-to-device) and a fresh state
     HIPCHECK(ctx, launch_reset(P, W, h_state, ctx->buf[B_CAMS_INIT].as<double>(), ctx->buf[B_PTS_INIT].as<double>(),
-                               ctx->buf[B_K_INIT].as<double>(), p->n_cams, p->n_points, s));
+                               ctx->buf[B_K_INIT].as<double>(), p->n_cams, ctx->dev_np, s));
     sum->num_obs_admissible = ctx->n_adm_all;
     sum->num_active_cams = P.nac;
     sum->num_active_points = P.n_ap;
@@ -992,7 +1114,8 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     // copy the best (= last accepted) parameters back in place
     const int cur = S.cur;
     HIPCHECK(ctx, hipMemcpyAsync(p->cams, P.cams[cur], sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToHost, s));
-    HIPCHECK(ctx, hipMemcpyAsync(p->points, P.pts[cur], sizeof(double) * 3 * (size_t)p->n_points, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(p->points, P.pts[cur] + 3 * (size_t)ctx->gather_off, sizeof(double) * 3 * (size_t)p->n_points,
+                                 hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipMemcpyAsync(p->intr, P.K[cur], sizeof(double) * 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipStreamSynchronize(s));
     const double t1 = now_ms();

@@ -54,7 +54,8 @@ class BaOptions(C.Structure):
         ("deterministic", C.c_int32),
         ("profile_kernels", C.c_int32),
         ("profile_mask", C.c_int32),
-        ("reserved", C.c_int32 * 4),
+        ("shard_min_obs", C.c_int32),
+        ("reserved", C.c_int32 * 3),
     ]
 
 
@@ -145,7 +146,8 @@ def default_options_py() -> BaOptions:
     o.gradient_tolerance = 1e-10
     o.parameter_tolerance = 1e-8
     o.device = -1
-    o.deterministic = 1
+    o.deterministic = 0  # = ba_default_options
+    o.shard_min_obs = 262144
     return o
 
 

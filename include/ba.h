@@ -81,10 +81,16 @@ typedef struct ba_options {
     double parameter_tolerance;         /* 1e-8 */
     /* MI355X execution knobs (no reference counterpart) */
     int32_t device;          /* HIP device ordinal for this context; -1 = current */
-    int32_t deterministic;   /* 1 = fixed-order reductions only (no float atomics) */
+    int32_t deterministic;   /* 1 = fixed-order reductions only (no float atomics): bitwise-reproducible
+                                solves (the Schur tiles write per-tile slabs summed in tile order; the
+                                overflow Schur terms run in one workgroup), at some speed cost */
     int32_t profile_kernels; /* 1 = HIP-event timing of kernel launches (ba_kernel_stats) */
     int32_t profile_mask;    /* with profile_kernels: bit k selects kernel id k of ba_kernel_stats order; 0 = all */
-    int32_t reserved[4];
+    int32_t shard_min_obs;   /* landmark shards (ba_comm_init*): a window with fewer admissible observations
+                                over all shards is gathered onto every rank at ba_prepare and solved there
+                                alone (no per-iteration collectives, deterministic mode), each rank keeping
+                                its own points; 0 = always run the sharded exchange. Default 262144 */
+    int32_t reserved[3];
 } ba_options;
 
 /* One window, flattened. Mirrors what windowOptimize feeds to Ceres

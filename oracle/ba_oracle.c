@@ -68,7 +68,8 @@ EXPORT void oracle_default_options(ba_options* o) {
     o->gradient_tolerance = 1e-10;
     o->parameter_tolerance = 1e-8;
     o->device = -1;
-    o->deterministic = 1;
+    o->deterministic = 0;        /* the oracle is single-ordered anyway; mirrors ba_default_options */
+    o->shard_min_obs = 262144;   /* libmiba execution knob, unused here */
 }
 
 /* ------------------------------------------------------------------ */

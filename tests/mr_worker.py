@@ -57,8 +57,10 @@ def main():
             s.comm_init_host(world, rank, shard.torch_allreduce())
             summ = s.solve(prob)
             log = s.iteration_log()
+            comm_launches = sum(k["launches"] for k in s.kernel_stats() if k["name"] == "comm")
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), cams=prob.cams, points=prob.points, intr=prob.intr,
-                 ids=ids, log=log, summary=json.dumps({k: v for k, v in summ.items() if not isinstance(v, bytes)}))
+                 ids=ids, log=log, summary=json.dumps({k: v for k, v in summ.items() if not isinstance(v, bytes)}),
+                 comm_launches=comm_launches)
     finally:
         dist.destroy_process_group()
 

@@ -134,7 +134,7 @@ def test_sharded_path_single_rank(case):
     q = p.copy()
     with Solver(minimizer_progress_to_stdout=0) as a:
         sa = a.solve(p)
-    with Solver(minimizer_progress_to_stdout=0) as b:
+    with Solver(minimizer_progress_to_stdout=0, shard_min_obs=0) as b:
         b.comm_init(1, 0, Solver.comm_unique_id())
         sb = b.solve(q)
     assert sb["num_obs_admissible"] == sa["num_obs_admissible"]
@@ -150,7 +150,7 @@ def test_sharded_path_matches_oracle_c2():
     from miba.solver import Solver
     p = synthetic.make_config("C2")
     q = p.copy()
-    with Solver(minimizer_progress_to_stdout=0) as b:
+    with Solver(minimizer_progress_to_stdout=0, shard_min_obs=0) as b:
         b.comm_init(1, 0, Solver.comm_unique_id())
         sb = b.solve(p)
     so = oracle.solve(q)

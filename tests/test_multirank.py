@@ -51,7 +51,7 @@ def run_ranks(tmp_path, world, spec, timeout=240):
     for r in range(world):
         z = np.load(os.path.join(tmp_path, f"rank{r}.npz"))
         res.append(dict(cams=z["cams"], points=z["points"], intr=z["intr"], ids=z["ids"], log=z["log"],
-                        summary=json.loads(str(z["summary"]))))
+                        summary=json.loads(str(z["summary"])), comm_launches=int(z["comm_launches"])))
     return res
 
 
@@ -90,7 +90,7 @@ def check(res, whole, ref_q, ref_s, ref_log, so):
 @pytest.mark.parametrize("world,nsplit,env", [(2, 2, {}), (2, 2, {"MIBA_BCR": "launch"}), (4, 3, {})])
 def test_c2_sharded_ranks(tmp_path, world, nsplit, env):
     """C2 (20 cams / 5k points / 50k obs) split over 2 ranks, and over 3 ranks + one empty shard."""
-    spec = {"problem": {"config": "C2"}, "nsplit": nsplit, "env": env}
+    spec = {"problem": {"config": "C2"}, "nsplit": nsplit, "env": env, "options": {"shard_min_obs": 0}}
     res = run_ranks(tmp_path, world, spec)
     whole = synthetic.make_config("C2")
     ref_q, ref_s, ref_log = unsharded(whole)
@@ -113,8 +113,28 @@ def test_c4_sharded_four_ranks_one_empty(tmp_path):
 def test_tum_like_two_ranks_wide_overflow(tmp_path):
     """Overflow (atomic) Schur points and repeated-camera links on both ranks."""
     mp = dict(n_cams=30, n_points=150, obs_per_point=(6, 16), seed=5, rot_noise=0.005, dup_frac=0.05)
-    res = run_ranks(tmp_path, 2, {"problem": {"make_problem": mp}, "nsplit": 2})
+    res = run_ranks(tmp_path, 2, {"problem": {"make_problem": mp}, "nsplit": 2, "options": {"shard_min_obs": 0}})
     whole = synthetic.make_problem(**mp)
     ref_q, ref_s, ref_log = unsharded(whole)
     so = oracle.solve(whole.copy())
     check(res, whole, ref_q, ref_s, ref_log, so)
+
+
+def test_small_window_is_gathered_not_sharded(tmp_path):
+    """ba_options.shard_min_obs (default 262144 admissible observations): C2's 50k observations are
+    gathered onto both ranks at ba_prepare and each rank solves the whole window alone (no per-iteration
+    collective), in deterministic mode, so both ranks hold bitwise the same cameras."""
+    spec = {"problem": {"config": "C2"}, "nsplit": 2, "options": {"profile_kernels": 1}}
+    res = run_ranks(tmp_path, 2, spec)
+    whole = synthetic.make_config("C2")
+    ref_q, ref_s, ref_log = unsharded(whole)
+    so = oracle.solve(whole.copy())
+    check(res, whole, ref_q, ref_s, ref_log, so)
+    assert all(r["comm_launches"] == 0 for r in res)  # no collective inside the LM loop
+
+
+def test_sharded_exchange_runs_collectives(tmp_path):
+    spec = {"problem": {"config": "C2"}, "nsplit": 2, "options": {"profile_kernels": 1, "shard_min_obs": 0,
+                                                                  "max_num_iterations": 4}}
+    res = run_ranks(tmp_path, 2, spec)
+    assert all(r["comm_launches"] > 0 for r in res)
