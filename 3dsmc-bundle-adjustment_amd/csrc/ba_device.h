@@ -133,6 +133,79 @@ __device__ __forceinline__ void lin_obs(const BaConsts& c, const double* __restr
     jk[4] = 0.0; jk[5] = su * y * iz; jk[6] = 0.0; jk[7] = su;
 }
 
+// Structural zeros of the local Jacobian (lin_obs): jc row 0 has no upsilon_y entry, row 1 no
+// upsilon_x, row 2 only upsilon_z / omega_x / omega_y; jk rows are [fx-col, 0, 1-col, 0] and
+// [0, fy-col, 0, 1-col] (times su). The camera-side sums therefore have 9 entries that are zero for
+// every observation — U(0,1), C(0,1), C(0,3), C(1,0), C(1,2), Ukk(0,1), Ukk(0,3), Ukk(1,2), Ukk(2,3) —
+// and the rest need 80 products instead of 160. CAM_NZ packed sums per observation:
+//   [0, 20)  U upper-packed without U(0,1)      [20, 40) C without its 4 zeros
+//   [40, 46) g = Jc^T f                          [46, 52) Ukk nonzeros (00, 02, 11, 13, 22, 33)
+//   [52, 56) gk = Jk^T f                         [56]     cost
+static constexpr int CAM_NZ = 57;
+__device__ __forceinline__ void cam_accum(double* a, const double jc[18], const double jk[8],
+                                          const double f[3], double cost, bool cam) {
+    // nonzeros of the three rows (index = camera dof)
+    const double c0 = jc[0], c2 = jc[2], c3 = jc[3], c4 = jc[4], c5 = jc[5];
+    const double e1 = jc[7], e2 = jc[8], e3 = jc[9], e4 = jc[10], e5 = jc[11];
+    const double h2 = jc[14], h3 = jc[15], h4 = jc[16];
+    const double k0 = jk[0], su = jk[2], k1 = jk[5];
+    if (cam) {
+        a[0] += c0 * c0; a[1] += c0 * c2; a[2] += c0 * c3; a[3] += c0 * c4; a[4] += c0 * c5;
+        a[5] += e1 * e1; a[6] += e1 * e2; a[7] += e1 * e3; a[8] += e1 * e4; a[9] += e1 * e5;
+        a[10] += c2 * c2 + e2 * e2 + h2 * h2;
+        a[11] += c2 * c3 + e2 * e3 + h2 * h3;
+        a[12] += c2 * c4 + e2 * e4 + h2 * h4;
+        a[13] += c2 * c5 + e2 * e5;
+        a[14] += c3 * c3 + e3 * e3 + h3 * h3;
+        a[15] += c3 * c4 + e3 * e4 + h3 * h4;
+        a[16] += c3 * c5 + e3 * e5;
+        a[17] += c4 * c4 + e4 * e4 + h4 * h4;
+        a[18] += c4 * c5 + e4 * e5;
+        a[19] += c5 * c5 + e5 * e5;
+        // C[i][m]: row 0 pairs with jk columns 0, 2; row 1 with 1, 3
+        a[20] += c0 * k0; a[21] += c0 * su;                        // C00, C02
+        a[22] += e1 * k1; a[23] += e1 * su;                        // C11, C13
+        a[24] += c2 * k0; a[25] += e2 * k1; a[26] += c2 * su; a[27] += e2 * su;  // C2*
+        a[28] += c3 * k0; a[29] += e3 * k1; a[30] += c3 * su; a[31] += e3 * su;  // C3*
+        a[32] += c4 * k0; a[33] += e4 * k1; a[34] += c4 * su; a[35] += e4 * su;  // C4*
+        a[36] += c5 * k0; a[37] += e5 * k1; a[38] += c5 * su; a[39] += e5 * su;  // C5*
+        a[40] += c0 * f[0];
+        a[41] += e1 * f[1];
+        a[42] += c2 * f[0] + e2 * f[1] + h2 * f[2];
+        a[43] += c3 * f[0] + e3 * f[1] + h3 * f[2];
+        a[44] += c4 * f[0] + e4 * f[1] + h4 * f[2];
+        a[45] += c5 * f[0] + e5 * f[1];
+    }
+    a[46] += k0 * k0; a[47] += k0 * su; a[48] += k1 * k1; a[49] += k1 * su; a[50] += su * su; a[51] += su * su;
+    a[52] += k0 * f[0]; a[53] += k1 * f[1]; a[54] += su * f[0]; a[55] += su * f[1];
+    a[56] += cost;
+}
+// Expand the packed sums into the CAMDATA (U 21 | C 24 | g 6) and SEGINTR (Ukk 10 | gk 4 | cost)
+// layouts: element e of [camdata | segintr] (66 values) from the packed array p.
+__device__ __forceinline__ double cam_unpack(const double* p, int e) {
+    // U upper-packed (i <= j): q = 6 i - i (i - 1) / 2 + (j - i); q = 1 is U(0,1) == 0
+    if (e < 21) return e == 0 ? p[0] : (e == 1 ? 0.0 : p[e - 1]);
+    if (e < 45) {  // C[i][m], e - 21 = 4 i + m
+        const int i = (e - 21) >> 2, m = (e - 21) & 3;
+        if (i == 0) return m == 0 ? p[20] : (m == 2 ? p[21] : 0.0);
+        if (i == 1) return m == 1 ? p[22] : (m == 3 ? p[23] : 0.0);
+        return p[24 + 4 * (i - 2) + m];
+    }
+    if (e < 51) return p[40 + (e - 45)];
+    if (e < 61) {  // Ukk packed (m <= l): 00 01 02 03 11 12 13 22 23 33
+        switch (e - 51) {
+            case 0: return p[46];
+            case 2: return p[47];
+            case 4: return p[48];
+            case 6: return p[49];
+            case 7: return p[50];
+            case 9: return p[51];
+            default: return 0.0;
+        }
+    }
+    return p[52 + (e - 61)];  // gk (4), cost
+}
+
 // Sophus T * exp(delta)  (se3.hpp:725-746, so3.hpp:537-571, so3.hpp:339-356)
 __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const double* __restrict__ d,
                                          double* __restrict__ out) {

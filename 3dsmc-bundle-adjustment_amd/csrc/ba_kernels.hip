@@ -158,17 +158,18 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
     if (blockIdx.x == 0 && threadIdx.x == 0) *gmax_word = 0.0;
     if (st->done || (gated && !st->need_lin)) return;
     const int cur = st->cur;
-    __shared__ double lds[4 * 66];
-    __shared__ double out[66];
+    __shared__ double lds[4 * CAM_NZ];
+    __shared__ double out[CAM_NZ];
     const int s = blockIdx.x;
     const int cam = P.seg_cam[s];
     const int ac = P.seg_ac[s];
     const double* pose = P.cams[cur] + 7 * cam;
     const double* pts = P.pts[cur];
     const double* K = P.K[cur];
-    double acc[66];
+    // packed sums without the structural zeros of the Jacobian (cam_accum, ba_device.h)
+    double acc[CAM_NZ];
 #pragma unroll
-    for (int i = 0; i < 66; ++i) acc[i] = 0.0;
+    for (int i = 0; i < CAM_NZ; ++i) acc[i] = 0.0;
     const int o0 = P.seg_ptr[s], o1 = P.seg_ptr[s + 1];
     // software pipeline: point index two observations ahead, point / pixel / depth one ahead
     const int oa = o0 + threadIdx.x;
@@ -199,32 +200,12 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
         double jc[18], jp[9], jk[8];
         lin_obs(c, pose, X, K, uv.x, uv.y, dep, e, jc, jp, jk);
         (void)jp;
-        if (ac >= 0) {
-            int q = 0;
-#pragma unroll
-            for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int j = i; j < 6; ++j, ++q) acc[q] += jc[i] * jc[j] + jc[6 + i] * jc[6 + j] + jc[12 + i] * jc[12 + j];
-#pragma unroll
-            for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int m = 0; m < 4; ++m) acc[21 + i * 4 + m] += jc[i] * jk[m] + jc[6 + i] * jk[4 + m];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) acc[45 + i] += jc[i] * e.f[0] + jc[6 + i] * e.f[1] + jc[12 + i] * e.f[2];
-        }
-        int q = 51;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int l = m; l < 4; ++l, ++q) acc[q] += jk[m] * jk[l] + jk[4 + m] * jk[4 + l];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc[61 + m] += jk[m] * e.f[0] + jk[4 + m] * e.f[1];
-        acc[65] += e.ok ? e.cost : __builtin_nan("");
+        cam_accum(acc, jc, jk, e.f, e.ok ? e.cost : __builtin_nan(""), ac >= 0);
     }
-    block_sum_rs<66>(acc, lds, out);
+    block_sum_rs<CAM_NZ>(acc, lds, out);
     if (ac >= 0)
-        for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)s * CAMDATA + i] = out[i];
-    for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = out[51 + i];
+        for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)s * CAMDATA + i] = cam_unpack(out, i);
+    for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = cam_unpack(out, CAMDATA + i);
 }
 
 // One launch for what follows the camera-side pass (was k_cam_reduce + k_lin_finalize):
@@ -396,11 +377,26 @@ __device__ __forceinline__ void vinv_from_g(const double* G, double Vf[9]) {
 // W~ (6x3) = s_c (Jc^T Jp) s_p  for one observation
 __device__ __forceinline__ void w_tilde(const double jc[18], const double jp[9], const double* sc, const double* sp,
                                         double W[18]) {
+    // structural zeros of jc skipped (cam_accum, ba_device.h): rows 0 / 1 / 2 have 5 / 5 / 3 nonzeros
 #pragma unroll
-    for (int d = 0; d < 6; ++d)
+    for (int i = 0; i < 3; ++i) {
+        const double p0 = jp[i], p1 = jp[3 + i], p2 = jp[6 + i];
+        double w[6];
+        w[0] = jc[0] * p0;
+        w[1] = jc[7] * p1;
+        w[2] = jc[2] * p0 + jc[8] * p1 + jc[14] * p2;
+        w[3] = jc[3] * p0 + jc[9] * p1 + jc[15] * p2;
+        w[4] = jc[4] * p0 + jc[10] * p1 + jc[16] * p2;
+        w[5] = jc[5] * p0 + jc[11] * p1;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-            W[d * 3 + i] = sc[d] * (jc[d] * jp[i] + jc[6 + d] * jp[3 + i] + jc[12 + d] * jp[6 + i]) * sp[i];
+        for (int d = 0; d < 6; ++d) W[d * 3 + i] = sc[d] * w[d] * sp[i];
+    }
+}
+// J_c v for the three rows (structural zeros skipped)
+__device__ __forceinline__ void jc_times(const double jc[18], const double v[6], double out[3]) {
+    out[0] = jc[0] * v[0] + jc[2] * v[2] + jc[3] * v[3] + jc[4] * v[4] + jc[5] * v[5];
+    out[1] = jc[7] * v[1] + jc[8] * v[2] + jc[9] * v[3] + jc[10] * v[4] + jc[11] * v[5];
+    out[2] = jc[14] * v[2] + jc[15] * v[3] + jc[16] * v[4];
 }
 // mode 0: column norms only (iteration 0, before the Jacobi scale exists)
 // mode 1: full Schur preparation.
@@ -749,9 +745,12 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
 #pragma unroll
             for (int i = 0; i < 3; ++i) acc[6 + i] += jp[i] * ev.f[0] + jp[3 + i] * ev.f[1] + jp[6 + i] * ev.f[2];
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int i = 0; i < 3; ++i) acc[9 + m * 3 + i] += jk[m] * jp[i] + jk[4 + m] * jp[3 + i];
+            for (int i = 0; i < 3; ++i) {  // Kt = Jk^T Jp: jk row 0 is [k0, 0, su, 0], row 1 [0, k1, 0, su]
+                acc[9 + 0 * 3 + i] += jk[0] * jp[i];
+                acc[9 + 1 * 3 + i] += jk[5] * jp[3 + i];
+                acc[9 + 2 * 3 + i] += jk[2] * jp[i];
+                acc[9 + 3 * 3 + i] += jk[7] * jp[3 + i];
+            }
         }
         if (mode == 0) {
             double v3[3] = {acc[0], acc[3], acc[5]};
@@ -876,11 +875,7 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, con
         lin_obs(c, P.cams[cur] + 7 * P.po_cam[a], X, K, uv.x, uv.y, P.po_depth[a], ev, jc, jp, jk);
         const double* sc = scale + 6 * ca;
         double W[18];
-#pragma unroll
-        for (int d = 0; d < 6; ++d)
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                W[d * 3 + i] = sc[d] * (jc[d] * jp[i] + jc[6 + d] * jp[3 + i] + jc[12 + d] * jp[6 + i]) * sp[i];
+        w_tilde(jc, jp, sc, sp, W);
 #pragma unroll
         for (int d = 0; d < 6; ++d)
 #pragma unroll
@@ -906,11 +901,7 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, con
         lin_obs(c, P.cams[cur] + 7 * P.po_cam[b], X, K, uv.x, uv.y, P.po_depth[b], ev, jc, jp, jk);
         const double* sc = scale + 6 * cb;
         double W[18];
-#pragma unroll
-        for (int d = 0; d < 6; ++d)
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                W[d * 3 + i] = sc[d] * (jc[d] * jp[i] + jc[6 + d] * jp[3 + i] + jc[12 + d] * jp[6 + i]) * sp[i];
+        w_tilde(jc, jp, sc, sp, W);
         // M = Y_a W_b^T  (block (ca, cb)); lower storage S[6cb + e][6ca + d]
         if (cb > ca) {
 #pragma unroll
@@ -1885,14 +1876,10 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
             const double* sc = scale + 6 * ac;
             const double* yc = y + 6 * ac;
             const double* sp = scale + P.off_pt + 3 * ap;
-            double jy[3];
+            double jy[3], sy[6];
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                double sacc = 0.0;
-#pragma unroll
-                for (int d = 0; d < 6; ++d) sacc += jc[r * 6 + d] * (sc[d] * yc[d]);
-                jy[r] = sacc;
-            }
+            for (int d = 0; d < 6; ++d) sy[d] = sc[d] * yc[d];
+            jc_times(jc, sy, jy);
 #pragma unroll
             for (int i = 0; i < 3; ++i) v[i] = sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
         }
