@@ -142,13 +142,15 @@ __device__ __forceinline__ void lin_obs(const BaConsts& c, const double* __restr
 //   [40, 46) g = Jc^T f                          [46, 52) Ukk nonzeros (00, 02, 11, 13, 22, 33)
 //   [52, 56) gk = Jk^T f                         [56]     cost
 static constexpr int CAM_NZ = 57;
-__device__ __forceinline__ void cam_accum(double* a, const double jc[18], const double jk[8],
-                                          const double f[3], double cost, bool cam) {
-    // nonzeros of the three rows (index = camera dof)
+// The packed sums in two halves (for callers short of registers): CAM_NZ_U = U (20) | g (6) | cost -> packed
+// [0, 20), [40, 46), 56; CAM_NZ_C = C (20) | Ukk (6) | gk (4) -> packed [20, 40), [46, 56).
+static constexpr int CAM_NZ_U = 27, CAM_NZ_C = 30;
+__device__ __forceinline__ int cam_nz_u_index(int i) { return i < 20 ? i : (i < 26 ? 40 + (i - 20) : 56); }
+__device__ __forceinline__ int cam_nz_c_index(int i) { return i < 20 ? 20 + i : 46 + (i - 20); }
+__device__ __forceinline__ void cam_accum_u(double* a, const double jc[18], const double f[3], double cost, bool cam) {
     const double c0 = jc[0], c2 = jc[2], c3 = jc[3], c4 = jc[4], c5 = jc[5];
     const double e1 = jc[7], e2 = jc[8], e3 = jc[9], e4 = jc[10], e5 = jc[11];
     const double h2 = jc[14], h3 = jc[15], h4 = jc[16];
-    const double k0 = jk[0], su = jk[2], k1 = jk[5];
     if (cam) {
         a[0] += c0 * c0; a[1] += c0 * c2; a[2] += c0 * c3; a[3] += c0 * c4; a[4] += c0 * c5;
         a[5] += e1 * e1; a[6] += e1 * e2; a[7] += e1 * e3; a[8] += e1 * e4; a[9] += e1 * e5;
@@ -162,23 +164,45 @@ __device__ __forceinline__ void cam_accum(double* a, const double jc[18], const 
         a[17] += c4 * c4 + e4 * e4 + h4 * h4;
         a[18] += c4 * c5 + e4 * e5;
         a[19] += c5 * c5 + e5 * e5;
-        // C[i][m]: row 0 pairs with jk columns 0, 2; row 1 with 1, 3
-        a[20] += c0 * k0; a[21] += c0 * su;                        // C00, C02
-        a[22] += e1 * k1; a[23] += e1 * su;                        // C11, C13
-        a[24] += c2 * k0; a[25] += e2 * k1; a[26] += c2 * su; a[27] += e2 * su;  // C2*
-        a[28] += c3 * k0; a[29] += e3 * k1; a[30] += c3 * su; a[31] += e3 * su;  // C3*
-        a[32] += c4 * k0; a[33] += e4 * k1; a[34] += c4 * su; a[35] += e4 * su;  // C4*
-        a[36] += c5 * k0; a[37] += e5 * k1; a[38] += c5 * su; a[39] += e5 * su;  // C5*
-        a[40] += c0 * f[0];
-        a[41] += e1 * f[1];
-        a[42] += c2 * f[0] + e2 * f[1] + h2 * f[2];
-        a[43] += c3 * f[0] + e3 * f[1] + h3 * f[2];
-        a[44] += c4 * f[0] + e4 * f[1] + h4 * f[2];
-        a[45] += c5 * f[0] + e5 * f[1];
+        a[20] += c0 * f[0];
+        a[21] += e1 * f[1];
+        a[22] += c2 * f[0] + e2 * f[1] + h2 * f[2];
+        a[23] += c3 * f[0] + e3 * f[1] + h3 * f[2];
+        a[24] += c4 * f[0] + e4 * f[1] + h4 * f[2];
+        a[25] += c5 * f[0] + e5 * f[1];
     }
-    a[46] += k0 * k0; a[47] += k0 * su; a[48] += k1 * k1; a[49] += k1 * su; a[50] += su * su; a[51] += su * su;
-    a[52] += k0 * f[0]; a[53] += k1 * f[1]; a[54] += su * f[0]; a[55] += su * f[1];
-    a[56] += cost;
+    a[26] += cost;
+}
+__device__ __forceinline__ void cam_accum_c(double* a, const double jc[18], const double jk[8], const double f[3],
+                                            bool cam) {
+    const double c0 = jc[0], c2 = jc[2], c3 = jc[3], c4 = jc[4], c5 = jc[5];
+    const double e1 = jc[7], e2 = jc[8], e3 = jc[9], e4 = jc[10], e5 = jc[11];
+    const double k0 = jk[0], su = jk[2], k1 = jk[5];
+    if (cam) {
+        // C[i][m]: row 0 pairs with jk columns 0, 2; row 1 with 1, 3
+        a[0] += c0 * k0; a[1] += c0 * su;                        // C00, C02
+        a[2] += e1 * k1; a[3] += e1 * su;                        // C11, C13
+        a[4] += c2 * k0; a[5] += e2 * k1; a[6] += c2 * su; a[7] += e2 * su;      // C2*
+        a[8] += c3 * k0; a[9] += e3 * k1; a[10] += c3 * su; a[11] += e3 * su;    // C3*
+        a[12] += c4 * k0; a[13] += e4 * k1; a[14] += c4 * su; a[15] += e4 * su;  // C4*
+        a[16] += c5 * k0; a[17] += e5 * k1; a[18] += c5 * su; a[19] += e5 * su;  // C5*
+    }
+    a[20] += k0 * k0; a[21] += k0 * su; a[22] += k1 * k1; a[23] += k1 * su; a[24] += su * su; a[25] += su * su;
+    a[26] += k0 * f[0]; a[27] += k1 * f[1]; a[28] += su * f[0]; a[29] += su * f[1];
+}
+__device__ __forceinline__ void cam_accum(double* a, const double jc[18], const double jk[8],
+                                          const double f[3], double cost, bool cam) {
+    double u[CAM_NZ_U], cc[CAM_NZ_C];
+#pragma unroll
+    for (int i = 0; i < CAM_NZ_U; ++i) u[i] = a[cam_nz_u_index(i)];
+#pragma unroll
+    for (int i = 0; i < CAM_NZ_C; ++i) cc[i] = a[cam_nz_c_index(i)];
+    cam_accum_u(u, jc, f, cost, cam);
+    cam_accum_c(cc, jc, jk, f, cam);
+#pragma unroll
+    for (int i = 0; i < CAM_NZ_U; ++i) a[cam_nz_u_index(i)] = u[i];
+#pragma unroll
+    for (int i = 0; i < CAM_NZ_C; ++i) a[cam_nz_c_index(i)] = cc[i];
 }
 // Expand the packed sums into the CAMDATA (U 21 | C 24 | g 6) and SEGINTR (Ukk 10 | gk 4 | cost)
 // layouts: element e of [camdata | segintr] (66 values) from the packed array p.

@@ -214,6 +214,28 @@ static constexpr double SC_BAD_TIMEOUT = 8.0;
 // per-iteration log row: cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius, accepted
 static constexpr int LOG_W = 8;
 
+// Small windows (ba_small.hip): the whole solve in one resident workgroup, the reduced system in LDS.
+// Eligible when npad <= SMALL_NPAD (<= 15 active cameras) and the observation / pair-entry counts stay
+// below the caps; the reference's TUM windows (10-keyframe windows, main.cpp:163-168) are of this size.
+static constexpr int SMALL_NPAD = 96;
+static constexpr int SMALL_MAX_OBS = 32768;
+static constexpr int SMALL_MAX_ENTRIES = 262144;
+static constexpr int SMALL_TPB = 512;
+struct SmallWork {
+    double* wc;   // [n_adm][18] W_o = Jc^T Jp (unscaled) of the last linearisation, point-major obs order
+    double* zb;   // [n_adm][18] Z_o = W~_o G^T of the current step (W~ = s_c W_o s_p, G = chol(V~)^-1)
+    double* pv;   // [n_ap][21] undamped point sums of the last linearisation: V packed (6) | e (3) | Kt (12)
+    double* zk;   // [n_ap][15] Zk = K~ G^T (12) | ze = G e~ (3) of the current step
+    // Schur tasks (one wave each): kind 0 = camera-pair block (a, b), a >= b, entries = ordered observation
+    // pairs (u, v) of one point with ac_u = a, ac_v = b (both orders when a == b and u != v); kind 1 =
+    // border of camera a (S_ka, rhs_a), entries (u, u) over the camera's observations
+    const int4* task;   // (a, b, kind, first entry)
+    const int* task_end;  // one past the last entry of each task
+    const int2* entry;
+    int n_task;
+    int on;  // this window runs the small-window path
+};
+
 struct DevWork {
     double* camdata;
     double* seg_intr;
@@ -248,18 +270,19 @@ struct DevWork {
     // nullptr: the tiles flush with f64 atomics
     double* det_tbuf = nullptr;
     const int2* det_trange = nullptr;
+    SmallWork sm{};
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
     K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
-    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_COUNT
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_SMALL, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
     "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
-    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy"};
+    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy", "small_solve"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {
@@ -305,6 +328,11 @@ int bcr_persist_ok(int nblk);
 hipError_t bcr_set_spin_limit(unsigned limit);
 // workgroups of k_schur_tile resident at once on the current device (CUs x blocks per CU)
 int schur_tile_slots();
+// Small windows (W.sm.on): iteration 0 and the whole LM loop in ONE launch of one workgroup
+// (ba_small.hip); the decisions land in W.st / W.log as with the multi-launch path.
+hipError_t launch_small(const DevProblem& P, const BaConsts& c, const LmParams& prm, int jacobi, DevWork& W,
+                        hipStream_t s, Prof* pf);
+size_t small_lds_bytes(int npad);
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s);
 

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "ba_common.h"
 #include "ba_device.h"
 #include "ba_kernels.h"
 
@@ -33,14 +34,6 @@ namespace miba {
 
 static constexpr int TPB = 256;
 
-// ---------------------------------------------------------------- reductions
-template <int NV>
-__device__ __forceinline__ void wave_sum(double (&v)[NV]) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
-}
 
 // Block (256 threads) sum of NV values; result valid in out[0..NV) after return (LDS).
 template <int NV>
@@ -56,36 +49,6 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* lds /*4*NV*/,
     __syncthreads();
 }
 
-// Wave reduce-scatter by recursive halving: at the step with lane offset OFF a lane keeps
-// one half of its N running sums (chosen by lane bit OFF) and adds its partner's copy of
-// that half, so N values cost N/2 + N/4 + ... shuffles instead of 6 N. Afterwards lane l
-// holds the wave sums of indices [base, base + len).
-template <int N, int OFF>
-struct WaveHalve {
-    static __device__ __forceinline__ void run(double* v, int lane, int& base, int& len) {
-        constexpr int H = (N + 1) / 2;
-        const bool hi = (lane & OFF) != 0;
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-            const double a = v[i];
-            const double b = (i + H < N) ? v[i + H] : 0.0;
-            const double keep = hi ? b : a;
-            const double send = hi ? a : b;
-            v[i] = keep + __shfl_xor(send, OFF);
-        }
-        if (hi) { base += H; len = len - H; } else { len = len < H ? len : H; }
-        WaveHalve<H, OFF / 2>::run(v, lane, base, len);
-    }
-};
-template <int N>
-struct WaveHalve<N, 0> {
-    static constexpr int kRemain = N;
-    static __device__ __forceinline__ void run(double*, int, int&, int&) {}
-};
-template <int N, int OFF>
-struct HalveRemain { static constexpr int value = HalveRemain<(N + 1) / 2, OFF / 2>::value; };
-template <int N>
-struct HalveRemain<N, 0> { static constexpr int value = N; };
 
 // Block (256 threads) sum of NV values via the wave reduce-scatter; out[0..NV) valid after return.
 // lds must hold 4 * NV doubles. Fixed summation order (deterministic).
@@ -104,35 +67,6 @@ __device__ __forceinline__ void block_sum_rs(double (&v)[NV], double* lds, doubl
     __syncthreads();
 }
 
-// NW-wave variants (k_final runs 16 waves); lds holds NW * NV doubles. Wave sums added in wave order.
-template <int NW, int NV>
-__device__ __forceinline__ void block_sum_nw(double (&v)[NV], double* lds, double* out) {
-    wave_sum<NV>(v);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0)
-#pragma unroll
-        for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
-    __syncthreads();
-    if (threadIdx.x < NV) {
-        double a = lds[threadIdx.x];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) a += lds[w * NV + threadIdx.x];
-        out[threadIdx.x] = a;
-    }
-    __syncthreads();
-}
-template <int NW>
-__device__ __forceinline__ double block_max_nw(double v, double* lds) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double r = lds[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) r = fmax(r, lds[w]);
-    __syncthreads();
-    return r;
-}
 
 __device__ __forceinline__ double block_max(double v, double* lds) {
 #pragma unroll
@@ -348,56 +282,6 @@ __global__ __launch_bounds__(TPB) void k_lin_finalize(DevProblem P, BaConsts c, 
     }
 }
 
-// ---------------------------------------------------------------- point side
-// G = L^-1 of the damped point block, packed lower (g00 g10 g11 g20 g21 g22).
-__device__ __forceinline__ void zk_ze(const double G[6], const double Ks[12], const double es[3], double Zk[12],
-                                      double ze[3]) {
-    // Zk[m][k] = sum_{i<=k} K[m][i] G[k][i] ; ze[k] = sum_{i<=k} G[k][i] e[i]
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        Zk[m * 3 + 0] = Ks[m * 3 + 0] * G[0];
-        Zk[m * 3 + 1] = Ks[m * 3 + 0] * G[1] + Ks[m * 3 + 1] * G[2];
-        Zk[m * 3 + 2] = Ks[m * 3 + 0] * G[3] + Ks[m * 3 + 1] * G[4] + Ks[m * 3 + 2] * G[5];
-    }
-    ze[0] = G[0] * es[0];
-    ze[1] = G[1] * es[0] + G[2] * es[1];
-    ze[2] = G[3] * es[0] + G[4] * es[1] + G[5] * es[2];
-}
-// V~^-1 = G^T G (full 3x3)
-__device__ __forceinline__ void vinv_from_g(const double* G, double Vf[9]) {
-    const double g00 = G[0], g10 = G[1], g11 = G[2], g20 = G[3], g21 = G[4], g22 = G[5];
-    Vf[0] = g00 * g00 + g10 * g10 + g20 * g20;
-    Vf[1] = g10 * g11 + g20 * g21;
-    Vf[2] = g20 * g22;
-    Vf[4] = g11 * g11 + g21 * g21;
-    Vf[5] = g21 * g22;
-    Vf[8] = g22 * g22;
-    Vf[3] = Vf[1]; Vf[6] = Vf[2]; Vf[7] = Vf[5];
-}
-// W~ (6x3) = s_c (Jc^T Jp) s_p  for one observation
-__device__ __forceinline__ void w_tilde(const double jc[18], const double jp[9], const double* sc, const double* sp,
-                                        double W[18]) {
-    // structural zeros of jc skipped (cam_accum, ba_device.h): rows 0 / 1 / 2 have 5 / 5 / 3 nonzeros
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const double p0 = jp[i], p1 = jp[3 + i], p2 = jp[6 + i];
-        double w[6];
-        w[0] = jc[0] * p0;
-        w[1] = jc[7] * p1;
-        w[2] = jc[2] * p0 + jc[8] * p1 + jc[14] * p2;
-        w[3] = jc[3] * p0 + jc[9] * p1 + jc[15] * p2;
-        w[4] = jc[4] * p0 + jc[10] * p1 + jc[16] * p2;
-        w[5] = jc[5] * p0 + jc[11] * p1;
-#pragma unroll
-        for (int d = 0; d < 6; ++d) W[d * 3 + i] = sc[d] * w[d] * sp[i];
-    }
-}
-// J_c v for the three rows (structural zeros skipped)
-__device__ __forceinline__ void jc_times(const double jc[18], const double v[6], double out[3]) {
-    out[0] = jc[0] * v[0] + jc[2] * v[2] + jc[3] * v[3] + jc[4] * v[4] + jc[5] * v[5];
-    out[1] = jc[7] * v[1] + jc[8] * v[2] + jc[9] * v[3] + jc[10] * v[4] + jc[11] * v[5];
-    out[2] = jc[14] * v[2] + jc[15] * v[3] + jc[16] * v[4];
-}
 // mode 0: column norms only (iteration 0, before the Jacobi scale exists)
 // mode 1: full Schur preparation.
 // pdata[ap*PDATA]: G = chol(V~)^-1 packed (6), e~ (3), K~ (12, [m][i]), D~ (3)
@@ -425,22 +309,6 @@ __device__ __forceinline__ double cam_sum(const DevProblem& P, const double* __r
     }
     return acc;
 }
-// The camera's share of the gradient max-norm ||x - Plus(x, -g)||_inf (Ceres 2.0 trust_region_minimizer).
-__device__ __forceinline__ double cam_gmax(const DevProblem& P, int cur, int ac, const double* g) {
-    const double* x = P.cams[cur] + 7 * P.ac_cam[ac];
-    double ng[6], tp[7];
-#pragma unroll
-    for (int d = 0; d < 6; ++d) ng[d] = -g[d];
-    se3_plus(x, ng, tp);
-    double gm = 0.0;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) gm = fmax(gm, fabs(x[j] - tp[j]));
-    return gm;
-}
-// Max-accumulate a non-negative double (its bit pattern orders like its value).
-__device__ __forceinline__ void atomic_max_nonneg(double* p, double v) {
-    atomicMax((unsigned long long*)p, (unsigned long long)__double_as_longlong(v));
-}
 // The intrinsics partials of all sub-segments in a fixed order (strided per thread, then block_sum).
 __device__ void intr_sums(const DevProblem& P, const double* __restrict__ seg_intr, double* lds, double* out) {
     double acc[SEGINTR];
@@ -450,27 +318,6 @@ __device__ void intr_sums(const DevProblem& P, const double* __restrict__ seg_in
 #pragma unroll
         for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)sg * SEGINTR + i];
     block_sum<SEGINTR>(acc, lds, out);
-}
-// From the summed intrinsics partials out[SEGINTR] and the IntrinsicsPrior block (OptimizationUtils.cpp:
-// 117-125, squared loss): lin16[0] = cost, lin16[2..12) = Ukk packed (+ prior), lin16[12..16) = gk (+ prior);
-// returns the intrinsics' gradient max-norm term.
-__device__ double intr_lin(const DevProblem& P, const BaConsts& c, const double* K, const double* out, double* lin16) {
-    double pc = 0.0, gm = 0.0;
-    double gk[4];
-    for (int m = 0; m < 4; ++m) {
-        const double fk = c.sw_k * (P.prior[m] - K[m]);
-        pc += fk * fk;
-        gk[m] = out[10 + m] + (-c.sw_k) * fk;
-        gm = fmax(gm, fabs(K[m] - (K[m] + -gk[m])));
-    }
-    lin16[0] = out[14] + 0.5 * pc;
-    for (int q = 0; q < 10; ++q) lin16[2 + q] = out[q];
-    int q = 0;
-    for (int m = 0; m < 4; ++m)
-        for (int l = m; l < 4; ++l, ++q)
-            if (l == m) lin16[2 + q] += c.sw_k * c.sw_k;
-    for (int m = 0; m < 4; ++m) lin16[12 + m] = gk[m];
-    return gm;
 }
 
 // ---------------------------------------------------------------- envelope assembly
@@ -594,76 +441,6 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
              lin_w);
 }
 
-// Point tail of the Schur preparation, from the point's sums acc = V packed (6) | e (3) | Kt (12):
-// gradient max-norm term, scaled + LM-damped V~, G = chol(V~)^-1, e~, K~, D~ -> rec[PDATA]; with
-// want_kk also the intrinsics Schur terms -Zk Zk^T (10 packed), -Zk ze (4) -> kk.
-__device__ __forceinline__ void point_tail(const DevProblem& P, const BaConsts& c, double radius,
-                                           const double* __restrict__ scale, int ap, const double* X,
-                                           const double* acc, bool want_kk, double* rec, double* kk, double& gmax,
-                                           double& bad) {
-    const double* V = acc;
-    const double* e = acc + 6;
-    const double* Kt = acc + 9;
-    // gradient max-norm contribution (points: x - (x + -g))
-#pragma unroll
-    for (int i = 0; i < 3; ++i) gmax = fmax(gmax, fabs(X[i] - (X[i] + -e[i])));
-    const double* sp = scale + P.off_pt + 3 * ap;
-    const double* sk = scale + P.off_k;
-    const double s0 = sp[0], s1 = sp[1], s2 = sp[2];
-    // scaled, damped V  (Ceres: lm_diagonal = sqrt(clamp(diag(JtJ~)) / radius))
-    double v00 = s0 * V[0] * s0, v01 = s0 * V[1] * s1, v02 = s0 * V[2] * s2;
-    double v11 = s1 * V[3] * s1, v12 = s1 * V[4] * s2, v22 = s2 * V[5] * s2;
-    rec[21] = fmin(fmax(v00, c.min_diag), c.max_diag) / radius;  // D~ (model cost change, k_backsub_chunk)
-    rec[22] = fmin(fmax(v11, c.min_diag), c.max_diag) / radius;
-    rec[23] = fmin(fmax(v22, c.min_diag), c.max_diag) / radius;
-    v00 += rec[21];
-    v11 += rec[22];
-    v22 += rec[23];
-    // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
-#pragma unroll
-    for (int i = 0; i < 6; ++i) rec[i] = 0.0;  // g00 g10 g11 g20 g21 g22
-    const bool pd = v00 > 0.0;
-    const double L00 = sqrt(v00);
-    const double L10 = v01 / L00, L20 = v02 / L00;
-    const double l11 = v11 - L10 * L10;
-    const double L11 = sqrt(l11);
-    const double L21 = (v12 - L20 * L10) / L11;
-    const double l22 = v22 - L20 * L20 - L21 * L21;
-    const double L22 = sqrt(l22);
-    if (pd && l11 > 0.0 && l22 > 0.0 && isfinite(l22)) {
-        const double i00 = 1 / L00, i11 = 1 / L11, i22 = 1 / L22;
-        rec[0] = i00;
-        rec[1] = -L10 * i00 * i11;
-        rec[2] = i11;
-        rec[4] = -L21 * i11 * i22;
-        rec[3] = -(L20 * i00 + L21 * rec[1]) * i22;
-        rec[5] = i22;
-    } else {
-        bad = 1.0;
-    }
-    const double* G = rec;
-    double* es = rec + 6;
-    double* Ks = rec + 9;
-    es[0] = s0 * e[0]; es[1] = s1 * e[1]; es[2] = s2 * e[2];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        Ks[m * 3 + 0] = sk[m] * Kt[m * 3 + 0] * s0;
-        Ks[m * 3 + 1] = sk[m] * Kt[m * 3 + 1] * s1;
-        Ks[m * 3 + 2] = sk[m] * Kt[m * 3 + 2] * s2;
-    }
-    if (want_kk) {  // intrinsics Schur terms once per point: -Zk Zk^T (10 packed), -Zk ze (4)
-        double Zk[12], ze[3];
-        zk_ze(G, Ks, es, Zk, ze);
-        int qq = 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int l = m; l < 4; ++l, ++qq)
-                kk[qq] = -(Zk[m * 3 + 0] * Zk[l * 3 + 0] + Zk[m * 3 + 1] * Zk[l * 3 + 1] + Zk[m * 3 + 2] * Zk[l * 3 + 2]);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) kk[10 + m] = -(Zk[m * 3 + 0] * ze[0] + Zk[m * 3 + 1] * ze[1] + Zk[m * 3 + 2] * ze[2]);
-    }
-}
 // Workgroups >= nb_pp assemble the envelope tiles of S (env_tile; independent of the point records),
 // so the assembly needs no launch of its own.
 template <int PP_LANES>
@@ -1462,45 +1239,7 @@ struct BandLds {
 };
 static constexpr int BAND_MAX_NB = 2048;                // fcol staged in LDS (nb <= 2048)
 
-// Diagnostic stamps (separate build via STAMP=true, MIBA_CHOL_STAMPS=1): cycles per phase
-// accumulated by thread 0: [0] prefetch issue, [1] trsm, [2] update || look-ahead potrf, [3] retire/install,
-// [4] tail+backward.
-// uniform broadcast of lane `l`'s double (v_readlane, no LDS round trip)
-__device__ __forceinline__ double bcast(double v, int l) {
-    const unsigned long long u = __double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-// 1/sqrt(x) to full f64 precision: v_rsq_f64 + two Newton steps
-__device__ __forceinline__ double rsqrt_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    y = y * (1.5 - 0.5 * x * y * y);
-    y = y * (1.5 - 0.5 * x * y * y);
-    return y;
-}
 
-// In-register 16x16 Cholesky by one wave: lane r (r < 16; replicated above) holds row r.
-// Entries above the diagonal are scratch (never consumed; masked at write-back), so the
-// rank-1 updates run unpredicated. rdiag[j] = 1 / L_jj.
-__device__ __forceinline__ void potrf16_regs(double (&a)[16], double* rdiag, int lane, bool& bad) {
-    const int r = lane & 15;
-    double my_inv = 0.0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        double djj = bcast(a[j], j);
-        const bool ok = (djj > 0.0) && (djj < INFINITY);
-        bad = bad || !ok;
-        djj = ok ? djj : 1.0;
-        const double inv = rsqrt_nr(djj);
-        const double lrj = a[j] * inv;  // lane j: sqrt(d_jj); lanes r > j: L_rj
-        a[j] = lrj;
-        my_inv = (r == j) ? inv : my_inv;
-#pragma unroll
-        for (int k = j + 1; k < 16; ++k) a[k] -= lrj * bcast(lrj, k);
-    }
-    if (lane < 16) rdiag[r] = my_inv;
-}
 
 template <int W, bool STAMP>
 __global__ __launch_bounds__(TPB) void k_chol_band(const LmState* __restrict__ st, double* __restrict__ A, int npad, int nb,
@@ -1971,8 +1710,6 @@ __global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st
 // k_assemble + the chol_flag memset (same values as k_assemble, element for element).
 
 // ---------------------------------------------------------------- final
-__device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
-                               const double* __restrict__ scal, double* __restrict__ log);
 // scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]; then the LM decision (k_lm_decide's
 // body, fused: one launch less per iteration)
 // 4 waves (16 measured 1 us slower at C4: more waves to start and to reduce than loads saved)
@@ -2154,116 +1891,6 @@ __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* 
                                    __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-}
-
-// One thread: Ceres 2.0 TrustRegionMinimizer::Minimize bookkeeping for the step whose
-// scalars k_final produced (model cost change, candidate cost, |step|, |x_cand|, flags).
-// Same decisions, in the same order, as oracle_solve() (oracle/ba_oracle.c).
-static __device__ void lm_decide_core(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
-                                      const double* __restrict__ scal, double* __restrict__ log);
-__device__ void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
-                               const double* __restrict__ scal, double* __restrict__ log) {
-    if (st->done) return;
-    lm_decide_core(st, prm, lin, scal, log);
-    LmState& S = *st;
-    S.n_decide += 1;
-    S.stop_next = !S.done && S.iter >= prm.max_iter;
-    if (prm.progress)
-        __hip_atomic_store(prm.progress, (unsigned)S.n_decide | (S.done ? 0x80000000u : 0u), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-}
-static __device__ void lm_decide_core(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
-                                      const double* __restrict__ scal, double* __restrict__ log) {
-    LmState S = *st;
-    if (S.done) return;
-    if (S.need_lin) {  // absorb the re-linearisation of the last accepted point
-        S.need_lin = 0;
-        S.x_cost = lin[0];
-        S.gmax_ci = lin[1];
-        log[S.iter * LOG_W + 0] = S.x_cost;
-        if (!isfinite(S.x_cost)) {
-            S.done = 1; S.termination = 2; S.msg = MSG_EVAL_FAIL;
-            *st = S;
-            return;
-        }
-        S.final_cost = fmin(S.final_cost, S.x_cost);
-    }
-    const double gmax = fmax(S.gmax_ci, scal[SC_GMAX_PT]);
-    log[S.iter * LOG_W + 2] = gmax;
-    // FinalizeIterationAndCheckIfMinimizerCanContinue
-    if (S.iter >= prm.max_iter) {
-        S.done = 1; S.termination = 1; S.msg = MSG_MAX_ITER; S.msg_a = S.iter;
-    } else if (S.step_ok && gmax <= prm.gradient_tolerance) {
-        S.done = 1; S.termination = 0; S.msg = MSG_GRAD_TOL; S.msg_a = gmax; S.msg_b = prm.gradient_tolerance;
-    } else if (S.radius <= prm.min_radius) {
-        S.done = 1; S.termination = 0; S.msg = MSG_MIN_RADIUS; S.msg_a = S.radius; S.msg_b = prm.min_radius;
-    }
-    if (S.done) { *st = S; return; }
-    S.iter += 1;
-    double* lg = log + S.iter * LOG_W;
-    if (scal[SC_BAD] >= SC_BAD_TIMEOUT) {  // a BCR hand-off timed out: no valid step; end the solve loudly
-        S.n_unsucc += 1;
-        S.done = 1; S.termination = 2; S.msg = MSG_TIMEOUT;
-        lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
-        *st = S;
-        return;
-    }
-    const double mcc = scal[SC_MCC];
-    const bool lsf = scal[SC_BAD] >= 2.0;  // linear solver failure (point block or Cholesky not PD)
-    const bool valid = !lsf && isfinite(mcc) && mcc > 0.0;
-    if (!valid) {  // HandleInvalidStep
-        S.n_unsucc += 1;
-        if (++S.n_invalid >= prm.max_invalid) {
-            S.done = 1; S.termination = 2; S.msg = MSG_INVALID; S.msg_a = prm.max_invalid;
-        } else {
-            S.radius /= S.decrease_factor;
-            S.decrease_factor *= 2.0;
-            S.step_ok = 0;
-        }
-        lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
-        *st = S;
-        return;
-    }
-    S.n_invalid = 0;
-    double cand = scal[SC_CAND];
-    if (scal[SC_BAD] >= 1.0 || !isfinite(cand)) cand = DBL_MAX;
-    const double step_norm = sqrt(scal[SC_SN2]);
-    const double xnorm = sqrt(S.xnorm2);
-    const double cost_change = S.x_cost - cand;
-    if (step_norm <= prm.parameter_tolerance * (xnorm + prm.parameter_tolerance)) {
-        S.done = 1; S.termination = 0; S.msg = MSG_PARAM_TOL;
-        S.msg_a = step_norm / (xnorm + prm.parameter_tolerance); S.msg_b = prm.parameter_tolerance;
-    } else if (fabs(cost_change) <= prm.function_tolerance * S.x_cost) {
-        S.done = 1; S.termination = 0; S.msg = MSG_FUNC_TOL;
-        S.msg_a = fabs(cost_change) / S.x_cost; S.msg_b = prm.function_tolerance;
-    }
-    if (S.done) {
-        lg[0] = cand; lg[1] = cost_change; lg[3] = step_norm; lg[4] = 0.0; lg[5] = S.radius; lg[6] = -1.0;
-        *st = S;
-        return;
-    }
-    const double rho = (cand >= DBL_MAX) ? -DBL_MAX : cost_change / mcc;
-    if (rho > prm.min_relative_decrease) {  // HandleSuccessfulStep + LM StepAccepted
-        S.cur ^= 1;
-        S.need_lin = 1;
-        S.xnorm2 = scal[SC_XN2];
-        const double t = 2.0 * rho - 1.0;
-        S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - t * t * t);
-        S.radius = fmin(prm.max_radius, S.radius);
-        S.decrease_factor = 2.0;
-        S.step_ok = 1;
-        S.n_succ += 1;
-        lg[0] = cand; lg[6] = 1.0;  // cost re-evaluated at absorb time
-    } else {  // HandleUnsuccessfulStep + LM StepRejected
-        S.radius /= S.decrease_factor;
-        S.decrease_factor *= 2.0;
-        S.step_ok = 0;
-        S.n_unsucc += 1;
-        S.final_cost = fmin(S.final_cost, cand);
-        lg[0] = cand; lg[6] = 0.0;
-    }
-    lg[1] = cost_change; lg[3] = step_norm; lg[4] = rho; lg[5] = S.radius;
-    *st = S;
 }
 
 __global__ void k_lm_decide(LmState* __restrict__ st, LmParams prm, const double* __restrict__ lin,

@@ -61,6 +61,7 @@ enum BufId {
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
     B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_ENV_GLOB, B_RED, B_PREP, B_BS_CHUNK, B_AC_SEG, B_CAMPART, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_DET_TRANGE,
+    B_SM_WC, B_SM_ZB, B_SM_PV, B_SM_ZK, B_SM_TASK, B_SM_TEND, B_SM_ENTRY,
     B_COUNT
 };
 
@@ -193,6 +194,7 @@ void ba_default_options(ba_options* o) {
     o->device = -1;
     o->deterministic = 0;
     o->shard_min_obs = 262144;
+    o->small_window = 0;
 }
 
 ba_context* ba_create(const ba_options* opts) {
@@ -749,6 +751,65 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         else if (!std::strcmp(e, "bcr") && cam_band < BCR_CAMS && bcr_nblk >= 2) P.solver = 2;
     }
     if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
+    // small windows: the whole solve in one workgroup (ba_small.hip), unless a solver is forced
+    const char* e_small = std::getenv("MIBA_SMALL");
+    const bool small = !shard && o.small_window && npad <= SMALL_NPAD && n_adm <= SMALL_MAX_OBS &&
+                       !std::getenv("MIBA_SOLVER") && !std::getenv("MIBA_DENSE_CHOL") && !(e_small && e_small[0] == '0');
+    ctx->W.sm.on = 0;
+    if (small) {
+        // Schur tasks: camera-pair blocks (a >= b) over the ordered observation pairs of each point, and
+        // each camera's border rows over its observations (point-major obs indices, point order)
+        std::vector<std::vector<int2>> blk((size_t)nac * nac), brd(nac);
+        size_t n_entries = 0;
+        for (int a = 0; a < n_ap && n_entries <= (size_t)SMALL_MAX_ENTRIES; ++a)
+            for (int q = pt_ptr[a]; q < pt_ptr[a + 1]; ++q) {
+                const int ai = po_ac[q];
+                if (ai < 0) continue;
+                brd[ai].push_back(make_int2(q, q));
+                for (int r = pt_ptr[a]; r < pt_ptr[a + 1]; ++r) {
+                    const int aj = po_ac[r];
+                    if (aj < 0 || aj > ai) continue;
+                    blk[(size_t)ai * nac + aj].push_back(make_int2(q, r));
+                    ++n_entries;
+                }
+                ++n_entries;
+            }
+        if (n_entries <= (size_t)SMALL_MAX_ENTRIES) {
+            struct T { int a, b, kind; const std::vector<int2>* e; };
+            std::vector<T> tasks;
+            for (int a = 0; a < nac; ++a)
+                for (int b = 0; b <= a; ++b)
+                    if (!blk[(size_t)a * nac + b].empty()) tasks.push_back({a, b, 0, &blk[(size_t)a * nac + b]});
+            for (int a = 0; a < nac; ++a)
+                if (!brd[a].empty()) tasks.push_back({a, a, 1, &brd[a]});
+            std::vector<int4> tk;
+            std::vector<int> tend;
+            std::vector<int2> ent;
+            for (const T& t : tasks) {
+                tk.push_back(make_int4(t.a, t.b, t.kind, (int)ent.size()));
+                ent.insert(ent.end(), t.e->begin(), t.e->end());
+                tend.push_back((int)ent.size());
+            }
+            HIPCHECK(ctx, upload(ctx, B_SM_TASK, tk.data(), tk.size()));
+            HIPCHECK(ctx, upload(ctx, B_SM_TEND, tend.data(), tend.size()));
+            HIPCHECK(ctx, upload(ctx, B_SM_ENTRY, ent.data(), ent.size()));
+            HIPCHECK(ctx, ctx->buf[B_SM_WC].ensure(sizeof(double) * 18 * std::max(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_SM_ZB].ensure(sizeof(double) * 18 * std::max(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_SM_PV].ensure(sizeof(double) * 21 * std::max(n_ap, 1)));
+            HIPCHECK(ctx, ctx->buf[B_SM_ZK].ensure(sizeof(double) * 15 * std::max(n_ap, 1)));
+            SmallWork& Z = ctx->W.sm;
+            Z.wc = ctx->buf[B_SM_WC].as<double>();
+            Z.zb = ctx->buf[B_SM_ZB].as<double>();
+            Z.pv = ctx->buf[B_SM_PV].as<double>();
+            Z.zk = ctx->buf[B_SM_ZK].as<double>();
+            Z.task = ctx->buf[B_SM_TASK].as<int4>();
+            Z.task_end = ctx->buf[B_SM_TEND].as<int>();
+            Z.entry = ctx->buf[B_SM_ENTRY].as<int2>();
+            Z.n_task = (int)tk.size();
+            Z.on = 1;
+            P.solver = BA_LS_SMALL;
+        }
+    }
     if (P.solver == 2) {
         const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 6 * bcr_nblk);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
@@ -1024,10 +1085,12 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     prm.progress = ctx->dprog;
     if (ctx->hprog) __atomic_store_n(ctx->hprog, 0u, __ATOMIC_RELEASE);
 
-    // IterationZero: cost, gradient, column norms -> Jacobi scale, |x|
-    HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
-    HIPCHECK(ctx, launch_scale(P, C, o.jacobi_scaling, W, s, pf));
-    HIPCHECK(ctx, launch_init_state(P, W, ctx->hprog ? ctx->dprog : nullptr, s, pf));
+    // IterationZero: cost, gradient, column norms -> Jacobi scale, |x| (the small-window kernel does its own)
+    if (!W.sm.on) {
+        HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
+        HIPCHECK(ctx, launch_scale(P, C, o.jacobi_scaling, W, s, pf));
+        HIPCHECK(ctx, launch_init_state(P, W, ctx->hprog ? ctx->dprog : nullptr, s, pf));
+    }
     // LM iterations: fixed launch sequence, device-side decisions; the host follows the device.
     // Iterations enqueued after the termination are no-ops (their kernels exit at once).
     int launched = 0;
@@ -1042,7 +1105,15 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         ++launched;
         return BA_OK;
     };
-    if (!pf && ctx->hprog) {
+    if (W.sm.on) {
+        // small window: iteration 0 and the whole LM loop in one launch (ba_small.hip)
+        LmParams ps = prm;
+        ps.progress = nullptr;
+        HIPCHECK(ctx, launch_small(P, C, ps, o.jacobi_scaling, W, s, pf));
+        HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
+        HIPCHECK(ctx, hipStreamSynchronize(s));
+        flush_prof(ctx);
+    } else if (!pf && ctx->hprog) {
         // Unprofiled: keep LM_AHEAD iterations in flight and follow the device through the host-mapped
         // progress word (n_decide | done << 31, written by every decision and by a failed initial
         // evaluation) instead of synchronising the stream per batch: the GPU never waits for the host.

@@ -55,7 +55,8 @@ class BaOptions(C.Structure):
         ("profile_kernels", C.c_int32),
         ("profile_mask", C.c_int32),
         ("shard_min_obs", C.c_int32),
-        ("reserved", C.c_int32 * 3),
+        ("small_window", C.c_int32),
+        ("reserved", C.c_int32 * 2),
     ]
 
 
@@ -148,6 +149,7 @@ def default_options_py() -> BaOptions:
     o.device = -1
     o.deterministic = 0  # = ba_default_options
     o.shard_min_obs = 262144
+    o.small_window = 0
     return o
 
 

@@ -42,7 +42,8 @@ def test_defaults_equal_oracle_defaults(L):
     a = BaOptions(); L.ba_default_options(C.byref(a))
     b = oracle.default_options()
     for name, _ in BaOptions._fields_:
-        if name in ("minimizer_progress_to_stdout", "deterministic", "profile_kernels", "profile_mask", "reserved"):
+        if name in ("minimizer_progress_to_stdout", "deterministic", "profile_kernels", "profile_mask", "small_window",
+                    "reserved"):
             continue
         assert getattr(a, name) == getattr(b, name), name
     assert a.minimizer_progress_to_stdout == 1  # BundleAdjustmentConfig.h:63
