@@ -737,6 +737,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
                                                     int nblk_pt, const double* __restrict__ part,
                                                     double* __restrict__ tbuf) {
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
+    __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
     if (skip_step(st)) return;
     if ((int)blockIdx.x == P.n_tiles) {
         // last workgroup: S_kk += the points' intrinsics Schur terms (k_point_prep's per-workgroup partials,
@@ -778,24 +779,32 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     const int base = P.tile_base[tile];
     const int span = P.tile_span[tile];
     const int kr = 6 * span, er = kr + 4;     // intrinsics rows, rhs row of M'
-    const int nrt = (er + 1 + 15) >> 4;        // 16-row tiles of M'
-    const int ntl = nrt * (nrt + 1) / 2;       // lower tiles of M' M'^T
-    // lower tiles in reverse row-major order, 4 consecutive per wave (operand rows shared
-    // within a wave); slots past ntl duplicate tile (0,0) and are never flushed
+    // span <= 10 (the common tile: one run of points observed by the same 10 cameras): M' without its rhs
+    // row fits 4 row tiles (60 camera + 4 intrinsics rows), so the MFMA product has 10 lower tiles instead of
+    // 15; the rhs row's products rhs_c -= M'_c ze are a VALU dot product on wave 3 (2 of the 10 tiles)
+    const bool rhs_aside = er <= 64;
+    const int nrt = (er + (rhs_aside ? 0 : 1) + 15) >> 4;  // 16-row tiles of M'
+    const int ntl = nrt * (nrt + 1) / 2;                     // lower tiles of M' M'^T
+    // lower tiles in reverse row-major order, 4 consecutive per wave (operand rows shared within a
+    // wave), or round-robin over the waves when the rhs row is aside (10 tiles: 3, 3, 2, 2); slots past
+    // ntl duplicate tile (0,0) and are never flushed
     int tib[4], tjb[4];
     bool tok[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int u = 4 * wave + q;
+        const int u = rhs_aside ? wave + 4 * q : 4 * wave + q;
         tok[q] = u < ntl;
         int t = tok[q] ? ntl - 1 - u : 0, ib = 0;
         while (t > ib) { t -= ib + 1; ++ib; }
         tib[q] = ib;
         tjb[q] = t;
     }
+    // the valid slots are a prefix; their count is wave-uniform (empty slots issue no MFMA)
+    const int ntok = __builtin_amdgcn_readfirstlane((int)tok[0] + (int)tok[1] + (int)tok[2] + (int)tok[3]);
     d4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    double rhs_acc = 0.0;
     const double* K = P.K[cur];
     // Software pipeline over the tile's chunks: the next chunk's bounds and level-1
     // observation records are loaded before this chunk's MFMAs, its level-2 operands
@@ -859,7 +868,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
                 double* col = Mt + (3 * tid + j) * SCH_LDM;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) col[kr + m] = zk[m * 3 + j];
-                col[er] = z3[j];
+                if (rhs_aside) zeL[3 * tid + j] = z3[j]; else col[er] = z3[j];
             }
         }
         if (o_ok) {
@@ -887,6 +896,11 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             ape_n = P.chunk_ap[ch + 2];
             load_rec(oe + tid);
         }
+        // ---- rhs row aside: rhs_acc(r) += sum_k M'[r][k] ze[k] (wave 3, lane = camera row r), k in order
+        if (rhs_aside && wave == 3 && lane < kr) {
+            const int nk = 3 * npts;
+            for (int k = 0; k < nk; ++k) rhs_acc = __builtin_fma(Mt[k * SCH_LDM + lane], zeL[k], rhs_acc);
+        }
         // ---- phase B: acc[t] += M'[16 ib..][k] M'[16 jb..][k]^T over the chunk's K
         const int ksteps = (3 * npts + 3) >> 2;
         {
@@ -900,7 +914,8 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 #pragma unroll
                 for (int t = 0; t < 4; ++t) { an[t] = nrow[16 * tib[t]]; bn[t] = nrow[16 * tjb[t]]; }
 #pragma unroll
-                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
+                for (int t = 0; t < 4; ++t)
+                    if (t < ntok) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) { a[t] = an[t]; b[t] = bn[t]; }
                 row = nrow;
@@ -929,7 +944,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int r1 = 16 * tib[t] + kq + 4 * g;
-            if (r1 < r2 || r1 > er) continue;
+            if (r1 < r2 || r1 > er || (rhs_aside && r1 == er)) continue;  // aside: wave 3 owns row er
             const double v = -acc[t][g];
             if (tbuf) {  // deterministic mode: the tile's own slab, summed in tile order by k_schur_gather
                 tbuf[(size_t)tile * SCH_TBUF + r1 * SCH_TBUF_LD + r2] = v;
@@ -939,6 +954,11 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             else if (r1 < er) atomicAdd(&S[(size_t)(P.kb + r1 - kr) * ld + g2], v);
             else atomicAdd(&rhs[g2], v);
         }
+    }
+    if (rhs_aside && wave == 3 && lane < kr) {
+        const double v = -rhs_acc;
+        if (tbuf) tbuf[(size_t)tile * SCH_TBUF + er * SCH_TBUF_LD + lane] = v;
+        else atomicAdd(&rhs[6 * base + lane], v);
     }
     if constexpr (STAMP) {
         __syncthreads();
