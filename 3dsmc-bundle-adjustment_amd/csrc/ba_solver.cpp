@@ -1287,6 +1287,27 @@ extern "C" int32_t ba_debug_reduced_system(ba_context* ctx, const ba_problem* p,
     return BA_OK;
 }
 
+extern "C" int32_t ba_debug_camera_sums(ba_context* ctx, const ba_problem* p, int32_t* nac, double* camdata,
+                                        double* lin, int32_t* ac_cam) {
+    if (!ctx) return BA_E_INVALID;
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = prepare(ctx, p);
+    if (rc) return rc;
+    DevProblem& P = ctx->P;
+    hipStream_t s = ctx->stream;
+    if (nac) *nac = P.nac;
+    if (!camdata || !lin) return BA_OK;
+    static thread_local LmState h_st;
+    h_st = fresh_state(ctx->opts, ctx->opts.initial_trust_region_radius);
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->W.st, &h_st, sizeof(LmState), hipMemcpyHostToDevice, s));
+    HIPCHECK(ctx, launch_linearize(P, ctx->C, 0, ctx->W, s, nullptr));
+    HIPCHECK(ctx, hipMemcpyAsync(camdata, ctx->W.camdata, sizeof(double) * CAMDATA * P.nac, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(lin, ctx->W.lin, sizeof(double) * LIN_N, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    if (ac_cam) std::copy(ctx->ac_cam.begin(), ctx->ac_cam.end(), ac_cam);
+    return BA_OK;
+}
+
 extern "C" int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, int32_t max_n) {
     if (!ctx || !out) return 0;
     int n = 0;

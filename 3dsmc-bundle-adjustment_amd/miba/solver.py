@@ -155,6 +155,23 @@ class Solver:
                                                _dptr(jk)), "ba_debug_linearize")
         return dict(cost=float(cost[0]), res=res, jcam=jc, jpt=jp, jint=jk)
 
+    def camera_sums(self, prob: ProblemArrays):
+        """The production camera-side pass (ba_debug_camera_sums): per active camera U (6x6), C (6x4), g (6),
+        the lin record (cost, gradient norm, intrinsics block + prior) and the active camera indices."""
+        ps = prob.struct()
+        n = C.c_int32(0)
+        self._check(self._L.ba_debug_camera_sums(self._h, C.byref(ps), C.byref(n), None, None, None),
+                    "ba_debug_camera_sums")
+        cd = np.zeros((max(n.value, 1), 51)); lin = np.zeros(16); ac = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._check(self._L.ba_debug_camera_sums(self._h, C.byref(ps), C.byref(n), _dptr(cd), _dptr(lin),
+                                                 ac.ctypes.data_as(C.POINTER(C.c_int32))), "ba_debug_camera_sums")
+        cd, ac = cd[: n.value], ac[: n.value]
+        U = np.zeros((n.value, 6, 6))
+        iu = np.triu_indices(6)
+        U[:, iu[0], iu[1]] = cd[:, :21]
+        U[:, iu[1], iu[0]] = cd[:, :21]
+        return dict(U=U, C=cd[:, 21:45].reshape(-1, 6, 4), g=cd[:, 45:51], lin=lin, ac_cam=ac)
+
     def reduced_system(self, prob: ProblemArrays, radius: float = 0.0):
         ps = prob.struct()
         n = C.c_int32(0)

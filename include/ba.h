@@ -246,6 +246,13 @@ int32_t ba_debug_linearize(ba_context* ctx, const ba_problem* prob, double* cost
 int32_t ba_debug_reduced_system(ba_context* ctx, const ba_problem* prob, double radius,
                                 int32_t* n_out, double* S, double* rhs);
 
+/* Test hook: the production camera-side pass (k_cam_side + k_cam_finalize, iteration-0 form) at the
+ * problem's parameters. camdata[nac*51]: per active camera U upper-packed (21) | C 6x4 (24) | g (6);
+ * lin[16]: cost, gradient max-norm of cameras + intrinsics, Ukk packed (10, + IntrinsicsPrior), gk (4,
+ * + prior); ac_cam[nac]: the camera index of each active camera. With NULL outputs only *nac is set. */
+int32_t ba_debug_camera_sums(ba_context* ctx, const ba_problem* prob, int32_t* nac, double* camdata,
+                             double* lin, int32_t* ac_cam);
+
 #ifdef __cplusplus
 }
 #endif

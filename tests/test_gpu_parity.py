@@ -47,6 +47,35 @@ def test_linearize_parity(solver, case):
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
+def test_camera_side_sums_parity(solver, case):
+    """The production camera-side pass (k_cam_side's packed sums + k_cam_finalize, not the debug kernel):
+    per active camera U = sum Jc^T Jc, C = sum Jc^T Jk, g = sum Jc^T f, and the intrinsics block with the
+    IntrinsicsPrior (OptimizationUtils.cpp:117-125), against sums of the oracle's per-observation
+    Jacobians; 1e-11 relative (summation order only)."""
+    p = synthetic.make_problem(**CASES[case])
+    g = solver.camera_sums(p)
+    r = oracle.linearize(p)
+    jc, jk, f = r["jcam"], r["jint"], r["res"]
+    adm = p.obs_depth > 1e-15
+    assert len(g["ac_cam"]) > 0
+    for a, cam in enumerate(g["ac_cam"]):
+        m = adm & (p.obs_cam == cam)
+        U = np.einsum("nri,nrj->ij", jc[m], jc[m])
+        Cc = np.einsum("nri,nrm->im", jc[m, :2], jk[m])
+        gg = np.einsum("nri,nr->i", jc[m], f[m])
+        assert _rel(g["U"][a], U) <= 1e-11, (case, cam)
+        assert _rel(g["C"][a], Cc) <= 1e-11, (case, cam)
+        assert _rel(g["g"][a], gg) <= 1e-11, (case, cam)
+    w = oracle.default_options().weight_intrinsics
+    Ukk = np.einsum("nrm,nrl->ml", jk[adm], jk[adm]) + w * np.eye(4)
+    gk = np.einsum("nrm,nr->m", jk[adm], f[adm, :2]) - w * (p.intr_prior - p.intr)
+    iu = np.triu_indices(4)
+    assert _rel(g["lin"][2:12], Ukk[iu]) <= 1e-11
+    assert _rel(g["lin"][12:16], gk) <= 1e-11
+    assert abs(g["lin"][0] - r["cost"]) <= 1e-12 * r["cost"]
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
 @pytest.mark.parametrize("radius", [1e4, 3.0])
 def test_reduced_system_parity(solver, case, radius):
     p = synthetic.make_problem(**CASES[case])
