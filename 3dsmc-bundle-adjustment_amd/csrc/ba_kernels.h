@@ -271,18 +271,22 @@ struct DevWork {
     double* det_tbuf = nullptr;
     const int2* det_trange = nullptr;
     SmallWork sm{};
+    // fused LM-loop linearisation (unsharded, default mode): k_lin_point (point side + camera side in one
+    // launch), the envelope tiles as atomic adds inside k_schur_tile onto an S / rhs zeroed by the previous
+    // iteration's k_backsub_chunk / k_final
+    int fused = 0;
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
     K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
-    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_SMALL, K_COUNT
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_SMALL, K_LIN_POINT, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
     "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
-    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy", "small_solve"};
+    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy", "small_solve", "lin_point"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {

@@ -84,17 +84,16 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
 // camera-major observation list; k_cam_finalize sums a camera's sub-segments in order.
 // camdata (per sub-segment partial here): U upper-packed (21), C (6x4 = 24), g (6)
 // seg_intr[s*SEGINTR + ..]: Ukk upper-packed (10), gk (4), cost (1)
-__global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
-                                                  double* __restrict__ camdata, double* __restrict__ seg_intr,
-                                                  double* __restrict__ gmax_word) {
-    // lin[1] is max-accumulated by k_cam_finalize (read only after a linearisation): clear it here,
-    // one kernel boundary ahead, whether or not this iteration linearises
-    if (blockIdx.x == 0 && threadIdx.x == 0) *gmax_word = 0.0;
+__device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
+                                               int gated, double* __restrict__ camdata, double* __restrict__ seg_intr,
+                                               double* __restrict__ gmax_word, const int s) {
+    // lin[1] is max-accumulated by the envelope tiles / k_cam_finalize (read only after a linearisation):
+    // clear it here, one kernel boundary ahead, whether or not this iteration linearises
+    if (s == 0 && threadIdx.x == 0) *gmax_word = 0.0;
     if (st->done || (gated && !st->need_lin)) return;
     const int cur = st->cur;
     __shared__ double lds[4 * CAM_NZ];
     __shared__ double out[CAM_NZ];
-    const int s = blockIdx.x;
     const int cam = P.seg_cam[s];
     const int ac = P.seg_ac[s];
     const double* pose = P.cams[cur] + 7 * cam;
@@ -140,6 +139,11 @@ __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, cons
     if (ac >= 0)
         for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)s * CAMDATA + i] = cam_unpack(out, i);
     for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = cam_unpack(out, CAMDATA + i);
+}
+__global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
+                                                  double* __restrict__ camdata, double* __restrict__ seg_intr,
+                                                  double* __restrict__ gmax_word) {
+    cam_side_block(P, c, st, gated, camdata, seg_intr, gmax_word, blockIdx.x);
 }
 
 // One launch for what follows the camera-side pass (was k_cam_reduce + k_lin_finalize):
@@ -336,7 +340,7 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
                          const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
                          double* __restrict__ rhs, int* __restrict__ chol_flag, int fin,
                          const double* __restrict__ cpart, const double* __restrict__ seg_intr, double* camdata_w,
-                         double* lin_w) {
+                         double* lin_w, bool accumulate = false) {
     __shared__ double cds[4 * CAMDATA];
     __shared__ double l16[LIN_N];
     __shared__ double ilds[4 * SEGINTR];
@@ -414,7 +418,8 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
             v = 1.0;
         }
     }
-    S[(size_t)r * P.npad + col] = v;
+    if (!accumulate) S[(size_t)r * P.npad + col] = v;
+    else if (v != 0.0) atomicAdd(&S[(size_t)r * P.npad + col], v);  // S zeroed by the last back-substitution
     if (ij.x == ij.y && tid < 16) {
         const int rr = 16 * ij.x + tid;
         double b = 0.0;
@@ -422,7 +427,8 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
             if (rr < nd) b = scale[rr] * cd[(size_t)(rr / 6 - ac0) * CAMDATA + 45 + rr % 6];
             else if (rr < kb + 4) b = sk[rr - kb] * linr[12 + rr - kb];
         }
-        rhs[rr] = b;
+        if (!accumulate) rhs[rr] = b;
+        else if (b != 0.0) atomicAdd(&rhs[rr], b);
     }
     if (t == 0 && tid == 0) *chol_flag = 0;
 }
@@ -441,6 +447,10 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
              lin_w);
 }
 
+template <int PP_LANES>
+__device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
+                                                 int mode, const double* __restrict__ scale, double* __restrict__ cnp,
+                                                 double* __restrict__ pdata, double* __restrict__ part, const int b);
 // Workgroups >= nb_pp assemble the envelope tiles of S (env_tile; independent of the point records),
 // so the assembly needs no launch of its own.
 template <int PP_LANES>
@@ -454,19 +464,26 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
                                                        int fin, const double* __restrict__ cpart,
                                                        const double* __restrict__ seg_intr, double* camdata_w,
                                                        double* lin_w) {
-    __shared__ double lds[4 * 14];
-    __shared__ double out[14];
-    __shared__ double red[4];
     if ((int)blockIdx.x >= nb_pp) {
         if (!st->done && (fin || !st->stop_next))
             env_tile(P, c, st, blockIdx.x - nb_pp, tiles, camdata, lin, scale, S, rhs, chol_flag, fin, cpart, seg_intr,
                      camdata_w, lin_w);
         return;
     }
+    point_prep_block<PP_LANES>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
+}
+// Point-side body of k_point_prep for point workgroup b (see k_point_prep).
+template <int PP_LANES>
+__device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
+                                                 int mode, const double* __restrict__ scale, double* __restrict__ cnp,
+                                                 double* __restrict__ pdata, double* __restrict__ part, const int b) {
+    __shared__ double lds[4 * 14];
+    __shared__ double out[14];
+    __shared__ double red[4];
     if (st->done) return;
     const int cur = st->cur;
     const double radius = st->radius;
-    const int gt = blockIdx.x * PP_TPB + threadIdx.x;
+    const int gt = b * PP_TPB + threadIdx.x;
     const int ap = gt / PP_LANES, q = gt % PP_LANES;
     double kk[14];
 #pragma unroll
@@ -551,11 +568,25 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
     bad = block_max(bad, red);
     // intrinsics terms: one partial per workgroup, summed in a fixed order by k_schur_tile's last workgroup (a
     // same-address f64 atomic per workgroup serialises at ~45 ns each: 391 x 14 of them cost ~17 us)
-    if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + blockIdx.x] = out[threadIdx.x];
+    if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + b] = out[threadIdx.x];
     if (threadIdx.x == 0) {
-        part[PART_PT_GMAX * P.part_stride + blockIdx.x] = gmax;
-        part[PART_PT_BAD * P.part_stride + blockIdx.x] = bad;
+        part[PART_PT_GMAX * P.part_stride + b] = gmax;
+        part[PART_PT_BAD * P.part_stride + b] = bad;
     }
+}
+
+// Fused linearisation launch of the LM loop (unsharded, default mode): point workgroups [0, nb_pp) run
+// k_point_prep's point side, the rest k_cam_side's sub-segments (gated on an accepted step). The point
+// side alone is one long dependent chain per thread at ~1.5 waves per SIMD; the camera sub-segments fill
+// the CUs it leaves idle. The envelope tiles, which need the camera sums, ride in k_schur_tile.
+template <int PP_LANES>
+__global__ __launch_bounds__(TPB) void k_lin_point(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                   const double* __restrict__ scale, double* __restrict__ cnp,
+                                                   double* __restrict__ pdata, double* __restrict__ part, int nb_pp,
+                                                   double* __restrict__ cpart, double* __restrict__ seg_intr,
+                                                   double* __restrict__ gmax_word) {
+    if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES>(P, c, st, 1, scale, cnp, pdata, part, blockIdx.x);
+    else cam_side_block(P, c, st, 1, cpart, seg_intr, gmax_word, blockIdx.x - nb_pp);
 }
 
 // Jacobi scale (Ceres: 1 / (1 + sqrt(squared column norm)), iteration 0 only)
@@ -729,15 +760,36 @@ static_assert(SCH_LDM * 6 * TILE_WIN == SCH_TBUF, "deterministic slab geometry")
 static_assert(6 * TILE_WIN + 5 <= SCH_LDM, "M' rows exceed 5 MFMA tiles");
 static_assert(CHUNK_OBS <= TPB, "phase A: one observation per thread");
 
+// Envelope tiles riding in k_schur_tile (fused LM-loop path, n_env > 0): what env_tile needs. They add
+// their values to an S (and rhs) that the previous back-substitution (k_final) zeroed, concurrently with the
+// tiles' flushes, so every writer of S in that launch is an atomic add.
+struct EnvArgs {
+    const int2* tiles;
+    int n_env;
+    const double* camdata;
+    const double* lin;
+    int* chol_flag;
+    const double* cpart;
+    const double* seg_intr;
+    double* camdata_w;
+    double* lin_w;
+};
+
 template <bool STAMP>
 __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
                                                     double* __restrict__ rhs, unsigned long long* __restrict__ stamps,
                                                     int nblk_pt, const double* __restrict__ part,
-                                                    double* __restrict__ tbuf) {
+                                                    double* __restrict__ tbuf, EnvArgs E) {
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
+    if ((int)blockIdx.x > P.n_tiles) {  // envelope tiles (fused path): also in the terminal stop_next iteration
+        if (!st->done)
+            env_tile(P, c, st, blockIdx.x - P.n_tiles - 1, E.tiles, E.camdata, E.lin, scale, S, rhs, E.chol_flag, 1,
+                     E.cpart, E.seg_intr, E.camdata_w, E.lin_w, true);
+        return;
+    }
     if (skip_step(st)) return;
     if ((int)blockIdx.x == P.n_tiles) {
         // last workgroup: S_kk += the points' intrinsics Schur terms (k_point_prep's per-workgroup partials,
@@ -754,9 +806,11 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             int m = 0, q = threadIdx.x;
             while (q >= 4 - m) { q -= 4 - m; ++m; }
             const int l = m + q;  // packed (m, l), l >= m
-            S[(size_t)(P.kb + l) * P.npad + P.kb + m] += out[threadIdx.x];
+            if (E.n_env) atomicAdd(&S[(size_t)(P.kb + l) * P.npad + P.kb + m], out[threadIdx.x]);
+            else S[(size_t)(P.kb + l) * P.npad + P.kb + m] += out[threadIdx.x];
         } else if (threadIdx.x < 14) {
-            rhs[P.kb + threadIdx.x - 10] += out[threadIdx.x];
+            if (E.n_env) atomicAdd(&rhs[P.kb + threadIdx.x - 10], out[threadIdx.x]);
+            else rhs[P.kb + threadIdx.x - 10] += out[threadIdx.x];
         }
         return;
     }
@@ -1605,12 +1659,20 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
 __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                        const double* __restrict__ scale,
                                                        const double* __restrict__ pdata, const double* __restrict__ y,
-                                                       const double* __restrict__ delta, double* __restrict__ part) {
+                                                       const double* __restrict__ delta, double* __restrict__ part,
+                                                       const int2* __restrict__ ztiles, int n_ztiles,
+                                                       double* __restrict__ Sz) {
     __shared__ double co[BS_OBS][3];
     __shared__ double dpl[BS_PTS][3];
     __shared__ double lds[4 * 5];
     __shared__ double out[5];
     if (skip_step(st)) return;
+    // fused path: the reduced solve has consumed S; zero this chunk's share of its envelope tiles for the next
+    // iteration's atomic assembly (k_final zeroes rhs, which still holds y here)
+    for (int t = blockIdx.x * n_ztiles / gridDim.x; t < (blockIdx.x + 1) * n_ztiles / (int)gridDim.x; ++t) {
+        const int2 ij = ztiles[t];
+        Sz[(size_t)(16 * ij.x + (threadIdx.x >> 4)) * P.npad + 16 * ij.y + (threadIdx.x & 15)] = 0.0;
+    }
     const int cur = st->cur;
     const int ch = blockIdx.x, tid = threadIdx.x;
     const int apb = P.bs_chunk[ch], ape = P.bs_chunk[ch + 1];
@@ -1737,11 +1799,14 @@ static constexpr int TPB_F = 256, NW_F = TPB_F / 64;
 __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                                int nblk_bs, const double* __restrict__ part,
                                                const int* __restrict__ chol_flag, double* __restrict__ scal,
-                                               LmParams prm, const double* __restrict__ lin, double* __restrict__ log) {
+                                               LmParams prm, const double* __restrict__ lin, double* __restrict__ log,
+                                               double* __restrict__ rhs_z) {
     __shared__ double lds[NW_F * 4];
     __shared__ double out[4];
     __shared__ double red[NW_F];
     if (st->done) return;
+    if (rhs_z)  // fused path: y has been consumed; rhs is the next assembly's atomic target
+        for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double gm = 0.0, bad = 0.0;
     const size_t stp = P.part_stride;
@@ -2007,6 +2072,7 @@ int schur_tile_slots() {
 }
 
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
+    if (gated && W.fused) return hipSuccess;  // the LM loop's camera side runs inside k_lin_point (launch_build)
     if (P.n_seg > 0)
         PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr,
            W.lin + 1);
@@ -2070,13 +2136,25 @@ hipError_t launch_init_state(const DevProblem& P, DevWork& W, unsigned* progress
 hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
     // point records + intrinsics Schur partials, then the envelope of S: clear + camera / intrinsics
     // blocks, LM diagonal, pad (rank 0 only), the points' intrinsics terms, rhs, chol_flag
-    if (P.n_ap > 0)
+    EnvArgs E{};
+    if (W.fused) {  // point side + gated camera side in one launch; the envelope tiles ride in k_schur_tile
+        const int nb = pp_blocks(P.n_ap);
+        switch (pp_lanes()) {
+            case 1: PL(K_LIN_POINT, k_lin_point<1>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
+                       W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
+            case 2: PL(K_LIN_POINT, k_lin_point<2>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
+                       W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
+            default: PL(K_LIN_POINT, k_lin_point<4>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
+                        W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
+        }
+        E = EnvArgs{W.env_tile, W.n_env, W.camdata, W.lin, W.chol_flag, W.camdata_part, W.seg_intr, W.camdata, W.lin};
+    } else if (P.n_ap > 0)
         CK(launch_point_prep(P, c, 1, W, s, pf));  // + the envelope tiles
     else
         PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin,
            W.scale, W.S, W.rhs, W.chol_flag, W.comm.on() ? 0 : 1, W.camdata_part, W.seg_intr, W.camdata, W.lin);
     // Schur tiles + one workgroup for the intrinsics Schur terms (when there are points)
-    const int n_sch = P.n_tiles + (P.n_ap > 0 ? 1 : 0);
+    const int n_sch = P.n_tiles + (P.n_ap > 0 ? 1 : 0) + E.n_env;
     if (n_sch > 0)
     {
         static int smode = -1;
@@ -2093,7 +2171,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                 scap = P.n_tiles;
             }
             PL(K_SCHUR_TILE, k_schur_tile<true>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
-               sst, pp_parts(P), W.part, W.det_tbuf);
+               sst, pp_parts(P), W.part, W.det_tbuf, E);
             std::vector<unsigned long long> h((size_t)4 * P.n_tiles);
             CK(hipMemcpyAsync(h.data(), sst, sizeof(h[0]) * h.size(), hipMemcpyDeviceToHost, s));
             CK(hipStreamSynchronize(s));
@@ -2107,7 +2185,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                     P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
         } else {
             PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
-               W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf);
+               W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf, E);
         }
         if (W.det_tbuf && P.n_tiles > 0)
             PL(K_SCHUR_TILE, k_schur_gather, dim3(W.n_env), dim3(TPB), 0, s, P, W.st, W.env_tile, W.det_tbuf,
@@ -2193,11 +2271,11 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
     const int nb_bs = P.n_bs_chunks;
     if (P.n_ap > 0)
         PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
-           W.part);
+           W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     const int nb_pt = pp_parts(P);
     if (!W.comm.on()) {
         PL(K_FINAL, k_final, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
-           W.chol_flag, W.scal, prm, W.lin, W.log);
+           W.chol_flag, W.scal, prm, W.lin, W.log, W.fused ? W.rhs : (double*)nullptr);
         return hipSuccess;
     }
     PL(K_FINAL, k_final_shard, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,

@@ -705,6 +705,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     HIPCHECK(ctx, ctx->buf[B_S].ensure(sizeof(double) * (size_t)npad * npad));
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)npad * npad, s));
     HIPCHECK(ctx, ctx->buf[B_RHS].ensure(sizeof(double) * npad));
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RHS].p, 0, sizeof(double) * npad, s));
     HIPCHECK(ctx, ctx->buf[B_DELTA].ensure(sizeof(double) * npad));
     HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
     HIPCHECK(ctx, ctx->buf[B_SCAL].ensure(sizeof(double) * SC_N));
@@ -881,6 +882,12 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         W.det_tbuf = ctx->buf[B_DET_TBUF].as<double>();
         W.det_trange = ctx->buf[B_DET_TRANGE].as<int2>();
     }
+    // fused LM-loop linearisation (k_lin_point + envelope tiles in k_schur_tile, S / rhs zeroed by the previous
+    // iteration): the unsharded default-mode path with points and camera segments
+    {
+        const char* e = std::getenv("MIBA_FUSED");
+        W.fused = (!shard && !W.det_tbuf && n_ap > 0 && n_seg > 0 && P.solver != BA_LS_SMALL && !(e && e[0] == '0')) ? 1 : 0;
+    }
     BaConsts& C = ctx->C;
     ctx->n_adm_all = n_adm_all;
     // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
@@ -960,6 +967,8 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         kb[K_BACKSUB_EVAL] = A * 2 * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read twice
         kf[K_BACKSUB_EVAL] = A * 450;
         kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
+        kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step
+        kf[K_LIN_POINT] = kf[K_CAM_SIDE] + kf[K_POINT_PREP];
     }
     return BA_OK;
 }
@@ -1085,6 +1094,11 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     prm.progress = ctx->dprog;
     if (ctx->hprog) __atomic_store_n(ctx->hprog, 0u, __ATOMIC_RELEASE);
 
+    // fused path: S and rhs are the atomic targets of the first assembly (later ones are zeroed in-loop)
+    if (W.fused) {
+        HIPCHECK(ctx, hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
+        HIPCHECK(ctx, hipMemsetAsync(W.rhs, 0, sizeof(double) * P.npad, s));
+    }
     // IterationZero: cost, gradient, column norms -> Jacobi scale, |x| (the small-window kernel does its own)
     if (!W.sm.on) {
         HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
