@@ -295,19 +295,15 @@ __device__ __forceinline__ void potrf16_regs(double (&a)[16], double* rdiag, int
 // One thread: Ceres 2.0 TrustRegionMinimizer::Minimize bookkeeping for the step whose
 // scalars k_final produced (model cost change, candidate cost, |step|, |x_cand|, flags).
 // Same decisions, in the same order, as oracle_solve() (oracle/ba_oracle.c).
-__device__ __forceinline__ void lm_decide_core(LmState* __restrict__ st, const LmParams& prm,
-                                               const double* __restrict__ lin, const double* __restrict__ scal,
-                                               double* __restrict__ log) {
-    LmState S = *st;
-    if (S.done) return;
+__device__ __forceinline__ void lm_decide_local(LmState& S, const LmParams& prm, double lin0, double lin1,
+                                                const double* __restrict__ scal, double* __restrict__ log) {
     if (S.need_lin) {  // absorb the re-linearisation of the last accepted point
         S.need_lin = 0;
-        S.x_cost = lin[0];
-        S.gmax_ci = lin[1];
+        S.x_cost = lin0;
+        S.gmax_ci = lin1;
         log[S.iter * LOG_W + 0] = S.x_cost;
         if (!isfinite(S.x_cost)) {
             S.done = 1; S.termination = 2; S.msg = MSG_EVAL_FAIL;
-            *st = S;
             return;
         }
         S.final_cost = fmin(S.final_cost, S.x_cost);
@@ -322,14 +318,13 @@ __device__ __forceinline__ void lm_decide_core(LmState* __restrict__ st, const L
     } else if (S.radius <= prm.min_radius) {
         S.done = 1; S.termination = 0; S.msg = MSG_MIN_RADIUS; S.msg_a = S.radius; S.msg_b = prm.min_radius;
     }
-    if (S.done) { *st = S; return; }
+    if (S.done) return;
     S.iter += 1;
     double* lg = log + S.iter * LOG_W;
     if (scal[SC_BAD] >= SC_BAD_TIMEOUT) {  // a BCR hand-off timed out: no valid step; end the solve loudly
         S.n_unsucc += 1;
         S.done = 1; S.termination = 2; S.msg = MSG_TIMEOUT;
         lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
-        *st = S;
         return;
     }
     const double mcc = scal[SC_MCC];
@@ -345,7 +340,6 @@ __device__ __forceinline__ void lm_decide_core(LmState* __restrict__ st, const L
             S.step_ok = 0;
         }
         lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
-        *st = S;
         return;
     }
     S.n_invalid = 0;
@@ -363,7 +357,6 @@ __device__ __forceinline__ void lm_decide_core(LmState* __restrict__ st, const L
     }
     if (S.done) {
         lg[0] = cand; lg[1] = cost_change; lg[3] = step_norm; lg[4] = 0.0; lg[5] = S.radius; lg[6] = -1.0;
-        *st = S;
         return;
     }
     const double rho = (cand >= DBL_MAX) ? -DBL_MAX : cost_change / mcc;
@@ -387,19 +380,26 @@ __device__ __forceinline__ void lm_decide_core(LmState* __restrict__ st, const L
         lg[0] = cand; lg[6] = 0.0;
     }
     lg[1] = cost_change; lg[3] = step_norm; lg[4] = rho; lg[5] = S.radius;
-    *st = S;
 }
 
-__device__ inline void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
-                                      const double* __restrict__ scal, double* __restrict__ log) {
-    if (st->done) return;
-    lm_decide_core(st, prm, lin, scal, log);
-    LmState& S = *st;
+// The decision on a state the caller has already loaded (S0) and the step scalars in registers: one store
+// of the new state, no global round trip between the reductions and the decision (k_final).
+__device__ inline void lm_decide_pre(const LmState& S0, LmState* __restrict__ st, const LmParams& prm, double lin0,
+                                     double lin1, const double* scal, double* __restrict__ log) {
+    if (S0.done) return;
+    LmState S = S0;
+    lm_decide_local(S, prm, lin0, lin1, scal, log);
     S.n_decide += 1;
     S.stop_next = !S.done && S.iter >= prm.max_iter;
+    *st = S;
     if (prm.progress)
         __hip_atomic_store(prm.progress, (unsigned)S.n_decide | (S.done ? 0x80000000u : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
+                                      const double* __restrict__ scal, double* __restrict__ log) {
+    const LmState S0 = *st;
+    lm_decide_pre(S0, st, prm, lin[0], lin[1], scal, log);
 }
 
 }  // namespace miba

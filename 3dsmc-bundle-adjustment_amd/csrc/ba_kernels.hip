@@ -1804,18 +1804,29 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
     __shared__ double lds[NW_F * 4];
     __shared__ double out[4];
     __shared__ double red[NW_F];
-    if (st->done) return;
-    if (rhs_z)  // fused path: y has been consumed; rhs is the next assembly's atomic target
-        for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
+    // every load up front (the state, the flag, lin and all partials), so the reductions and the decision
+    // wait for one memory round trip instead of one per loop trip
+    LmState S0;
+    int cf = 0;
+    double lin0 = 0.0, lin1 = 0.0;
+    if (threadIdx.x == 0) {
+        S0 = *st;
+        cf = *chol_flag;
+        lin0 = lin[0];
+        lin1 = lin[1];
+    }
+    const int done = __builtin_amdgcn_readfirstlane(st->done);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double gm = 0.0, bad = 0.0;
     const size_t stp = P.part_stride;
+#pragma unroll 2
     for (int i = threadIdx.x; i < nblk_upd; i += TPB_F) {
         acc[0] += part[PART_UPD_SN2 * stp + i];
         acc[1] += part[PART_UPD_MCC * stp + i];
         acc[2] += part[PART_UPD_COST * stp + i];
         acc[3] += part[PART_UPD_XN2 * stp + i];
     }
+#pragma unroll 8
     for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
         acc[0] += part[PART_BS_SN2 * stp + i];
         acc[1] += part[PART_BS_MCC * stp + i];
@@ -1823,22 +1834,28 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
         acc[3] += part[PART_BS_XN2 * stp + i];
         bad = fmax(bad, part[PART_BS_BAD * stp + i]);
     }
+#pragma unroll 4
     for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
         gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
     }
+    if (done) return;
+    if (rhs_z)  // fused path: y has been consumed; rhs is the next assembly's atomic target
+        for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
     block_sum_nw<NW_F, 4>(acc, lds, out);
     gm = block_max_nw<NW_F>(gm, red);
     bad = block_max_nw<NW_F>(bad, red);
     if (threadIdx.x == 0) {
-        scal[SC_XN2] = out[3];
-        scal[SC_SN2] = out[0];
-        scal[SC_MCC] = out[1];
-        scal[SC_CAND] = out[2];
-        scal[SC_GMAX_PT] = gm;
-        const int cf = *chol_flag;
-        scal[SC_BAD] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
-        lm_decide_body(st, prm, lin, scal, log);
+        double sc[SC_N] = {};
+        sc[SC_XN2] = out[3];
+        sc[SC_SN2] = out[0];
+        sc[SC_MCC] = out[1];
+        sc[SC_CAND] = out[2];
+        sc[SC_GMAX_PT] = gm;
+        sc[SC_BAD] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
+#pragma unroll
+        for (int k = 0; k < SC_N; ++k) scal[k] = sc[k];
+        lm_decide_pre(S0, st, prm, lin0, lin1, sc, log);
     }
 }
 
