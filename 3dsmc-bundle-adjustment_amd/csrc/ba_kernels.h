@@ -211,6 +211,8 @@ static constexpr int FLAG_NOT_PD = 1;
 static constexpr int FLAG_TIMEOUT = 2;
 // scal[SC_BAD] >= SC_BAD_TIMEOUT: some workgroup's hand-off timed out
 static constexpr double SC_BAD_TIMEOUT = 8.0;
+// offset of the sharded scalar exchange in DevWork::red
+static constexpr int RED_X = 16;
 // per-iteration log row: cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius, accepted
 static constexpr int LOG_W = 8;
 
@@ -264,8 +266,8 @@ struct DevWork {
     int n_env;
     double* env_loc;       // [n_env * 256 + npad]
     double* env_glob;
-    double* red;           // [32]: 0..3 local sums, 4..5 local maxima, 6..9 replicated sums, 10 chol flag,
-                           //       16..19 global sums, 20..21 global maxima
+    double* red;           // [RED_X + 2 * (4 + 2 * nranks)]: 6..9 replicated sums, 10 chol flag; at RED_X the
+                           // exchange (4 local sums, then a (gmax, bad) slot pair per rank), then its reduction
     // deterministic mode (ba_options.deterministic): per-tile Schur slabs + each active camera's tile range;
     // nullptr: the tiles flush with f64 atomics
     double* det_tbuf = nullptr;

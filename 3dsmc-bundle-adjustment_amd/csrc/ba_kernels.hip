@@ -375,12 +375,15 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
         if (diag) {  // cameras whose first dof lies in this tile's rows
             for (int e = tid; e < ncam * CAMDATA; e += TPB) {
                 const int ac = lo + e / CAMDATA;
-                if (6 * ac >= r0 && !stop) camdata_w[(size_t)ac * CAMDATA + e % CAMDATA] = cds[e];
+                if (6 * ac >= r0 && (fin == 2 || !stop)) camdata_w[(size_t)ac * CAMDATA + e % CAMDATA] = cds[e];
             }
-            if (tid < ncam && 6 * (lo + tid) >= r0)
+            if (fin == 1 && tid < ncam && 6 * (lo + tid) >= r0)
                 atomic_max_nonneg(lin_w + 1, cam_gmax(P, cur, lo + tid, cds + tid * CAMDATA + 45));
         }
-        if (kk_any) {
+        if (fin == 2 && kk_any) {  // shard: this rank's raw intrinsics sums go into the exchange
+            if (diag && r0 <= kb && kb < r0 + 16 && tid < SEGINTR) lin_w[tid] = io[tid];
+            linr = nullptr;
+        } else if (kk_any) {
             if (tid == 0) {
                 const double gm = intr_lin(P, c, P.K[cur], io, l16);
                 if (diag && r0 <= kb && kb < r0 + 16) {
@@ -398,7 +401,24 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
     if (stop) return;
     const double* sk = scale + P.off_k;
     double v = 0.0;
-    if (P.rank == 0) {
+    if (fin == 2) {
+        // landmark shard, folded exchange: this rank's camera-side terms without the LM diagonal and the
+        // prior (k_env_unpack_fin adds them from the reduced sums); the pad identity on rank 0
+        if (r < nd && col <= r && r / 6 == col / 6) {
+            const int ac = r / 6, i = col - 6 * ac, j = r - 6 * ac;
+            const int q = 6 * i - i * (i - 1) / 2 + (j - i);
+            v = scale[6 * ac + i] * cd[(size_t)(ac - ac0) * CAMDATA + q] * scale[6 * ac + j];
+        } else if (r >= kb && r < kb + 4 && col < nd) {
+            const int m = r - kb, ac = col / 6, i = col - 6 * ac;
+            v = scale[6 * ac + i] * cd[(size_t)(ac - ac0) * CAMDATA + 21 + i * 4 + m] * sk[m];
+        } else if (r >= kb && r < kb + 4 && col >= kb && col <= r) {
+            const int m = col - kb, l = r - kb;
+            const int q = 4 * m - m * (m - 1) / 2 + (l - m);
+            v = sk[m] * io[q] * sk[l];
+        } else if (r == col && r >= P.n && P.rank == 0) {
+            v = 1.0;
+        }
+    } else if (P.rank == 0) {
         const double radius = st->radius;
         if (r < nd && col <= r && r / 6 == col / 6) {
             const int ac = r / 6, i = col - 6 * ac, j = r - 6 * ac;
@@ -423,7 +443,10 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
     if (ij.x == ij.y && tid < 16) {
         const int rr = 16 * ij.x + tid;
         double b = 0.0;
-        if (P.rank == 0) {
+        if (fin == 2) {
+            if (rr < nd) b = scale[rr] * cd[(size_t)(rr / 6 - ac0) * CAMDATA + 45 + rr % 6];
+            else if (rr < kb + 4) b = sk[rr - kb] * io[10 + rr - kb];
+        } else if (P.rank == 0) {
             if (rr < nd) b = scale[rr] * cd[(size_t)(rr / 6 - ac0) * CAMDATA + 45 + rr % 6];
             else if (rr < kb + 4) b = sk[rr - kb] * linr[12 + rr - kb];
         }
@@ -773,6 +796,7 @@ struct EnvArgs {
     const double* seg_intr;
     double* camdata_w;
     double* lin_w;
+    int fin;  // 1: unsharded (finish the camera sums, lin); 2: landmark shard (local terms for the exchange)
 };
 
 template <bool STAMP>
@@ -786,7 +810,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
     if ((int)blockIdx.x > P.n_tiles) {  // envelope tiles (fused path): also in the terminal stop_next iteration
         if (!st->done)
-            env_tile(P, c, st, blockIdx.x - P.n_tiles - 1, E.tiles, E.camdata, E.lin, scale, S, rhs, E.chol_flag, 1,
+            env_tile(P, c, st, blockIdx.x - P.n_tiles - 1, E.tiles, E.camdata, E.lin, scale, S, rhs, E.chol_flag, E.fin,
                      E.cpart, E.seg_intr, E.camdata_w, E.lin_w, true);
         return;
     }
@@ -1860,79 +1884,187 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
 }
 
 // ---------------------------------------------------------------- landmark sharding
-// Envelope of S (its 16x16 tiles) + rhs <-> one contiguous buffer for the all-reduce.
-// unpack == 0: S, rhs -> buf; unpack == 1: buf -> S, rhs.
+// Envelope of S (its 16x16 tiles) + rhs (+ camera / intrinsics sums) <-> one contiguous buffer for the
+// all-reduce. unpack == 0: S, rhs, cam -> buf; unpack == 1: buf -> S, rhs. Workgroups < n_env move one tile
+// each; the rest move the tail [rhs | cam] one element per thread (env_tail_blocks of them), so no workgroup
+// walks a long serial copy.
+__host__ __device__ inline int env_tail_blocks(int npad, int ncam) { return (npad + ncam + TPB - 1) / TPB; }
 __global__ __launch_bounds__(TPB) void k_env_pack(const LmState* __restrict__ st, const int2* __restrict__ tiles, int n_env,
                                                   int npad, double* __restrict__ S, double* __restrict__ rhs,
-                                                  double* __restrict__ buf, int unpack) {
-    if (skip_step(st)) return;
+                                                  double* __restrict__ buf, int unpack, const double* __restrict__ cam,
+                                                  int ncam) {
     const int t = blockIdx.x;
     if (t < n_env) {
+        if (skip_step(st)) return;
         const int2 ij = tiles[t];
         const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;
         double* sp = S + (size_t)(16 * ij.x + r) * npad + 16 * ij.y + cc;
         double* bp = buf + (size_t)t * 256 + threadIdx.x;
         if (unpack) *sp = *bp; else *bp = *sp;
+        return;
+    }
+    const int j = (t - n_env) * TPB + threadIdx.x;
+    double* bp = buf + (size_t)n_env * 256 + j;
+    if (j < npad) {
+        if (skip_step(st)) return;
+        if (unpack) rhs[j] = *bp; else *bp = rhs[j];
+    } else if (j < npad + ncam) {  // folded exchange: this rank's camera-side and intrinsics sums (also when stop_next)
+        if (st->done) return;
+        *bp = cam[j - npad];
+    }
+}
+// Folded exchange, after the all-reduce (landmark shards, fused LM loop): buf = [envelope tiles | rhs | camera
+// sums (nac x CAMDATA) | intrinsics sums (SEGINTR)], each summed over the ranks. Workgroups < n_env: S tiles,
+// plus the LM diagonal of the camera / intrinsics dofs and the IntrinsicsPrior diagonal (from the reduced camera
+// and intrinsics sums: env_tile's rank-0 formulas); the next env_tail_blocks: rhs plus the prior's gradient and
+// the camdata copy, one element per thread; the last: lin (cost, gradient max-norm, prior-augmented intrinsics
+// block) for the step kernels and the decision.
+__global__ __launch_bounds__(TPB) void k_env_unpack_fin(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                        const int2* __restrict__ tiles, int n_env,
+                                                        const double* __restrict__ buf, const double* __restrict__ scale,
+                                                        double* __restrict__ S, double* __restrict__ rhs,
+                                                        double* __restrict__ camdata, double* __restrict__ lin) {
+    __shared__ double red[4];
+    __shared__ double l16[LIN_N];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int npad = P.npad, nd = 6 * P.nac, kb = P.kb;
+    const double* cdg = buf + (size_t)n_env * 256 + npad;
+    const double* iog = cdg + (size_t)P.nac * CAMDATA;
+    const double* sk = scale + P.off_k;
+    const double wk = c.sw_k * c.sw_k;
+    const int ntail = env_tail_blocks(npad, P.nac * CAMDATA);
+    if (t < n_env) {
+        if (skip_step(st)) return;
+        const int2 ij = tiles[t];
+        const int r = 16 * ij.x + (tid >> 4), col = 16 * ij.y + (tid & 15);
+        double v = buf[(size_t)t * 256 + tid];
+        if (r == col) {
+            const double radius = st->radius;
+            if (r < nd) {
+                const int ac = r / 6, i = r - 6 * ac;
+                const double u = scale[r] * cdg[(size_t)ac * CAMDATA + 6 * i - i * (i - 1) / 2] * scale[r];
+                v += fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+            } else if (r < kb + 4) {
+                const int m = r - kb;
+                const double u = sk[m] * (iog[4 * m - m * (m - 1) / 2] + wk) * sk[m];
+                v += sk[m] * wk * sk[m] + fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+            }
+        }
+        S[(size_t)r * npad + col] = v;
+    } else if (t < n_env + ntail) {
+        const int j = (t - n_env) * TPB + tid;
+        if (j < npad) {
+            if (skip_step(st)) return;
+            double b = buf[(size_t)n_env * 256 + j];
+            if (j >= kb && j < kb + 4) {
+                const int m = j - kb;
+                b += sk[m] * (-c.sw_k) * (c.sw_k * (P.prior[m] - P.K[st->cur][m]));
+            }
+            rhs[j] = b;
+        } else if (j < npad + P.nac * CAMDATA) {
+            if (st->done) return;
+            camdata[j - npad] = cdg[j - npad];
+        }
     } else {
-        for (int i = threadIdx.x; i < npad; i += TPB) {
-            double* bp = buf + (size_t)n_env * 256 + i;
-            if (unpack) rhs[i] = *bp; else *bp = rhs[i];
+        if (st->done) return;
+        const int cur = st->cur;
+        double gm = 0.0;
+        for (int ac = tid; ac < P.nac; ac += TPB) gm = fmax(gm, cam_gmax(P, cur, ac, cdg + (size_t)ac * CAMDATA + 45));
+        gm = block_max(gm, red);
+        if (tid == 0) {
+            const double gi = intr_lin(P, c, P.K[cur], iog, l16);
+            lin[0] = l16[0];
+            lin[1] = fmax(gm, gi);
+            for (int q = 2; q < LIN_N; ++q) lin[q] = l16[q];
         }
     }
 }
+
 // Sharded k_final: this rank's point-side sums / maxima and the (replicated) camera-side
 // sums go to red[] for the all-reduce; k_combine assembles scal[] from the reduced values.
-__global__ __launch_bounds__(TPB) void k_final_shard(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
-                                                     int nblk_upd, int nblk_bs, const double* __restrict__ part,
-                                                     const int* __restrict__ chol_flag, double* __restrict__ red) {
-    __shared__ double lds[4 * 8];
+__global__ __launch_bounds__(TPB_F) void k_final_shard(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
+                                                       int nblk_upd, int nblk_bs, const double* __restrict__ part,
+                                                       const int* __restrict__ chol_flag, double* __restrict__ red,
+                                                       double* __restrict__ rhs_z, int nranks) {
+    __shared__ double lds[NW_F * 8];
     __shared__ double out[8];
-    __shared__ double rl[4];
-    if (st->done) return;
+    __shared__ double rl[NW_F];
+    // k_final's shape: every load up front, one memory round trip before the reductions
+    const int cf = *chol_flag;
+    const int done = __builtin_amdgcn_readfirstlane(st->done);
     double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // 0..3 local, 4..7 replicated
     double gm = 0.0, bad = 0.0;
     const size_t stp = P.part_stride;
-    for (int i = threadIdx.x; i < nblk_upd; i += TPB) {
+#pragma unroll 2
+    for (int i = threadIdx.x; i < nblk_upd; i += TPB_F) {
         acc[4] += part[PART_UPD_SN2 * stp + i];
         acc[5] += part[PART_UPD_MCC * stp + i];
         acc[6] += part[PART_UPD_COST * stp + i];
         acc[7] += part[PART_UPD_XN2 * stp + i];
     }
-    for (int i = threadIdx.x; i < nblk_bs; i += TPB) {
+#pragma unroll 8
+    for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
         acc[0] += part[PART_BS_SN2 * stp + i];
         acc[1] += part[PART_BS_MCC * stp + i];
         acc[2] += part[PART_BS_COST * stp + i];
         acc[3] += part[PART_BS_XN2 * stp + i];
         bad = fmax(bad, part[PART_BS_BAD * stp + i]);
     }
-    for (int i = threadIdx.x; i < nblk_pt; i += TPB) {
+#pragma unroll 4
+    for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
         gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
     }
-    block_sum<8>(acc, lds, out);
-    gm = block_max(gm, rl);
-    bad = block_max(bad, rl);
+    if (done) return;
+    if (rhs_z)  // fused path: y has been consumed; rhs is the next local assembly's atomic target
+        for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
+    // one SUM all-reduce carries both the sums and the maxima: each rank writes its two maxima into its own
+    // slot pair of red[RED_X + 4 ...] and zeros into the others' (x + 0 is exact), k_combine takes the max
+    double* x = red + RED_X;
+    for (int i = 4 + threadIdx.x; i < 4 + 2 * nranks; i += TPB_F)
+        if (((i - 4) >> 1) != P.rank) x[i] = 0.0;
+    block_sum_nw<NW_F, 8>(acc, lds, out);
+    gm = block_max_nw<NW_F>(gm, rl);
+    bad = block_max_nw<NW_F>(bad, rl);
     if (threadIdx.x == 0) {
-        for (int i = 0; i < 4; ++i) red[i] = out[i];
-        red[4] = gm;
+        for (int i = 0; i < 4; ++i) x[i] = out[i];
+        x[4 + 2 * P.rank] = gm;
         // the factorisation flag is identical on every rank (replicated reduced solve) except for a hand-off
-        // timeout, which is local: both ride the max all-reduce, so every rank takes the same decision
-        const int cf = *chol_flag;
-        red[5] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
+        // timeout, which is local: both ride the exchange, so every rank takes the same decision
+        x[5 + 2 * P.rank] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
         for (int i = 0; i < 4; ++i) red[6 + i] = out[4 + i];
         red[10] = 0.0;
     }
 }
 __global__ void k_combine(LmState* __restrict__ st, const double* __restrict__ red, double* __restrict__ scal,
-                          LmParams prm, const double* __restrict__ lin, double* __restrict__ log) {
-    if (st->done || threadIdx.x != 0) return;
-    scal[SC_SN2] = red[16 + 0] + red[6];
-    scal[SC_MCC] = red[16 + 1] + red[7];
-    scal[SC_CAND] = red[16 + 2] + red[8];
-    scal[SC_XN2] = red[16 + 3] + red[9];
-    scal[SC_GMAX_PT] = red[20];
-    scal[SC_BAD] = red[21] + red[10];
-    lm_decide_body(st, prm, lin, scal, log);
+                          LmParams prm, const double* __restrict__ lin, double* __restrict__ log, int nranks) {
+    if (threadIdx.x != 0) return;
+    const LmState S0 = *st;
+    const double lin0 = lin[0], lin1 = lin[1];
+    const double* y = red + RED_X + 4 + 2 * nranks;  // the reduced exchange
+    double r6[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r6[i] = red[6 + i];
+    double y4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y4[i] = y[i];
+    if (S0.done) return;
+    double gm = 0.0, bad = 0.0;
+    for (int r = 0; r < nranks; ++r) {
+        gm = fmax(gm, y[4 + 2 * r]);
+        const double b = y[5 + 2 * r];
+        bad = (b != b || bad != bad) ? b + bad : fmax(bad, b);  // NaN propagates
+    }
+    double sc[SC_N] = {};
+    sc[SC_SN2] = y4[0] + r6[0];
+    sc[SC_MCC] = y4[1] + r6[1];
+    sc[SC_CAND] = y4[2] + r6[2];
+    sc[SC_XN2] = y4[3] + r6[3];
+    sc[SC_GMAX_PT] = gm;
+    sc[SC_BAD] = bad + r6[4];
+#pragma unroll
+    for (int k = 0; k < SC_N; ++k) scal[k] = sc[k];
+    lm_decide_pre(S0, st, prm, lin0, lin1, sc, log);
 }
 
 // ---------------------------------------------------------------- LM control
@@ -2156,7 +2288,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     EnvArgs E{};
     if (W.fused) {  // point side + gated camera side in one launch; the envelope tiles ride in k_schur_tile
         const int nb = pp_blocks(P.n_ap);
-        switch (pp_lanes()) {
+        if (nb + P.n_seg > 0) switch (pp_lanes()) {
             case 1: PL(K_LIN_POINT, k_lin_point<1>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
                        W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
             case 2: PL(K_LIN_POINT, k_lin_point<2>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
@@ -2164,14 +2296,20 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             default: PL(K_LIN_POINT, k_lin_point<4>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
                         W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
         }
-        E = EnvArgs{W.env_tile, W.n_env, W.camdata, W.lin, W.chol_flag, W.camdata_part, W.seg_intr, W.camdata, W.lin};
+        // unsharded: the envelope tiles finish the camera sums and lin (fin 1); landmark shard: they write this
+        // rank's terms and sums for the folded exchange (fin 2; camdata_loc = [camera sums | intrinsics sums])
+        const int ncd = P.nac * CAMDATA;
+        E = W.comm.on() ? EnvArgs{W.env_tile, W.n_env, W.camdata, W.lin, W.chol_flag, W.camdata_part, W.seg_intr,
+                                  W.camdata_loc, W.camdata_loc + ncd, 2}
+                        : EnvArgs{W.env_tile, W.n_env, W.camdata, W.lin, W.chol_flag, W.camdata_part, W.seg_intr,
+                                  W.camdata, W.lin, 1};
     } else if (P.n_ap > 0)
         CK(launch_point_prep(P, c, 1, W, s, pf));  // + the envelope tiles
     else
         PL(K_ASSEMBLE, k_env_assemble, dim3(W.n_env), dim3(TPB), 0, s, P, c, W.st, W.env_tile, W.camdata, W.lin,
            W.scale, W.S, W.rhs, W.chol_flag, W.comm.on() ? 0 : 1, W.camdata_part, W.seg_intr, W.camdata, W.lin);
     // Schur tiles + one workgroup for the intrinsics Schur terms (when there are points)
-    const int n_sch = P.n_tiles + (P.n_ap > 0 ? 1 : 0) + E.n_env;
+    const int n_sch = P.n_tiles + ((P.n_ap > 0 || W.fused) ? 1 : 0) + E.n_env;
     if (n_sch > 0)
     {
         static int smode = -1;
@@ -2215,13 +2353,24 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale,
                W.pdata, W.S, W.rhs);
     }
-    if (W.comm.on()) {  // S = sum over the landmark shards: envelope tiles + rhs
-        const size_t ne = (size_t)W.n_env * 256 + P.npad;
-        PL(K_COMM, k_env_pack, dim3(W.n_env + 1), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs,
-           W.env_loc, 0);
+    if (W.comm.on() && W.fused) {
+        // folded exchange: ONE all-reduce of [envelope | rhs | camera sums | intrinsics sums]; the LM diagonal,
+        // the prior, camdata and lin follow from the reduced sums (k_env_unpack_fin)
+        const int ncam = P.nac * CAMDATA + SEGINTR;
+        const size_t ne = (size_t)W.n_env * 256 + P.npad + ncam;
+        PL(K_COMM, k_env_pack, dim3(W.n_env + env_tail_blocks(P.npad, ncam)), dim3(TPB), 0, s, W.st, W.env_tile,
+           W.n_env, P.npad, W.S, W.rhs, W.env_loc, 0, W.camdata_loc, ncam);
         COMM(W.env_loc, W.env_glob, ne, COMM_F64, COMM_SUM);
-        PL(K_COMM, k_env_pack, dim3(W.n_env + 1), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs,
-           W.env_glob, 1);
+        PL(K_COMM, k_env_unpack_fin, dim3(W.n_env + env_tail_blocks(P.npad, P.nac * CAMDATA) + 1), dim3(TPB), 0, s,
+           P, c, W.st, W.env_tile, W.n_env, W.env_glob, W.scale, W.S, W.rhs, W.camdata, W.lin);
+    } else if (W.comm.on()) {  // S = sum over the landmark shards: envelope tiles + rhs
+        const size_t ne = (size_t)W.n_env * 256 + P.npad;
+        const int nt = W.n_env + env_tail_blocks(P.npad, 0);
+        PL(K_COMM, k_env_pack, dim3(nt), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs, W.env_loc, 0,
+           (const double*)nullptr, 0);
+        COMM(W.env_loc, W.env_glob, ne, COMM_F64, COMM_SUM);
+        PL(K_COMM, k_env_pack, dim3(nt), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs, W.env_glob,
+           1, (const double*)nullptr, 0);
     }
     return hipSuccess;
 }
@@ -2286,6 +2435,8 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
         PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.camdata, W.lin, W.rhs,
            W.delta, W.part);
     const int nb_bs = P.n_bs_chunks;
+    if (W.fused && P.n_ap == 0)  // an empty landmark shard: no back-substitution chunk zeroes S for the next assembly
+        PL(K_MEMSET_S, k_env_zero, dim3(W.n_env), dim3(TPB), 0, s, W.st, W.env_tile, P.npad, W.S);
     if (P.n_ap > 0)
         PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
@@ -2295,11 +2446,11 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
            W.chol_flag, W.scal, prm, W.lin, W.log, W.fused ? W.rhs : (double*)nullptr);
         return hipSuccess;
     }
-    PL(K_FINAL, k_final_shard, dim3(1), dim3(TPB), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
-       W.chol_flag, W.red);
-    COMM(W.red, W.red + 16, 4, COMM_F64, COMM_SUM);
-    COMM(W.red + 4, W.red + 20, 2, COMM_F64, COMM_MAX);
-    PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal, prm, W.lin, W.log);
+    PL(K_FINAL, k_final_shard, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
+       W.chol_flag, W.red, W.fused ? W.rhs : (double*)nullptr, W.comm.nranks);
+    const int nx = 4 + 2 * W.comm.nranks;
+    COMM(W.red + RED_X, W.red + RED_X + nx, nx, COMM_F64, COMM_SUM);
+    PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal, prm, W.lin, W.log, W.comm.nranks);
     return hipSuccess;
 }
 

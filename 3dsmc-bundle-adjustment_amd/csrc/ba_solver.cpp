@@ -688,13 +688,15 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         for (int j = fcol[i]; j <= i; ++j) env_tile.push_back(make_int2(i, j));
     HIPCHECK(ctx, upload(ctx, B_ENV_TILE, env_tile.data(), env_tile.size()));
     if (shard) {
-        const size_t ne = env_tile.size() * 256 + (size_t)npad;
+        // envelope tiles + rhs (+ the camera and intrinsics sums of the folded exchange)
+        const size_t ne = env_tile.size() * 256 + (size_t)npad + (size_t)nac * CAMDATA + SEGINTR + 1;
         HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
         HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
         HIPCHECK(ctx, ctx->buf[B_ENV_GLOB].ensure(sizeof(double) * ne));
-        HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * 32));
-        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * 32, s));
+        const size_t nred = RED_X + 2 * (4 + 2 * (size_t)ctx->W.comm.nranks);
+        HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * nred));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * nred, s));
     }
     HIPCHECK(ctx, ctx->buf[B_SEGINTR].ensure(sizeof(double) * SEGINTR * std::max(n_seg, 1)));
     HIPCHECK(ctx, ctx->buf[B_CAMPART].ensure(sizeof(double) * CAMDATA * std::max(n_seg, 1)));
@@ -886,7 +888,10 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     // iteration): the unsharded default-mode path with points and camera segments
     {
         const char* e = std::getenv("MIBA_FUSED");
-        W.fused = (!shard && !W.det_tbuf && n_ap > 0 && n_seg > 0 && P.solver != BA_LS_SMALL && !(e && e[0] == '0')) ? 1 : 0;
+        const bool off = e && e[0] == '0';
+        // landmark shards: the same choice on every rank (it fixes the collective sequence), so only uniform inputs
+        W.fused = (shard ? (!o.deterministic && !off)
+                         : (!W.det_tbuf && n_ap > 0 && n_seg > 0 && P.solver != BA_LS_SMALL && !off)) ? 1 : 0;
     }
     BaConsts& C = ctx->C;
     ctx->n_adm_all = n_adm_all;
