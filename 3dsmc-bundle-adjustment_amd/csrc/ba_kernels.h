@@ -264,10 +264,9 @@ struct DevWork {
     double* camdata_part;  // [n_seg * CAMDATA]: per sub-segment camera partials
     const int2* env_tile;  // (block row, block col) of every 16x16 envelope tile of S
     int n_env;
-    double* env_loc;       // [n_env * 256 + npad]
-    double* env_glob;
-    double* red;           // [RED_X + 2 * (4 + 2 * nranks)]: 6..9 replicated sums, 10 chol flag; at RED_X the
-                           // exchange (4 local sums, then a (gmax, bad) slot pair per rank), then its reduction
+    double* env_loc;       // [n_env * 256 + npad (+ camera sums)]: the exchange, reduced in place
+    double* red;           // [RED_X + 4 + 2 * nranks]: 6..9 replicated sums, 10 chol flag; at RED_X the exchange
+                           // (4 local sums, then a (gmax, bad) slot pair per rank), reduced in place
     // deterministic mode (ba_options.deterministic): per-tile Schur slabs + each active camera's tile range;
     // nullptr: the tiles flush with f64 atomics
     double* det_tbuf = nullptr;

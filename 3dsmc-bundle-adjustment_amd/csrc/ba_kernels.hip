@@ -1818,8 +1818,11 @@ __global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st
 // ---------------------------------------------------------------- final
 // scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]; then the LM decision (k_lm_decide's
 // body, fused: one launch less per iteration)
-// 4 waves (16 measured 1 us slower at C4: more waves to start and to reduce than loads saved)
+// 4 waves (16 measured 1 us slower at C4: more waves to start and to reduce than loads saved). UNR: unroll of
+// the partial-sum loops (C4 rocprof: k_final 9.2 / 6.9 / 7.5 us at 1 / 2 / 8; k_final_shard with twice the
+// accumulators 6.7 / 11.0 / 12.8 us at 1 / 4 / 8)
 static constexpr int TPB_F = 256, NW_F = TPB_F / 64;
+template <int UNR>
 __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                                int nblk_bs, const double* __restrict__ part,
                                                const int* __restrict__ chol_flag, double* __restrict__ scal,
@@ -1843,14 +1846,14 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double gm = 0.0, bad = 0.0;
     const size_t stp = P.part_stride;
-#pragma unroll 2
+#pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_upd; i += TPB_F) {
         acc[0] += part[PART_UPD_SN2 * stp + i];
         acc[1] += part[PART_UPD_MCC * stp + i];
         acc[2] += part[PART_UPD_COST * stp + i];
         acc[3] += part[PART_UPD_XN2 * stp + i];
     }
-#pragma unroll 8
+#pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
         acc[0] += part[PART_BS_SN2 * stp + i];
         acc[1] += part[PART_BS_MCC * stp + i];
@@ -1858,7 +1861,7 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
         acc[3] += part[PART_BS_XN2 * stp + i];
         bad = fmax(bad, part[PART_BS_BAD * stp + i]);
     }
-#pragma unroll 4
+#pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
         gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
@@ -1982,6 +1985,7 @@ __global__ __launch_bounds__(TPB) void k_env_unpack_fin(DevProblem P, BaConsts c
 
 // Sharded k_final: this rank's point-side sums / maxima and the (replicated) camera-side
 // sums go to red[] for the all-reduce; k_combine assembles scal[] from the reduced values.
+template <int UNR>
 __global__ __launch_bounds__(TPB_F) void k_final_shard(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
                                                        int nblk_upd, int nblk_bs, const double* __restrict__ part,
                                                        const int* __restrict__ chol_flag, double* __restrict__ red,
@@ -1995,14 +1999,14 @@ __global__ __launch_bounds__(TPB_F) void k_final_shard(DevProblem P, const LmSta
     double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // 0..3 local, 4..7 replicated
     double gm = 0.0, bad = 0.0;
     const size_t stp = P.part_stride;
-#pragma unroll 2
+#pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_upd; i += TPB_F) {
         acc[4] += part[PART_UPD_SN2 * stp + i];
         acc[5] += part[PART_UPD_MCC * stp + i];
         acc[6] += part[PART_UPD_COST * stp + i];
         acc[7] += part[PART_UPD_XN2 * stp + i];
     }
-#pragma unroll 8
+#pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
         acc[0] += part[PART_BS_SN2 * stp + i];
         acc[1] += part[PART_BS_MCC * stp + i];
@@ -2010,7 +2014,7 @@ __global__ __launch_bounds__(TPB_F) void k_final_shard(DevProblem P, const LmSta
         acc[3] += part[PART_BS_XN2 * stp + i];
         bad = fmax(bad, part[PART_BS_BAD * stp + i]);
     }
-#pragma unroll 4
+#pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
         gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
@@ -2041,7 +2045,7 @@ __global__ void k_combine(LmState* __restrict__ st, const double* __restrict__ r
     if (threadIdx.x != 0) return;
     const LmState S0 = *st;
     const double lin0 = lin[0], lin1 = lin[1];
-    const double* y = red + RED_X + 4 + 2 * nranks;  // the reduced exchange
+    const double* y = red + RED_X;  // the reduced exchange (in place)
     double r6[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) r6[i] = red[6 + i];
@@ -2360,16 +2364,16 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
         const size_t ne = (size_t)W.n_env * 256 + P.npad + ncam;
         PL(K_COMM, k_env_pack, dim3(W.n_env + env_tail_blocks(P.npad, ncam)), dim3(TPB), 0, s, W.st, W.env_tile,
            W.n_env, P.npad, W.S, W.rhs, W.env_loc, 0, W.camdata_loc, ncam);
-        COMM(W.env_loc, W.env_glob, ne, COMM_F64, COMM_SUM);
+        COMM(W.env_loc, W.env_loc, ne, COMM_F64, COMM_SUM);  // in place (a 1-rank communicator copies nothing)
         PL(K_COMM, k_env_unpack_fin, dim3(W.n_env + env_tail_blocks(P.npad, P.nac * CAMDATA) + 1), dim3(TPB), 0, s,
-           P, c, W.st, W.env_tile, W.n_env, W.env_glob, W.scale, W.S, W.rhs, W.camdata, W.lin);
+           P, c, W.st, W.env_tile, W.n_env, W.env_loc, W.scale, W.S, W.rhs, W.camdata, W.lin);
     } else if (W.comm.on()) {  // S = sum over the landmark shards: envelope tiles + rhs
         const size_t ne = (size_t)W.n_env * 256 + P.npad;
         const int nt = W.n_env + env_tail_blocks(P.npad, 0);
         PL(K_COMM, k_env_pack, dim3(nt), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs, W.env_loc, 0,
            (const double*)nullptr, 0);
-        COMM(W.env_loc, W.env_glob, ne, COMM_F64, COMM_SUM);
-        PL(K_COMM, k_env_pack, dim3(nt), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs, W.env_glob,
+        COMM(W.env_loc, W.env_loc, ne, COMM_F64, COMM_SUM);
+        PL(K_COMM, k_env_pack, dim3(nt), dim3(TPB), 0, s, W.st, W.env_tile, W.n_env, P.npad, W.S, W.rhs, W.env_loc,
            1, (const double*)nullptr, 0);
     }
     return hipSuccess;
@@ -2442,14 +2446,13 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
            W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     const int nb_pt = pp_parts(P);
     if (!W.comm.on()) {
-        PL(K_FINAL, k_final, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
+        PL(K_FINAL, k_final<2>, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
            W.chol_flag, W.scal, prm, W.lin, W.log, W.fused ? W.rhs : (double*)nullptr);
         return hipSuccess;
     }
-    PL(K_FINAL, k_final_shard, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
+    PL(K_FINAL, k_final_shard<1>, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
        W.chol_flag, W.red, W.fused ? W.rhs : (double*)nullptr, W.comm.nranks);
-    const int nx = 4 + 2 * W.comm.nranks;
-    COMM(W.red + RED_X, W.red + RED_X + nx, nx, COMM_F64, COMM_SUM);
+    COMM(W.red + RED_X, W.red + RED_X, 4 + 2 * W.comm.nranks, COMM_F64, COMM_SUM);  // in place
     PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal, prm, W.lin, W.log, W.comm.nranks);
     return hipSuccess;
 }

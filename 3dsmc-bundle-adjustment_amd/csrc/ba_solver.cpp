@@ -59,7 +59,7 @@ enum BufId {
     B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PO_PT, B_PT_PTR, B_PT_IDX,
     B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_ENV_GLOB, B_RED, B_PREP, B_BS_CHUNK, B_AC_SEG, B_CAMPART, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_RED, B_PREP, B_BS_CHUNK, B_AC_SEG, B_CAMPART, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_DET_TRANGE,
     B_SM_WC, B_SM_ZB, B_SM_PV, B_SM_ZK, B_SM_TASK, B_SM_TEND, B_SM_ENTRY,
     B_COUNT
@@ -693,8 +693,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
         HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
-        HIPCHECK(ctx, ctx->buf[B_ENV_GLOB].ensure(sizeof(double) * ne));
-        const size_t nred = RED_X + 2 * (4 + 2 * (size_t)ctx->W.comm.nranks);
+        const size_t nred = RED_X + 4 + 2 * (size_t)ctx->W.comm.nranks;
         HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * nred));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * nred, s));
     }
@@ -858,7 +857,6 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     W.env_tile = ctx->buf[B_ENV_TILE].as<int2>();
     W.n_env = (int)env_tile.size();
     W.env_loc = shard ? ctx->buf[B_ENV_LOC].as<double>() : nullptr;
-    W.env_glob = shard ? ctx->buf[B_ENV_GLOB].as<double>() : nullptr;
     W.red = shard ? ctx->buf[B_RED].as<double>() : nullptr;
     P.rank = W.comm.rank;
     P.nranks = W.comm.nranks;
