@@ -21,6 +21,7 @@ static constexpr int CHUNK_OBS = 256;
 static constexpr int SCH_TBUF_LD = 6 * TILE_WIN;
 static constexpr int SCH_TBUF = 80 * SCH_TBUF_LD;
 static constexpr int SUBSEG_OBS = 1024;  // observations per camera-side sub-segment (one workgroup)
+static constexpr int SUBSEG_OBS_LARGE = 1700;  // the same on windows of >= 200k observations
 static constexpr int BS_PTS = 64;     // points per back-substitution chunk
 static constexpr int BS_OBS = 512;    // observations per back-substitution chunk (a single point may exceed)
 // k_point_prep: PP_LANES lanes per active point (one aligned lane group), each taking every
