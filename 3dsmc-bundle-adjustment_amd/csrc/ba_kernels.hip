@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
@@ -974,14 +975,79 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             ape_n = P.chunk_ap[ch + 2];
             load_rec(oe + tid);
         }
-        // ---- rhs row aside: rhs_acc(r) += sum_k M'[r][k] ze[k] (wave 3, lane = camera row r), k in order
+        // ---- rhs row aside: rhs_acc(r) += sum_k M'[r][k] ze[k] (wave 3, lane = camera row r): four
+        // interleaved partial chains (k mod 4; f64 FMA dependent latency is 32 cycles), summed in a fixed order
         if (rhs_aside && wave == 3 && lane < kr) {
             const int nk = 3 * npts;
-            for (int k = 0; k < nk; ++k) rhs_acc = __builtin_fma(Mt[k * SCH_LDM + lane], zeL[k], rhs_acc);
+            double ra[4] = {0.0, 0.0, 0.0, 0.0};
+            int k = 0;
+            for (; k + 4 <= nk; k += 4)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ra[u] = __builtin_fma(Mt[(k + u) * SCH_LDM + lane], zeL[k + u], ra[u]);
+            for (; k < nk; ++k) ra[0] = __builtin_fma(Mt[k * SCH_LDM + lane], zeL[k], ra[0]);
+            rhs_acc += (ra[0] + ra[1]) + (ra[2] + ra[3]);
         }
         // ---- phase B: acc[t] += M'[16 ib..][k] M'[16 jb..][k]^T over the chunk's K
         const int ksteps = (3 * npts + 3) >> 2;
-        {
+        if ((rhs_aside && nrt == 4) || (!rhs_aside && nrt == 5)) {
+            // the two common tile shapes, each wave running a fixed tile list (slot order as tib / tjb) and
+            // loading only the row tiles its list reads, once per k-step (<= 5 LDS loads instead of 8):
+            //   span <= 10, rhs aside (10 tiles, round-robin):
+            //     wave 0: (3,3) (2,2) (1,0) | 1: (3,2) (2,1) (0,0) | 2: (3,1) (2,0) | 3: (3,0) (1,1)
+            //   span 11 / 12 (15 tiles, 4 consecutive per wave in reverse row-major order):
+            //     wave 0: (4,4) (4,3) (4,2) (4,1) | 1: (4,0) (3,3) (3,2) (3,1) | 2: (3,0) (2,2) (2,1) (2,0)
+            //     wave 3: (1,1) (1,0) (0,0)
+            const double* row = Mt + kq * SCH_LDM + rr;
+            auto run = [&](auto ntag, auto wtag) {
+                constexpr int NR = decltype(ntag)::value, W = decltype(wtag)::value;
+                constexpr int TI[2][4][4] = {{{3, 2, 1, -1}, {3, 2, 0, -1}, {3, 2, -1, -1}, {3, 1, -1, -1}},
+                                             {{4, 4, 4, 4}, {4, 3, 3, 3}, {3, 2, 2, 2}, {1, 1, 0, -1}}};
+                constexpr int TJ[2][4][4] = {{{3, 2, 0, -1}, {2, 1, 0, -1}, {1, 0, -1, -1}, {0, 1, -1, -1}},
+                                             {{4, 3, 2, 1}, {0, 3, 2, 1}, {0, 2, 1, 0}, {1, 0, 0, -1}}};
+                constexpr int S = NR == 4 ? 0 : 1;
+                constexpr auto uses = [](int r) {
+                    for (int q = 0; q < 4; ++q)
+                        if (TI[S][W][q] == r || TJ[S][W][q] == r) return true;
+                    return false;
+                };
+                double rv[5], nv[5];
+#pragma unroll
+                for (int r = 0; r < 5; ++r) rv[r] = uses(r) ? row[16 * r] : 0.0;
+                for (int s4 = 0; s4 < ksteps; ++s4) {
+                    const double* nrow = row + (s4 + 1 < ksteps ? 4 * SCH_LDM : 0);
+#pragma unroll
+                    for (int r = 0; r < 5; ++r) nv[r] = uses(r) ? nrow[16 * r] : 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)  // (constant conditions once unrolled)
+                        if (TI[S][W][q] >= 0)
+                            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(rv[TI[S][W][q] < 0 ? 0 : TI[S][W][q]],
+                                                                         rv[TJ[S][W][q] < 0 ? 0 : TJ[S][W][q]], acc[q],
+                                                                         0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 5; ++r) rv[r] = nv[r];
+                    row = nrow;
+                }
+            };
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            using I3 = std::integral_constant<int, 3>;
+            if (nrt == 4) {
+                switch (wave) {
+                    case 0: run(std::integral_constant<int, 4>{}, I0{}); break;
+                    case 1: run(std::integral_constant<int, 4>{}, I1{}); break;
+                    case 2: run(std::integral_constant<int, 4>{}, I2{}); break;
+                    default: run(std::integral_constant<int, 4>{}, I3{}); break;
+                }
+            } else {
+                switch (wave) {
+                    case 0: run(std::integral_constant<int, 5>{}, I0{}); break;
+                    case 1: run(std::integral_constant<int, 5>{}, I1{}); break;
+                    case 2: run(std::integral_constant<int, 5>{}, I2{}); break;
+                    default: run(std::integral_constant<int, 5>{}, I3{}); break;
+                }
+            }
+        } else {
             const double* row = Mt + kq * SCH_LDM + rr;
             double a[4], b[4];
 #pragma unroll
@@ -2342,6 +2408,25 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             }
             fprintf(stderr, "schur_tile %d tiles, mean cycles/tile: zero %.0f phaseA %.0f phaseB %.0f flush %.0f | max total %.0f\n",
                     P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
+            // the slowest tiles: span, chunks, points (the kernel lasts as long as its slowest tile)
+            std::vector<int> tspan(P.n_tiles), tch(P.n_tiles + 1), cap;
+            CK(hipMemcpy(tspan.data(), P.tile_span, sizeof(int) * P.n_tiles, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(tch.data(), P.tile_chunk, sizeof(int) * (P.n_tiles + 1), hipMemcpyDeviceToHost));
+            cap.resize(tch[P.n_tiles] + 1);
+            CK(hipMemcpy(cap.data(), P.chunk_ap, sizeof(int) * cap.size(), hipMemcpyDeviceToHost));
+            std::vector<std::pair<double, int>> tot(P.n_tiles);
+            for (int t = 0; t < P.n_tiles; ++t)
+                tot[t] = {(double)(h[4 * t] + h[4 * t + 1] + h[4 * t + 2] + h[4 * t + 3]), t};
+            std::sort(tot.begin(), tot.end());
+            for (int q = 0; q < 6 && q < P.n_tiles; ++q) {
+                const int t = tot[P.n_tiles - 1 - q].second;
+                fprintf(stderr, "  slow tile %d: %.0f cycles (zero %llu A %llu B %llu flush %llu) span %d chunks %d points %d\n", t,
+                        tot[P.n_tiles - 1 - q].first, h[4 * t], h[4 * t + 1], h[4 * t + 2], h[4 * t + 3], tspan[t],
+                        tch[t + 1] - tch[t], cap[tch[t + 1]] - cap[tch[t]]);
+            }
+            const int t50 = tot[P.n_tiles / 2].second;
+            fprintf(stderr, "  median tile %d: %.0f cycles span %d chunks %d points %d\n", t50, tot[P.n_tiles / 2].first,
+                    tspan[t50], tch[t50 + 1] - tch[t50], cap[tch[t50 + 1]] - cap[tch[t50]]);
         } else {
             PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
                W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf, E);
