@@ -1140,17 +1140,24 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         // Unprofiled: keep LM_AHEAD iterations in flight and follow the device through the host-mapped
         // progress word (n_decide | done << 31, written by every decision and by a failed initial
         // evaluation) instead of synchronising the stream per batch: the GPU never waits for the host.
-        // When no launch is allowed the host also checks that the stream still runs: an idle or failed
-        // stream without a published decision (a device fault) ends the polling instead of spinning.
+        // When no launch is allowed and the word has not moved for 2 ms, the host also checks that the stream
+        // still runs: an idle or failed stream without a published decision (a device fault) ends the polling
+        // instead of spinning. (Not sooner: a hipStreamQuery on a busy stream enqueues a marker behind the
+        // last launch, which cost ~5.5 us between k_final and the next iteration's first kernel when it was
+        // issued every 256 spins.)
         constexpr int LM_AHEAD = 2;
         volatile unsigned* hp = ctx->hprog;
-        unsigned w = 0;
-        for (unsigned spins = 0;;) {
+        unsigned w = 0, w_seen = ~0u;
+        auto t_seen = std::chrono::steady_clock::now();
+        for (;;) {
             w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
             if ((w >> 31) || launched > max_iter + 1) break;
+            const auto t_now = std::chrono::steady_clock::now();
+            if (w != w_seen) { w_seen = w; t_seen = t_now; }
             if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD) {
                 if (int rc = launch_iter()) return rc;
-            } else if ((++spins & 255u) == 0) {
+            } else if (t_now - t_seen > std::chrono::milliseconds(2)) {
+                t_seen = t_now;
                 const hipError_t q = hipStreamQuery(s);
                 if (q == hipSuccess) {  // idle: re-read the word once (it is written before the kernel ends)
                     w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
