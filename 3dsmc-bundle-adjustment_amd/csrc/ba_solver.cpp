@@ -1151,10 +1151,12 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         auto t_seen = std::chrono::steady_clock::now();
         for (;;) {
             w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
-            if ((w >> 31) || launched > max_iter + 1) break;
+            if (w >> 31) break;
             const auto t_now = std::chrono::steady_clock::now();
             if (w != w_seen) { w_seen = w; t_seen = t_now; }
-            if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD) {
+            // at most max_iter + 1 iterations can run (max_iter steps, then the terminal re-linearisation of the
+            // stop_next iteration): no look-ahead launch past that one
+            if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD && launched < max_iter + 1) {
                 if (int rc = launch_iter()) return rc;
             } else if (t_now - t_seen > std::chrono::milliseconds(2)) {
                 t_seen = t_now;
@@ -1173,7 +1175,7 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         // of iterations. The decisions are identical on all ranks; the host has enqueued between d and
         // d + LM_AHEAD - 1 iterations when it sees the terminating decision d: pad to d + LM_AHEAD - 1.
         if (shard && (w >> 31)) {
-            const int target = std::min((int)(w & 0x7fffffffu) + LM_AHEAD - 1, max_iter + 2);
+            const int target = std::min((int)(w & 0x7fffffffu) + LM_AHEAD - 1, max_iter + 1);
             while (launched < target)
                 if (int rc = launch_iter()) return rc;
         }
