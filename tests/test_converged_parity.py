@@ -6,7 +6,8 @@ tolerances and max_num_iterations = 75, to termination (OptimizationUtils.cpp:30
 BundleAdjustmentConfig.h:61-67). C5 (1000 cams / 500k points / 5M obs) runs 12 LM iterations with
 the tolerances off. Checked: the termination, the iteration counts, the accept / reject sequence
 (identical), the cost of every iteration and the final cost (<= 1e-6 relative, north_star's bound;
-the first iterations to 1e-9), the trust-region radius sequence (C4: exact up to rounding, every
+the first iterations to 1e-9), each step's cost change, gradient max-norm, step norm and step quality rho
+(the last pins the model cost change the device forms from the normal equations), the trust-region radius sequence (C4: exact up to rounding, every
 tr_ratio saturates the radius update; C5: 1e-3 relative, the late tr_ratios are ratios of cost
 changes of ~1e-9 relative and carry the summation-order difference of 5M-term costs), the final
 intrinsics and camera checksums."""
@@ -48,6 +49,17 @@ def test_converged_window_matches_oracle(name, radius_rtol):
     np.testing.assert_allclose(log[:, 0], tr[:, 0], rtol=1e-6)  # cost of every iteration
     np.testing.assert_allclose(log[:3, 0], tr[:3, 0], rtol=1e-9)
     np.testing.assert_allclose(log[:, 5], tr[:, 5], rtol=radius_rtol)
+    # iteration by iteration: the cost change, the gradient max-norm, the step norm and the step quality
+    # rho = cost change / model cost change. The oracle forms the model cost change as Ceres does,
+    # -(J d)^T (f + J d / 2); the device from the normal equations, 0.5 (g~^T y + y^T D~ y),
+    # so rho pins that identity on every step, not only through the final cost.
+    scale = np.abs(tr[:, 0]).max()
+    np.testing.assert_allclose(log[:, 1], tr[:, 1], rtol=radius_rtol, atol=1e-9 * scale)  # cost change
+    # gradient max-norm of every linearised point (the terminal row of a solve that stops on a tolerance
+    # after its last step has none: the oracle repeats the previous value, the device log leaves 0)
+    np.testing.assert_allclose(log[:-1, 2], tr[:-1, 2], rtol=max(radius_rtol, 1e-6))
+    np.testing.assert_allclose(log[:, 3], tr[:, 3], rtol=max(radius_rtol, 1e-6))             # |step|
+    np.testing.assert_allclose(log[:, 4], tr[:, 4], rtol=max(radius_rtol, 1e-6), atol=1e-9)  # rho
     np.testing.assert_allclose(p.intr, g["final_intrinsics"], rtol=1e-6)
     cs = g["cams_checksum"]
     assert abs(np.sum(p.cams * p.cams) - cs["sum_sq"]) <= 1e-9 * cs["sum_sq"]
