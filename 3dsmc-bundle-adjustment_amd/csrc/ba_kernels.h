@@ -22,8 +22,8 @@ static constexpr int SCH_TBUF_LD = 6 * TILE_WIN;
 static constexpr int SCH_TBUF = 80 * SCH_TBUF_LD;
 static constexpr int SUBSEG_OBS = 1024;  // observations per camera-side sub-segment (one workgroup)
 static constexpr int SUBSEG_OBS_LARGE = 1700;  // the same on windows of >= 200k observations
-static constexpr int BS_PTS = 64;     // points per back-substitution chunk
-static constexpr int BS_OBS = 512;    // observations per back-substitution chunk (a single point may exceed)
+static constexpr int BS_PTS = 128;    // points per back-substitution chunk (C4: 64 / 512 29.4 us, 128 / 1024 27.6, 256 / 2048 33.1)
+static constexpr int BS_OBS = 1024;   // observations per back-substitution chunk (a single point may exceed)
 // k_point_prep: PP_LANES lanes per active point (one aligned lane group), each taking every
 // PP_LANES-th observation of the point; the group sums by xor-shuffles (fixed order)
 static constexpr int PP_LANES_MAX = 4;
