@@ -382,6 +382,21 @@ __device__ __forceinline__ void lm_decide_local(LmState& S, const LmParams& prm,
     lg[1] = cost_change; lg[3] = step_norm; lg[4] = rho; lg[5] = S.radius;
 }
 
+// Publishes the LM progress to the host-mapped block (one thread): the terminal state first (8-byte
+// system-scope stores, drained), then the word n_decide | done << 31.
+__device__ inline void publish_progress(unsigned* progress, const LmState& S) {
+    if (S.done) {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(progress) + PROG_STATE_OFF);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(LmState) / 8); ++k)
+            __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_store(progress, (unsigned)S.n_decide | (S.done ? 0x80000000u : 0u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The decision on a state the caller has already loaded (S0) and the step scalars in registers: one store
 // of the new state, no global round trip between the reductions and the decision (k_final).
 __device__ inline void lm_decide_pre(const LmState& S0, LmState* __restrict__ st, const LmParams& prm, double lin0,
@@ -392,9 +407,7 @@ __device__ inline void lm_decide_pre(const LmState& S0, LmState* __restrict__ st
     S.n_decide += 1;
     S.stop_next = !S.done && S.iter >= prm.max_iter;
     *st = S;
-    if (prm.progress)
-        __hip_atomic_store(prm.progress, (unsigned)S.n_decide | (S.done ? 0x80000000u : 0u), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (prm.progress) publish_progress(prm.progress, S);
 }
 __device__ inline void lm_decide_body(LmState* __restrict__ st, const LmParams& prm, const double* __restrict__ lin,
                                       const double* __restrict__ scal, double* __restrict__ log) {

@@ -203,6 +203,12 @@ struct LmParams {
     int max_iter, max_invalid;
     unsigned* progress;  // host-mapped word: n_decide | done << 31 after every decision (nullptr: none)
 };
+// Host-mapped progress block (LmParams::progress): the word at byte 0 and, at byte PROG_STATE_OFF, a copy of
+// the terminal LmState, stored (system scope, drained) before the word's done bit: the host reads the summary
+// there instead of a device-to-host copy behind a stream synchronisation.
+static constexpr int PROG_STATE_OFF = 64;
+static constexpr int PROG_BYTES = PROG_STATE_OFF + (int)((sizeof(LmState) + 63) / 64 * 64);
+static_assert(sizeof(LmState) % 8 == 0, "LmState is copied as 8-byte words");
 enum LmMsg { MSG_NONE = 0, MSG_MAX_ITER, MSG_GRAD_TOL, MSG_MIN_RADIUS, MSG_PARAM_TOL, MSG_FUNC_TOL, MSG_INVALID,
              MSG_EVAL_FAIL, MSG_TIMEOUT };
 // chol_flag bits: the reduced-system factorisation hit a non-positive pivot (a linear-solver failure,

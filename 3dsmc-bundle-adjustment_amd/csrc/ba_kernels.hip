@@ -599,8 +599,9 @@ __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaCo
     }
 }
 
-// Fused linearisation launch of the LM loop (unsharded, default mode): point workgroups [0, nb_pp) run
-// k_point_prep's point side, the rest k_cam_side's sub-segments (gated on an accepted step). The point
+// Fused linearisation launch of the LM loop (default mode): point workgroups [0, nb_pp) run
+// k_point_prep's point side, the rest k_cam_side's sub-segments (gated on an accepted step). mode 0
+// (IterationZero): the points' column norms and the ungated camera side. The point
 // side alone is one long dependent chain per thread at ~1.5 waves per SIMD; the camera sub-segments fill
 // the CUs it leaves idle. The envelope tiles, which need the camera sums, ride in k_schur_tile.
 template <int PP_LANES>
@@ -608,9 +609,9 @@ __global__ __launch_bounds__(TPB) void k_lin_point(DevProblem P, BaConsts c, con
                                                    const double* __restrict__ scale, double* __restrict__ cnp,
                                                    double* __restrict__ pdata, double* __restrict__ part, int nb_pp,
                                                    double* __restrict__ cpart, double* __restrict__ seg_intr,
-                                                   double* __restrict__ gmax_word) {
-    if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES>(P, c, st, 1, scale, cnp, pdata, part, blockIdx.x);
-    else cam_side_block(P, c, st, 1, cpart, seg_intr, gmax_word, blockIdx.x - nb_pp);
+                                                   double* __restrict__ gmax_word, int mode) {
+    if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
+    else cam_side_block(P, c, st, mode, cpart, seg_intr, gmax_word, blockIdx.x - nb_pp);
 }
 
 // Jacobi scale (Ceres: 1 / (1 + sqrt(squared column norm)), iteration 0 only)
@@ -2190,9 +2191,10 @@ __global__ __launch_bounds__(TPB) void k_xnorm_init(DevProblem P, const double* 
             st->termination = 2;  // FAILURE
             st->msg = MSG_EVAL_FAIL;
             // the host follows the progress word: publish the termination (no decision will run)
-            if (progress)
-                __hip_atomic_store(progress, (unsigned)st->n_decide | 0x80000000u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            if (progress) {
+                const LmState S = *st;
+                publish_progress(progress, S);
+            }
         }
     }
 }
@@ -2290,9 +2292,32 @@ int schur_tile_slots() {
     return per_cu * ncu;
 }
 
+// k_lin_point over nb point workgroups + the camera sub-segments (mode 1: LM loop, mode 0: IterationZero)
+static hipError_t launch_lin_point(const DevProblem& P, const BaConsts& c, int mode, DevWork& W, hipStream_t s,
+                                   Prof* pf) {
+    const int nb = pp_blocks(P.n_ap);
+    const int kid = mode ? K_LIN_POINT : K_CAM_SIDE;
+    if (nb + P.n_seg > 0) switch (pp_lanes()) {
+        case 1: PL(kid, k_lin_point<1>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
+                   W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
+        case 2: PL(kid, k_lin_point<2>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
+                   W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
+        default: PL(kid, k_lin_point<4>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
+                    W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
+    }
+    return hipSuccess;
+}
+
+// IterationZero of the fused path: the points' column norms ride in the camera-side launch (k_lin_point
+// mode 0), so launch_scale has no point pass of its own
+static bool zero_fused(const DevProblem& P, const DevWork& W) { return W.fused && P.n_ap > 0; }
+
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf) {
     if (gated && W.fused) return hipSuccess;  // the LM loop's camera side runs inside k_lin_point (launch_build)
-    if (P.n_seg > 0)
+    if (!gated && zero_fused(P, W)) {
+        CK(launch_lin_point(P, c, 0, W, s, pf));
+        if (P.n_seg == 0) CK(hipMemsetAsync(W.lin + 1, 0, sizeof(double), s));
+    } else if (P.n_seg > 0)
         PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr,
            W.lin + 1);
     else
@@ -2317,7 +2342,7 @@ hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, D
 }
 
 hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf) {
-    if (P.n_ap > 0)
+    if (P.n_ap > 0 && !zero_fused(P, W))
         CK(launch_point_prep(P, c, 0, W, s, pf));
     const int nt = 6 * P.nac + 3 * P.n_ap + 4;
     PL(K_SCALE, k_scale, dim3(nblocks(nt, TPB)), dim3(TPB), 0, s, P, W.camdata, W.cnp, W.lin, jacobi, W.scale);
@@ -2325,22 +2350,32 @@ hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevW
 }
 
 // Start of a solve: both parameter slots from the prepared initial values, and the fresh LM state
-// (one launch instead of six copies and a host-to-device state copy).
+// (one launch instead of six copies and a host-to-device state copy); fused path: also zeroes S and rhs,
+// the atomic targets of the first assembly (grid-stride, 16-byte stores).
 __global__ __launch_bounds__(TPB) void k_reset(DevProblem P, LmState st0, LmState* __restrict__ st,
                                                const double* __restrict__ cams0, const double* __restrict__ pts0,
-                                               const double* __restrict__ K0, int ncd, int npd) {
+                                               const double* __restrict__ K0, int ncd, int npd,
+                                               double* __restrict__ S, size_t nS2, double* __restrict__ rhs,
+                                               int nrhs) {
     const int t = blockIdx.x * TPB + threadIdx.x;
     if (t < ncd) { const double v = cams0[t]; P.cams[0][t] = v; P.cams[1][t] = v; }
     if (t < npd) { const double v = pts0[t]; P.pts[0][t] = v; P.pts[1][t] = v; }
     if (t < 4) { const double v = K0[t]; P.K[0][t] = v; P.K[1][t] = v; }
     if (t == 0) *st = st0;
+    if (t < nrhs) rhs[t] = 0.0;
+    const size_t stride = (size_t)gridDim.x * TPB;
+    for (size_t e = t; e < nS2; e += stride) reinterpret_cast<double2*>(S)[e] = double2{0.0, 0.0};
 }
 
 hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
                         const double* K0, int n_cams, int n_points, hipStream_t s) {
     const int ncd = 7 * n_cams, npd = 3 * n_points;
-    hipLaunchKernelGGL(k_reset, dim3(nblocks(std::max({ncd, npd, 4}), TPB)), dim3(TPB), 0, s, P, st0, W.st, cams0, pts0,
-                       K0, ncd, npd);
+    // fused path: S (npad^2, even: npad is a multiple of 16) and rhs are zeroed here too
+    const size_t nS2 = W.fused ? (size_t)P.npad * P.npad / 2 : 0;
+    const int nrhs = W.fused ? P.npad : 0;
+    const int nb = std::max(nblocks(std::max({ncd, npd, nrhs, 4}), TPB), (int)std::min<size_t>(nS2 / (4 * TPB), 2048));
+    hipLaunchKernelGGL(k_reset, dim3(nb), dim3(TPB), 0, s, P, st0, W.st, cams0, pts0, K0, ncd, npd, W.S, nS2, W.rhs,
+                       nrhs);
     return hipGetLastError();
 }
 
@@ -2357,15 +2392,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     // blocks, LM diagonal, pad (rank 0 only), the points' intrinsics terms, rhs, chol_flag
     EnvArgs E{};
     if (W.fused) {  // point side + gated camera side in one launch; the envelope tiles ride in k_schur_tile
-        const int nb = pp_blocks(P.n_ap);
-        if (nb + P.n_seg > 0) switch (pp_lanes()) {
-            case 1: PL(K_LIN_POINT, k_lin_point<1>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
-                       W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
-            case 2: PL(K_LIN_POINT, k_lin_point<2>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
-                       W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
-            default: PL(K_LIN_POINT, k_lin_point<4>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp,
-                        W.pdata, W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1); break;
-        }
+        CK(launch_lin_point(P, c, 1, W, s, pf));
         // unsharded: the envelope tiles finish the camera sums and lin (fin 1); landmark shard: they write this
         // rank's terms and sums for the folded exchange (fin 2; camdata_loc = [camera sums | intrinsics sums])
         const int ncd = P.nac * CAMDATA;

@@ -74,6 +74,8 @@ struct ba_context {
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     unsigned* hprog = nullptr;  // host-mapped LM progress word (LmParams::progress)
     unsigned* dprog = nullptr;  // its device address
+    double* hres = nullptr;     // pinned staging of the solved cameras + intrinsics (async device-to-host copies)
+    size_t hres_cap = 0;        // its capacity in doubles
     DevBuf buf[B_COUNT];
     std::string err;
     // host-side structure of the last prepared problem
@@ -220,7 +222,7 @@ ba_context* ba_create(const ba_options* opts) {
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->hprog, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->hprog, PROG_BYTES, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->dprog, ctx->hprog, 0);
     if (ctx->opts.profile_kernels) {
         for (int i = 0; i < 2 * Prof::MAXP && e == hipSuccess; ++i) e = hipEventCreate(&ctx->prof.ev[i]);
@@ -248,6 +250,7 @@ void ba_destroy(ba_context* ctx) {
     if (ctx->prof_events)
         for (int i = 0; i < 2 * Prof::MAXP; ++i) hipEventDestroy(ctx->prof.ev[i]);
     if (ctx->hprog) hipHostFree(ctx->hprog);
+    if (ctx->hres) hipHostFree(ctx->hres);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1105,11 +1108,8 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     prm.progress = ctx->dprog;
     if (ctx->hprog) __atomic_store_n(ctx->hprog, 0u, __ATOMIC_RELEASE);
 
-    // fused path: S and rhs are the atomic targets of the first assembly (later ones are zeroed in-loop)
-    if (W.fused) {
-        HIPCHECK(ctx, hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
-        HIPCHECK(ctx, hipMemsetAsync(W.rhs, 0, sizeof(double) * P.npad, s));
-    }
+    // fused path: S and rhs, the atomic targets of the first assembly (later ones are zeroed in-loop), were
+    // zeroed by k_reset
     // IterationZero: cost, gradient, column norms -> Jacobi scale, |x| (the small-window kernel does its own)
     if (!W.sm.on) {
         HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
@@ -1181,8 +1181,12 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
             while (launched < target)
                 if (int rc = launch_iter()) return rc;
         }
-        HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
-        HIPCHECK(ctx, hipStreamSynchronize(s));
+        if (w >> 31) {  // the terminal state was stored to the host-mapped block before the done bit
+            std::memcpy(&S, reinterpret_cast<const char*>(ctx->hprog) + PROG_STATE_OFF, sizeof(LmState));
+        } else {
+            HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
+            HIPCHECK(ctx, hipStreamSynchronize(s));
+        }
     }
     // profiled (HIP events around every launch) or no host-mapped word: batches of iterations, one
     // stream synchronisation per batch (the same batch sizes on every landmark shard)
@@ -1216,13 +1220,24 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
             print_row(it, r[0], r[1], r[2], r[3], r[4], r[5], 0.0, 0.0);
         }
     }
-    // copy the best (= last accepted) parameters back in place
+    // copy the best (= last accepted) parameters back in place: cameras + intrinsics by DMA into pinned
+    // staging (no host-side staging round trip per copy), the points straight into the caller's buffer
     const int cur = S.cur;
-    HIPCHECK(ctx, hipMemcpyAsync(p->cams, P.cams[cur], sizeof(double) * 7 * (size_t)p->n_cams, hipMemcpyDeviceToHost, s));
+    const size_t ncd = 7 * (size_t)p->n_cams;
+    if (ctx->hres_cap < ncd + 4) {
+        if (ctx->hres) HIPCHECK(ctx, hipHostFree(ctx->hres));
+        ctx->hres = nullptr;
+        ctx->hres_cap = 0;
+        HIPCHECK(ctx, hipHostMalloc((void**)&ctx->hres, sizeof(double) * (ncd + 4), hipHostMallocDefault));
+        ctx->hres_cap = ncd + 4;
+    }
+    if (ncd) HIPCHECK(ctx, hipMemcpyAsync(ctx->hres, P.cams[cur], sizeof(double) * ncd, hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->hres + ncd, P.K[cur], sizeof(double) * 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipMemcpyAsync(p->points, P.pts[cur] + 3 * (size_t)ctx->gather_off, sizeof(double) * 3 * (size_t)p->n_points,
                                  hipMemcpyDeviceToHost, s));
-    HIPCHECK(ctx, hipMemcpyAsync(p->intr, P.K[cur], sizeof(double) * 4, hipMemcpyDeviceToHost, s));
     HIPCHECK(ctx, hipStreamSynchronize(s));
+    if (ncd) std::memcpy(p->cams, ctx->hres, sizeof(double) * ncd);
+    std::memcpy(p->intr, ctx->hres + ncd, sizeof(double) * 4);
     const double t1 = now_ms();
     sum->time_lm_ms = t1 - tl0;
     sum->time_total_ms = t1 - t0;
