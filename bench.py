@@ -13,7 +13,11 @@ Timed region: ba_solve_prepared() with max_num_iterations = K and the
 convergence tolerances disabled, so exactly K LM iterations run on a window
 already resident in HBM (ba_prepare(), the host structure build + upload, is
 timed separately as setup_ms). Five timed runs after the warmup; value is the
-median (BASELINE.md's protocol).
+median (BASELINE.md's protocol). Each timed run is preceded by one untimed
+re-solve of the same prepared window (identical work from the same prepared
+start; MIBA_BENCH_WARM_EACH=0 turns it off): the host-side prepare leaves the
+GPU idle for ~20 ms, and without it the timed solve runs ~3.5 % slower while
+the clocks ramp back up (profiles/r02_bench_c4_warm_ab.txt).
 
 --gpus N (torchrun, one rank per GPU, RCCL over xGMI): strong scaling of ONE
 window: the BASELINE window's landmarks are split N ways (miba.shard.
@@ -174,6 +178,11 @@ def time_runs(solver, prob0, steps, runs):
         ts = time.perf_counter()
         solver.prepare(prob)
         setup.append((time.perf_counter() - ts) * 1e3)
+        if os.environ.get("MIBA_BENCH_WARM_EACH", "1") == "1":
+            # untimed re-solve of the same prepared window (identical work, from the same prepared start):
+            # the host-side prepare above leaves the GPU idle for ~20 ms, and the timed solve should not
+            # pay for its clocks ramping back up
+            solver.solve_prepared(prob.copy())
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
