@@ -10,7 +10,7 @@ import subprocess
 from .capi import BaKernelStat, BaOptions, BaProblem, BaSummary
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmiba.so")
+LIB_PATH = os.environ.get("MIBA_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libmiba.so")  # override: A/B builds
 
 # exported symbols, exactly those declared in include/ba.h and include/ba_io.h
 EXPORTS = (
