@@ -267,11 +267,20 @@ static constexpr int NCT = (NCONTRIB + NWE - 2) / (NWE - 1);  // tiles per helpe
 struct ContribTile {
     int ib, cb, aoff, boff, ldd;
     double sign;
-    bool valid, rhs;
+    bool valid, rhs, gram;
 };
+// Tile GRAM_TILE (k_bcr_split only, past the k_bcr_contrib map): the Gram x^T x of the block's
+// forward-solved right-hand sides x = [b_a | B] (5 of the 8 x columns). Summed over all blocks it is
+// [b_a | B]^T A^-1 [b_a | B] (A = L L^T in elimination order, x_i = (L^-1 [b_a | B])_i), which is all
+// the 4x4 border system needs: (C - B^T A^-1 B) y_k = b_k - B^T A^-1 b_a.
+static constexpr int GRAM_TILE = NCONTRIB;
 __device__ __forceinline__ ContribTile contrib_tile(int t, bool has_r) {
-    ContribTile c{0, 0, 0, 0, BB, 1.0, true, false};
-    if (t < 20) {
+    ContribTile c{0, 0, 0, 0, BB, 1.0, true, false, false};
+    if (t == GRAM_TILE) {
+        c.aoff = c.boff = 2 * BB;
+        c.ldd = RC;
+        c.rhs = c.gram = true;
+    } else if (t < 20) {
         c.valid = t < 10 || has_r;
         int p = 0, rem = t % 10;
         while (rem > p) { rem -= p + 1; ++p; }
@@ -799,8 +808,46 @@ __global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ 
 // step of its cameras (was k_update_cams): lanes < BCR_CAMS, workgroup 0 also the intrinsics; one
 // partial per workgroup of the step scalars for k_final. PUB: inside k_bcr_split, after every
 // block's back-substitution flag, so Bp and Y are read with sc1 loads; bk = [b_k | S_kk packed].
+// 4x4 border system (C - sum B^T V) y_k = b_k - sum B^T u on one thread: bk = [b_k | S_kk lower packed],
+// red[m * 5 + c] = (B^T [u | V])[m][c]. bad: a non-positive pivot (replaced by 1).
+__device__ __forceinline__ void border_solve4(const double* bk, const double* red, double* yk, bool& bad) {
+    double Cm[16], bp[4];
+    int q = 0;
+    for (int mm = 0; mm < 4; ++mm)
+        for (int l = 0; l <= mm; ++l, ++q) {
+            const double v = bk[4 + q];
+            Cm[mm * 4 + l] = v - red[mm * 5 + 1 + l];
+            Cm[l * 4 + mm] = v - red[l * 5 + 1 + mm];
+        }
+    for (int mm = 0; mm < 4; ++mm) bp[mm] = bk[mm] - red[mm * 5];
+    double Lm[16] = {0};
+    for (int j = 0; j < 4; ++j) {
+        double d = Cm[j * 4 + j];
+        for (int k = 0; k < j; ++k) d -= Lm[j * 4 + k] * Lm[j * 4 + k];
+        if (!(d > 0.0)) { bad = true; d = 1.0; }
+        Lm[j * 4 + j] = sqrt(d);
+        for (int r = j + 1; r < 4; ++r) {
+            double v = Cm[r * 4 + j];
+            for (int k = 0; k < j; ++k) v -= Lm[r * 4 + k] * Lm[j * 4 + k];
+            Lm[r * 4 + j] = v / Lm[j * 4 + j];
+        }
+    }
+    double z[4];
+    for (int r = 0; r < 4; ++r) {
+        double v = bp[r];
+        for (int k = 0; k < r; ++k) v -= Lm[r * 4 + k] * z[k];
+        z[r] = v / Lm[r * 4 + r];
+    }
+    for (int r = 3; r >= 0; --r) {
+        double v = z[r];
+        for (int k = r + 1; k < 4; ++k) v -= Lm[k * 4 + r] * z[k];
+        z[r] = v / Lm[r * 4 + r];
+    }
+    for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
+}
+
 static constexpr int TPB_BD = 64;
-static constexpr int BP_CHUNK = 32;  // border partials staged in LDS per round (20 doubles per block)
+static constexpr int BP_CHUNK = 32;  // blocks' border partials (20 doubles) / Grams (25) staged in LDS per round
 template <bool PUB>
 __device__ __forceinline__ void border_apply(const LmState* __restrict__ st, const DevProblem& P, double* __restrict__ rhs,
                                              const BcrWork& Bw, int* __restrict__ flag, const BaConsts& c,
@@ -826,40 +873,8 @@ __device__ __forceinline__ void border_apply(const LmState* __restrict__ st, con
     if (tid < 20) red[tid] = bsum;
     __syncthreads();
     if (tid == 0) {
-        double Cm[16], bp[4];
-        int q = 0;
-        for (int mm = 0; mm < 4; ++mm)
-            for (int l = 0; l <= mm; ++l, ++q) {
-                const double v = bk[4 + q];
-                Cm[mm * 4 + l] = v - red[mm * 5 + 1 + l];
-                Cm[l * 4 + mm] = v - red[l * 5 + 1 + mm];
-            }
-        for (int mm = 0; mm < 4; ++mm) bp[mm] = bk[mm] - red[mm * 5];
         bool bad = false;
-        double Lm[16] = {0};
-        for (int j = 0; j < 4; ++j) {
-            double d = Cm[j * 4 + j];
-            for (int k = 0; k < j; ++k) d -= Lm[j * 4 + k] * Lm[j * 4 + k];
-            if (!(d > 0.0)) { bad = true; d = 1.0; }
-            Lm[j * 4 + j] = sqrt(d);
-            for (int r = j + 1; r < 4; ++r) {
-                double v = Cm[r * 4 + j];
-                for (int k = 0; k < j; ++k) v -= Lm[r * 4 + k] * Lm[j * 4 + k];
-                Lm[r * 4 + j] = v / Lm[j * 4 + j];
-            }
-        }
-        double z[4];
-        for (int r = 0; r < 4; ++r) {
-            double v = bp[r];
-            for (int k = 0; k < r; ++k) v -= Lm[r * 4 + k] * z[k];
-            z[r] = v / Lm[r * 4 + r];
-        }
-        for (int r = 3; r >= 0; --r) {
-            double v = z[r];
-            for (int k = r + 1; k < 4; ++k) v -= Lm[k * 4 + r] * z[k];
-            z[r] = v / Lm[r * 4 + r];
-        }
-        for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
+        border_solve4(bk, red, yk, bad);
         if (bad && i == 0) raise_flag(flag, FLAG_NOT_PD);
     }
     __syncthreads();
@@ -884,6 +899,44 @@ __device__ __forceinline__ void border_apply(const LmState* __restrict__ st, con
     if (tid < BCR_CAMS && ac < P.nac)
         update_camera(P, c, cur, radius, scale, camdata, ac, ybl + 6 * tid, delta, acc);
     else if (i == 0 && tid == BCR_CAMS)
+        update_intrinsics(P, c, cur, radius, scale, lin, yk, delta, acc);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+    if (tid == 0) {
+        part[PART_UPD_SN2 * P.part_stride + i] = acc[0];
+        part[PART_UPD_MCC * P.part_stride + i] = acc[1];
+        part[PART_UPD_COST * P.part_stride + i] = acc[2];
+        part[PART_UPD_XN2 * P.part_stride + i] = acc[3];
+    }
+}
+// k_bcr_split's step of block i once its y rows [u | V] (LDS, stride RC) and y_k (LDS) are known:
+// y_a = u - V y_k into rhs, the block's camera steps (wave 0) and their model-cost / norm terms
+// (part[*][i]); the root block also y_k itself and the intrinsics step. No wait for other blocks.
+__device__ __forceinline__ void block_step(const LmState* __restrict__ st, const DevProblem& P, double* __restrict__ rhs,
+                                           const BaConsts& c, const double* __restrict__ scale,
+                                           const double* __restrict__ camdata, const double* __restrict__ lin,
+                                           double* __restrict__ delta, double* __restrict__ part, int i, bool intr,
+                                           const double* Yrows, const double* yk, double* ybl) {
+    const int tid = threadIdx.x;
+    const int b0 = i * G_DOF, nd = 6 * P.nac;
+    if (tid < G_DOF && b0 + tid < nd) {
+        const double* y = Yrows + tid * RC;
+        const double ya = y[0] - (y[1] * yk[0] + y[2] * yk[1] + y[3] * yk[2] + y[4] * yk[3]);
+        rhs[b0 + tid] = ya;
+        ybl[tid] = ya;
+    }
+    if (intr && tid < 4) rhs[P.kb + tid] = yk[tid];
+    __syncthreads();
+    if (tid >= 64) return;  // the camera step is wave 0's
+    const int cur = st->cur;
+    const double radius = st->radius;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
+    const int ac = i * BCR_CAMS + tid;
+    if (tid < BCR_CAMS && ac < P.nac)
+        update_camera(P, c, cur, radius, scale, camdata, ac, ybl + 6 * tid, delta, acc);
+    else if (intr && tid == BCR_CAMS)
         update_intrinsics(P, c, cur, radius, scale, lin, yk, delta, acc);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
@@ -1179,10 +1232,10 @@ struct HLds {
     double rdiag[BB];
     double W[4][256];
     double Bl[4 * BB];
-    double red[80];
+    double red[100];  // border partials / the root's Gram quarters
     double yl[RSZ], yr[RSZ], yt[RSZ];
-    double bk[16], bred[20], byk[4], bybl[G_DOF];  // fused border: S_kk / b_k, sums, y_k, the block's y rows
-    double bpl[20 * 32];                            // fused border: staged partials (BP_CHUNK blocks)
+    double bk[16], bred[25], byk[4], bybl[G_DOF];  // border: S_kk / b_k, sums / Gram, y_k, the block's y rows
+    double bpl[25 * 32];                            // staged border partials / Grams (BP_CHUNK blocks)
     int ok;
     int pre;  // next panel's flags already set (prefetch)
 };
@@ -1208,10 +1261,11 @@ __device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok, const u
 }
 // Wave 0 polls every block's flag (lane j: blocks j, j + 64, ...; relaxed, bounded); uniform result.
 // The payload behind these flags is read with sc1 loads only (ld_pub), so no acquire fence.
-__device__ bool wait_all_eq(const unsigned* f, int n, unsigned epoch, int* lds_ok) {
+__device__ bool wait_all_eq(const unsigned* f, int n, unsigned epoch, int* lds_ok, int skip = -1) {
     if (threadIdx.x < 64) {
         int ok = 1;
         for (int j = threadIdx.x; j < n && ok; j += 64) {
+            if (j == skip) continue;
             unsigned cnt = 0;
             while (__hip_atomic_load((gu32*)const_cast<unsigned*>(f + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
                    epoch) {
@@ -1277,18 +1331,20 @@ __device__ __forceinline__ HelperMap helper_map(int role, int wave, bool root) {
 #pragma unroll
         for (int q = 0; q < NCT8; ++q) {
             const int t = (NWE - 1 - wave) + NWE * q;
-            h.tiles[q] = t < NCONTRIB ? t : -1;
+            h.tiles[q] = t <= GRAM_TILE ? t : -1;  // tile 44 (the Gram) lands on wave 3, which has 5 others
         }
         return h;
     }
     const bool B = role == 2;
     h.cb = wave < 4 ? (B ? 4 + wave : wave) : -1;  // one XL / XR tile per SIMD; x rows: x_rows_* below
-    // A: UL (0..9) + rL (36..39); B: UR (10..19) + rR (40..43); entry w and w + 8 of the list
+    // A: UL (0..9) + rL (36..39); B: UR (10..19) + rR (40..43) + the Gram (entry 14: wave 6);
+    // entry w and w + 8 of the list
 #pragma unroll
     for (int q = 0; q < NCT8; ++q) {
         const int e = wave + NWE * q;
         int t = -1;
         if (q < 2 && e < 14) t = e < 10 ? (B ? 10 + e : e) : (B ? 40 + e - 10 : 36 + e - 10);
+        if (q < 2 && e == 14 && B) t = GRAM_TILE;
         h.tiles[q] = t;
     }
     return h;
@@ -1487,21 +1543,15 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const bool roleB = NH == 1 || role == 2;  // owns XR, the fill and the back-substitution
     if (root && roleA) return;                // the root has only the x columns (helper B)
     HLds& L = *reinterpret_cast<HLds*>(smem);
-    if (roleB && tid < 14) {  // border inputs [b_k | S_kk packed], read before the border overwrites rhs
+    // Border without a second pass (was k_bcr_border): every block's helper B publishes the Gram of its
+    // forward-solved x = [b_a | B] with its contributions; the root sums them with its own, solves the
+    // 4x4 border system before its back-substitution and publishes y_k with y_root, so each block
+    // applies its camera step right after its own back-substitution (no wait for every block).
+    if (root && tid < 14) {  // border inputs [b_k | S_kk packed]
         int q = tid - 4, mm = 0;
         while (q > mm) { q -= mm + 1; ++mm; }
         L.bk[tid] = tid < 4 ? rhs[P.kb + tid] : S[(size_t)(P.kb + mm) * ld + P.kb + q];
     }
-    // fused border (was k_bcr_border): after this block's back-substitution flag, wait for every
-    // block's, then solve the border redundantly and apply the block's camera step
-    auto border = [&]() {
-        if (!wait_all_eq(back_f, nblk, epoch, &L.ok)) {
-            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-            return;
-        }
-        border_apply<true>(st, P, rhs, Bw, flag, c, scale, camdata, lin, delta, part, i, L.bk, L.bred, L.byk, L.bybl,
-                           L.bpl);
-    };
     {
         const bool has_r0 = i + 1 < nblk;
         if (mi == 0) {
@@ -1523,7 +1573,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         double rv = 0.0;
         if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
         L.X[r * XW + 2 * BB + c] = rv;
-        if (roleB && tid < 4 * BB) L.Bl[tid] = border_load(P, S, i, tid);
     }
     for (int m = 0; m < mi; ++m) {
         const int s = 1 << m, a = i - s, b = i + s;
@@ -1561,6 +1610,24 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         const double rb = b < nblk ? ld_pub(Bw.rL + (size_t)b * RSZ + tid) : 0.0;
         const int r = tid >> 3, c = tid & 7;
         L.X[r * XW + 2 * BB + c] = (L.X[r * XW + 2 * BB + c] - ra) - rb;
+    }
+    if (root) {
+        // the other blocks' Grams (published with their helper-B contributions, which the root's own
+        // levels already waited on or soon will), summed in block order; overlaps F's first panel
+        if (!wait_all_eq((NH == 2 ? elimB_f : elim_f), nblk, epoch, &L.ok, i)) {
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
+            return;
+        }
+        double gsum = 0.0;
+        for (int j0 = 0; j0 < nblk; j0 += BP_CHUNK) {
+            const int nb = nblk - j0 < BP_CHUNK ? nblk - j0 : BP_CHUNK;
+            for (int e = tid; e < 25 * nb; e += TPB_E) L.bpl[e] = j0 + e / 25 == i ? 0.0 : ld_pub(Bw.Bp + (size_t)(j0 + e / 25) * 32 + e % 25);
+            __syncthreads();
+            if (tid < 25)
+                for (int b = 0; b < nb; ++b) gsum += L.bpl[25 * b + tid];
+            __syncthreads();
+        }
+        if (tid < 25) L.bred[tid] = gsum;
     }
     TLS(1);
     double* X = root ? L.X + 2 * BB : L.X;
@@ -1755,10 +1822,11 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 const ContribTile ct = contrib_tile(t < 0 ? 0 : t, has_r);
                 const bool on = t >= 0 && ct.valid;
                 const bool bok = on && (!ct.rhs || rr < RC);
+                const bool aok = on && (!ct.gram || rr < RC);
 #pragma unroll
                 for (int s4 = 0; s4 < 4; ++s4) {
                     const double* row = L.X + (16 * kb + 4 * s4 + kk) * XW;
-                    av[q][s4] = on ? row[ct.aoff + 16 * ct.ib + rr] : 0.0;
+                    av[q][s4] = aok ? row[ct.aoff + 16 * ct.ib + rr] : 0.0;
                     bv[q][s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
                 }
             }
@@ -1789,19 +1857,38 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             Yl[tid] = L.X[r * XW + 2 * BB + c];
         }
         __syncthreads();
-        trsm_t_lanes(L.L, L.rdiag, Yl);
-        st_pub(Bw.Y + (size_t)i * RSZ + tid, Yl[tid]);
-        if (tid < 4) Bw.bk[tid] = rhs[P.kb + tid];
-        if (tid >= 4 && tid < 14) {
-            int q = tid - 4, mm = 0;
-            while (q > mm) { q -= mm + 1; ++mm; }
-            Bw.bk[tid] = S[(size_t)(P.kb + mm) * ld + P.kb + q];
+        // the root's Gram z^T z: 25 entries x 4 row quarters (fixed-order sums)
+        if (tid < 100) {
+            const int q = tid >> 2, part4 = tid & 3, gr = q / 5, gc = q % 5;
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 16 * part4; k < 16 * part4 + 16; ++k) acc = __builtin_fma(Yl[k * RC + gr], Yl[k * RC + gc], acc);
+            L.red[tid] = acc;
         }
         __syncthreads();
-        border_partial(L.Bl, Yl, L.red, i, Bw.Bp);
+        // border system on one lane of wave 4 while waves 0-3 back-solve [u | V] = Cf^-T z
+        if (tid == 256) {
+            double g20[20];  // (B^T A^-1 [b_a | B])[m][c] = G[1 + m][c]
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int cc = 0; cc < 5; ++cc) {
+                    const int q = (1 + m) * 5 + cc;
+                    g20[m * 5 + cc] = L.bred[q] + (((L.red[4 * q] + L.red[4 * q + 1]) + L.red[4 * q + 2]) + L.red[4 * q + 3]);
+                }
+            bool bad = false;
+            border_solve4(L.bk, g20, L.byk, bad);
+            if (bad) raise_flag(flag, FLAG_NOT_PD);
+        }
+        trsm_t_lanes(L.L, L.rdiag, Yl);  // ends with a barrier
+        st_pub(Bw.Y + (size_t)i * RSZ + tid, Yl[tid]);
+        if (tid < 4) st_pub(Bw.Bp + (size_t)i * 32 + 28 + tid, L.byk[tid]);
         publish_flag(back_f + i, epoch);
+        // next call's epoch: every workgroup has read this one (all helper-B flags were waited on above,
+        // and each helper B waited on its factor workgroup's panels)
+        if (tid == 0) Bw.flags[0] += 1;
         TLS(14);
-        border();
+        block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, true, Yl, L.byk, L.bybl);
         return;
     }
 #pragma unroll
@@ -1810,6 +1897,12 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         if (t < 0) continue;
         const ContribTile ct = contrib_tile(t, has_r);
         if (!ct.valid || (ct.rhs && rr >= RC)) continue;
+        if (ct.gram) {  // x^T x (5 x 5) -> Bp[i], published with this helper's flag
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                if (kk + 4 * g < 5 && rr < 5) st_pub(Bw.Bp + (size_t)i * 32 + (kk + 4 * g) * 5 + rr, cacc[q][g]);
+            continue;
+        }
         double* dst = (t < 10 ? Bw.UL : t < 20 ? Bw.UR : t < 36 ? Bw.F : t < 40 ? Bw.rL : Bw.rR) +
                       (size_t)i * (ct.rhs ? RSZ : BSZ);
 #pragma unroll
@@ -1857,6 +1950,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     L.yl[tid] = has_l ? ld_pub(Bw.Y + (size_t)(i - s_i) * RSZ + tid) : 0.0;
     L.yr[tid] = has_r ? ld_pub(Bw.Y + (size_t)(i + s_i) * RSZ + tid) : 0.0;
     L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
+    if (tid < 4) L.byk[tid] = ld_pub(Bw.Bp + (size_t)Bw.vroot * 32 + 28 + tid);  // published before the root's flag
     __syncthreads();
     if (wave < 4) {
         double al[16], ar[16];
@@ -1880,10 +1974,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     }
     __syncthreads();
     st_pub(Bw.Y + (size_t)i * RSZ + tid, L.yt[tid]);
-    border_partial(L.Bl, L.yt, L.red, i, Bw.Bp);
     publish_flag(back_f + i, epoch);
     TLS(14);
-    border();
+    block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, false, L.yt, L.byk, L.bybl);
 }
 #undef TLS
 static_assert(PANEL_DOUBLES <= BCR_BLOCK_DOUBLES, "published panels fit the block's workspace");
