@@ -1657,10 +1657,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
     for (int q = 0; q < NCT8; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
     // NH = 2: helper A stores its finished XL row block kb (sc1) during its X update of panel kb and
-    // raises xl_f = 4 epoch + kb after that panel's contributions (the drain is then nearly free);
-    // helper B loads it at the start of panel kb + 2 (rows 2, 3 after its last panel; its
-    // back-substitution needs XL) and, when the block has a right neighbour, accumulates the fill
-    // F = -XR^T XL row block by row block.
+    // raises xl_f = 4 epoch + 3 with its contributions; helper B, after publishing its own
+    // contributions, loads all of XL (its back-substitution needs it) and, when the block has a right
+    // neighbour, forms the fill F = -XR^T XL (off B's panel loop, which then keeps A's pace).
     const bool xl_on = NH == 2 && !root;
     const bool fill_on = xl_on && has_r;
     // XL of this block, 64 x 64 (stride BB), in the Dacc slot (used only by the per-level launches;
@@ -1693,12 +1692,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
         pv[2] = tid < 256 ? ld_pub(pg + BB * BB + k * 256 + tid) : 0.0;
         pv[3] = tid < 16 ? ld_pub(pg + BB * BB + 4 * 256 + 16 * k + tid) : 0.0;
-        if (xl_on && roleB && k >= 2)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int e = tid + TPB_E * u, r = 16 * (k - 2) + (e >> 6), c = e & 63;
-                pv[4 + u] = ld_pub(xlg + r * BB + c);
-            }
     };
     auto commit = [&](int k) {
 #pragma unroll
@@ -1708,19 +1701,12 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
         if (tid < 256) L.W[k][tid] = pv[2];
         if (tid < 16) L.rdiag[16 * k + tid] = pv[3];
-        if (xl_on && roleB && k >= 2)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int e = tid + TPB_E * u;
-                L.X[(16 * (k - 2) + (e >> 6)) * XW + (e & 63)] = pv[4 + u];
-            }
     };
     bool have = false;  // panel kb's loads already issued (prefetched)
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         if (!have) {
-            const bool xl_now = xl_on && roleB && kb >= 2;
-            if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok, xl_now ? xl_f + i : nullptr, 4 * epoch + kb - 2)) {
+            if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok)) {
                 if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                 return;
             }
@@ -1732,12 +1718,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         // (lane 0 of wave 7: in the two-helper layout it has no work in the X-update phase of panels 0-2,
         // so the flag loads' latency stays off the waves that compute)
         constexpr int TPOLL = 7 * 64;
-        unsigned fpan = 0, fxl = ~0u;
-        if (kb < 3 && tid == TPOLL) {
-            fpan = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (xl_on && roleB && kb + 1 >= 2)
-                fxl = __hip_atomic_load((gu32*)(xl_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        unsigned fpan = 0;
+        if (kb < 3 && tid == TPOLL) fpan = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         TLS(16 + 4 * kb);
         if (NH == 2 && wave == 4 + kb) {  // x_kb <- W_kb x_kb (LDS row block, 8 valid columns)
@@ -1785,12 +1767,10 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 for (int g = 0; g < 4; ++g) st_pub(xlg + (16 * kb + kk + 4 * g) * BB + 16 * cb + rr, w[g]);
         }
         // second flag read (its value is tested after the contributions, when the first test failed)
-        unsigned fpan2 = 0, fxl2 = ~0u;
+        unsigned fpan2 = 0;
         if (kb < 3 && tid == TPOLL) {
-            L.pre = fpan >= 4 * epoch + kb + 1 && (!(xl_on && roleB && kb + 1 >= 2) || fxl >= 4 * epoch + kb - 1);
+            L.pre = fpan >= 4 * epoch + kb + 1;
             fpan2 = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (xl_on && roleB && kb + 1 >= 2)
-                fxl2 = __hip_atomic_load((gu32*)(xl_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         TLS(17 + 4 * kb);
@@ -1813,7 +1793,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                 for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + 2 * BB + rr] = acc[g];
         }
-        if (fill_on && roleB && kb >= 2) fill_rows(kb - 2);
         if (!root) {  // contributions of row block kb: operands of every tile first, then interleaved chains
             double av[NCT8][4], bv[NCT8][4];
 #pragma unroll
@@ -1839,9 +1818,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
         const bool late = kb < 3 && !have;
         if (late && tid == TPOLL)
-            L.pre = fpan2 >= 4 * epoch + kb + 1 && (!(xl_on && roleB && kb + 1 >= 2) || fxl2 >= 4 * epoch + kb - 1);
-        if (xl_on && roleA) publish_flag(xl_f + i, 4 * epoch + kb);  // XL_kb stores (issued above) drained
-        else if (late) __syncthreads();
+            L.pre = fpan2 >= 4 * epoch + kb + 1;
+        if (late) __syncthreads();
         if (late && L.pre) {  // panel kb + 1 arrived during the contributions: no poll round trip
             issue(kb + 1);
             have = true;
@@ -1910,25 +1888,34 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             st_pub(dst + (size_t)(16 * ct.ib + kk + 4 * g) * ct.ldd + 16 * ct.cb + rr, ct.sign * cacc[q][g]);
     }
     publish_flag((roleA || NH == 1) ? elim_f + i : elimB_f + i, epoch);
+    // helper A: its final XL (stored during the X updates) is drained by the same publication
+    if (xl_on && roleA && tid == 0) __hip_atomic_store((gu32*)(xl_f + i), 4 * epoch + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     TLS(10);
     if (roleA) {
         TLS(11);
         return;
     }
     if (NH == 2) {
-        // last row block of the fill, then F = -XR^T XL; the back-substitution needs all of XL
+        // the fill F = -XR^T XL after B's contributions are out (it is needed only by the next level's
+        // helpers, before their first panel); the back-substitution needs all of XL
         if (!wait_ge(xl_f + i, 4 * epoch + 3, &L.ok)) {
             if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
-        for (int e = tid; e < 32 * BB; e += TPB_E) {
-            const int r = 32 + (e >> 6), c = e & 63;
-            L.X[r * XW + c] = ld_pub(xlg + r * BB + c);
+        {
+            double xv[BSZ / TPB_E];
+#pragma unroll
+            for (int u = 0; u < BSZ / TPB_E; ++u) xv[u] = ld_pub(xlg + tid + TPB_E * u);
+#pragma unroll
+            for (int u = 0; u < BSZ / TPB_E; ++u) {
+                const int e = tid + TPB_E * u;
+                L.X[(e >> 6) * XW + (e & 63)] = xv[u];
+            }
         }
         __syncthreads();
         if (fill_on) {
-            fill_rows(2);
-            fill_rows(3);
+#pragma unroll
+            for (int kbk = 0; kbk < 4; ++kbk) fill_rows(kbk);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const ContribTile ct = contrib_tile(20 + wave + NWE * q, true);
