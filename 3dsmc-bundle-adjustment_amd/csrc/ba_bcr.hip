@@ -1281,6 +1281,16 @@ __device__ bool wait_all_eq(const unsigned* f, int n, unsigned epoch, int* lds_o
     return *lds_ok != 0;
 }
 
+// k_bcr_split's back-substitution hand-off without flags: block i's y rows for epoch e live in
+// ybuf(e) (Y / Racc by parity); the producer stores them (agent scope) with no drain, barrier or flag,
+// and resets its slot of ybuf(e + 1) to BCR_Y_EMPTY at the start of the launch; a consumer polls the
+// 8-byte values themselves, so a hop costs one store-to-load latency instead of drain + flag + poll +
+// load. The root carries y_k in its rows 0..3, column 5 (a pad column of [u | V]).
+__device__ __forceinline__ double* ybuf(const BcrWork& Bw, unsigned epoch) { return (epoch & 1) ? Bw.Racc : Bw.Y; }
+__device__ __forceinline__ unsigned long long ld_u64(const double* p) {
+    return __hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 static constexpr int NCT8 = (NCONTRIB + NWE - 1) / NWE;  // contribution tiles per wave (all 8 waves)
 __device__ __forceinline__ void contrib_accumulate8(const double* X, int kbk, d4b (&cacc)[NCT8], bool has_r, int wave,
                                                     int rr, int kk) {
@@ -1375,7 +1385,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const int b0 = i * G_DOF;
     const unsigned epoch = Bw.flags[0] + 1;
     unsigned* elim_f = Bw.flags + 16;              // NH = 1: all contributions; NH = 2: helper A's (UL, rL)
-    unsigned* back_f = Bw.flags + 16 + nblk;
     unsigned* panel_f = Bw.flags + 16 + 2 * nblk;
     unsigned* elimB_f = NH == 2 ? Bw.flags + 16 + 3 * nblk : elim_f;  // helper B's (UR, rR)
     unsigned* fill_f = NH == 2 ? Bw.flags + 16 + 4 * nblk : elim_f;   // F of block i
@@ -1547,6 +1556,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // forward-solved x = [b_a | B] with its contributions; the root sums them with its own, solves the
     // 4x4 border system before its back-substitution and publishes y_k with y_root, so each block
     // applies its camera step right after its own back-substitution (no wait for every block).
+    if (roleB)  // this block's slot of the next epoch's y buffer starts empty
+        reinterpret_cast<unsigned long long*>(ybuf(Bw, epoch + 1))[(size_t)i * RSZ + tid] = BCR_Y_EMPTY;
     if (root && tid < 14) {  // border inputs [b_k | S_kk packed]
         int q = tid - 4, mm = 0;
         while (q > mm) { q -= mm + 1; ++mm; }
@@ -1859,9 +1870,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             if (bad) raise_flag(flag, FLAG_NOT_PD);
         }
         trsm_t_lanes(L.L, L.rdiag, Yl);  // ends with a barrier
-        st_pub(Bw.Y + (size_t)i * RSZ + tid, Yl[tid]);
-        if (tid < 4) st_pub(Bw.Bp + (size_t)i * 32 + 28 + tid, L.byk[tid]);
-        publish_flag(back_f + i, epoch);
+        st_pub(ybuf(Bw, epoch) + (size_t)i * RSZ + tid, ((tid & 7) == 5 && tid < 4 * RC) ? L.byk[tid >> 3] : Yl[tid]);
         // next call's epoch: every workgroup has read this one (all helper-B flags were waited on above,
         // and each helper B waited on its factor workgroup's panels)
         if (tid == 0) Bw.flags[0] += 1;
@@ -1929,16 +1938,32 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     }
     // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
     trsm_lower64_t(L.L, L.rdiag, L.X, XW, XC);
-    if (!wait_flags(has_l ? back_f + (i - s_i) : nullptr, has_r ? back_f + (i + s_i) : nullptr, epoch, &L.ok)) {
-        if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-        return;
+    {
+        // the neighbours' y rows and y_k, polled value by value (bounded)
+        const double* Yb = ybuf(Bw, epoch);
+        const double* pl = Yb + (size_t)(i - s_i) * RSZ + tid;
+        const double* pr = Yb + (size_t)(i + s_i) * RSZ + tid;
+        const double* pk = Yb + (size_t)Bw.vroot * RSZ + tid * RC + 5;
+        unsigned long long ul = has_l ? ld_u64(pl) : 0ull, ur = has_r ? ld_u64(pr) : 0ull, uk = tid < 4 ? ld_u64(pk) : 0ull;
+        int okp = 1;
+        unsigned n = 0;
+        while (ul == BCR_Y_EMPTY || ur == BCR_Y_EMPTY || uk == BCR_Y_EMPTY) {
+            __builtin_amdgcn_s_sleep(1);
+            if (ul == BCR_Y_EMPTY) ul = ld_u64(pl);
+            if (ur == BCR_Y_EMPTY) ur = ld_u64(pr);
+            if (uk == BCR_Y_EMPTY) uk = ld_u64(pk);
+            if (++n > SPIN_LIMIT) { okp = 0; break; }
+        }
+        L.yl[tid] = __longlong_as_double((long long)ul);
+        L.yr[tid] = __longlong_as_double((long long)ur);
+        if (tid < 4) L.byk[tid] = __longlong_as_double((long long)uk);
+        L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
+        if (!__syncthreads_and(okp)) {
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
+            return;
+        }
     }
     TLS(12);
-    L.yl[tid] = has_l ? ld_pub(Bw.Y + (size_t)(i - s_i) * RSZ + tid) : 0.0;
-    L.yr[tid] = has_r ? ld_pub(Bw.Y + (size_t)(i + s_i) * RSZ + tid) : 0.0;
-    L.yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
-    if (tid < 4) L.byk[tid] = ld_pub(Bw.Bp + (size_t)Bw.vroot * 32 + 28 + tid);  // published before the root's flag
-    __syncthreads();
     if (wave < 4) {
         double al[16], ar[16];
 #pragma unroll
@@ -1960,8 +1985,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             for (int g = 0; g < 4; ++g) L.yt[(16 * wave + kk + 4 * g) * RC + rr] -= acc0[g] + acc1[g];
     }
     __syncthreads();
-    st_pub(Bw.Y + (size_t)i * RSZ + tid, L.yt[tid]);
-    publish_flag(back_f + i, epoch);
+    st_pub(ybuf(Bw, epoch) + (size_t)i * RSZ + tid, L.yt[tid]);
     TLS(14);
     block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, false, L.yt, L.byk, L.bybl);
 }

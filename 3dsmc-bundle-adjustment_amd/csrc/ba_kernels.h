@@ -128,6 +128,11 @@ struct BcrWork {
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level
 };
+// k_bcr_split's flag-free back-substitution hand-off: y rows double-buffered by epoch parity (Y even,
+// Racc odd — Racc belongs to the per-level path only); an empty slot holds this signalling-NaN pattern,
+// which no f64 operation produces (they return quiet NaNs).
+static constexpr unsigned BCR_Y_EMPTY_D32 = 0xFFF7A5A5u;
+static constexpr unsigned long long BCR_Y_EMPTY = 0xFFF7A5A5FFF7A5A5ull;
 // [XL | XR | x] row stride (136 columns; padding to 144 for conflict-free operand rows measured no gain)
 static constexpr int BCR_XW = 136;
 static constexpr size_t BCR_BLOCK_DOUBLES = (size_t)5 * 64 * 64 + 64 * BCR_XW + 4 * 64 * 8 + 32 + 64;

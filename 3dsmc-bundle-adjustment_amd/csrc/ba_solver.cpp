@@ -854,6 +854,8 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
         Bw.bk = Bw.rd + (size_t)64 * bcr_nblk;
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
+        // k_bcr_split's y hand-off buffers (Racc | Y, epoch parity) start empty (BCR_Y_EMPTY)
+        HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Racc, BCR_Y_EMPTY_D32, 4 * b8, ctx->stream));
         Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;

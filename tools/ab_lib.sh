@@ -1,10 +1,10 @@
 # Same-box A/B of two libmiba builds (abl/libmiba_<name>.so) on C4: bench value + per-kernel ms,
-# alternating builds to cancel clock drift. usage: bash tools/ab_lib.sh old new [rounds] [config]
+# alternating builds to cancel clock drift. usage: bash tools/ab_lib.sh "old new ..." [rounds] [config]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-rounds=${3:-3}; cfg=${4:-C4}
+rounds=${2:-3}; cfg=${3:-C4}
 for r in $(seq 1 $rounds); do
-  for name in $1 $2; do
+  for name in $1; do
     MIBA_LIB_PATH=$PWD/abl/libmiba_$name.so timeout -k 10 200 python bench.py --no-cpu-baseline --config $cfg > gpurun_out/ab_${name}_$r.log 2>&1 || { echo "FAIL $name"; tail -5 gpurun_out/ab_${name}_$r.log; exit 1; }
     python - "$name" "$r" <<'PY'
 import json,sys
