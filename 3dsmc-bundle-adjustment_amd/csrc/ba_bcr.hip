@@ -1964,28 +1964,45 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
     }
     TLS(12);
-    if (wave < 4) {
-        double al[16], ar[16];
+    {
+        // y_i = u - P y_l - Q y_r on all 8 waves: wave w owns row block w & 3 and half (w >> 2) of the
+        // 64-deep contraction (two 8-deep MFMA chains, operands loaded up front); the second half's
+        // partials meet the first's in LDS, and the first-half waves store the finished rows straight
+        // from registers (the next hop's consumers poll them)
+        const int rb = wave & 3, kh = wave >> 2;
+        double al[8], ar[8], bl[8], br[8];
 #pragma unroll
-        for (int s4 = 0; s4 < 16; ++s4) {
-            const double* row = L.X + (16 * wave + rr) * XW + 4 * s4 + kk;
-            al[s4] = row[0];
+        for (int s4 = 0; s4 < 8; ++s4) {
+            const int k = 8 * kh + s4;
+            const double* row = L.X + (16 * rb + rr) * XW + 4 * k + kk;
+            al[s4] = has_l ? row[0] : 0.0;
             ar[s4] = has_r ? row[BB] : 0.0;
+            bl[s4] = has_l && rr < RC ? L.yl[(4 * k + kk) * RC + rr] : 0.0;
+            br[s4] = has_r && rr < RC ? L.yr[(4 * k + kk) * RC + rr] : 0.0;
         }
         d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int s4 = 0; s4 < 16; ++s4) {
-            const double bl = rr < RC ? L.yl[(4 * s4 + kk) * RC + rr] : 0.0;
-            const double br = rr < RC ? L.yr[(4 * s4 + kk) * RC + rr] : 0.0;
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bl, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s4], br, acc1, 0, 0, 0);
+        for (int s4 = 0; s4 < 8; ++s4) {
+            if (has_l) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bl[s4], acc0, 0, 0, 0);
+            if (has_r) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s4], br[s4], acc1, 0, 0, 0);
         }
-        if (rr < RC)
+        double* part2 = L.bpl;  // 64 x RC partials of the second half
+        if (kh == 1 && rr < RC)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) L.yt[(16 * wave + kk + 4 * g) * RC + rr] -= acc0[g] + acc1[g];
+            for (int g = 0; g < 4; ++g) part2[(16 * rb + kk + 4 * g) * RC + rr] = acc0[g] + acc1[g];
+        __syncthreads();
+        if (kh == 0 && rr < RC) {
+            double* yout = ybuf(Bw, epoch) + (size_t)i * RSZ;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int e = (16 * rb + kk + 4 * g) * RC + rr;
+                const double v = L.yt[e] - ((acc0[g] + acc1[g]) + part2[e]);
+                st_pub(yout + e, v);
+                L.yt[e] = v;
+            }
+        }
     }
     __syncthreads();
-    st_pub(ybuf(Bw, epoch) + (size_t)i * RSZ + tid, L.yt[tid]);
     TLS(14);
     block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, false, L.yt, L.byk, L.bybl);
 }
