@@ -10,7 +10,7 @@ for r in $(seq 1 $rounds); do
 import json,sys
 d=json.loads(open(f'gpurun_out/ab_{sys.argv[1]}_{sys.argv[2]}.log').read().strip().splitlines()[-1])
 k=d.get('kernel_ms_per_step') or {}
-print(f"{sys.argv[1]:8s} {d['value']:9.1f} {d['ms_per_step']*1e3:7.1f} us/it bcr_avg={d['roofline']['avg_launch_ms']*1e3:.1f} |", " ".join(f"{n}={v*1e3:.1f}" for n,v in k.items()))
+print(f"{sys.argv[1]:8s} {d['value']:9.1f} {d['ms_per_step']*1e3:7.1f} us/it bcr_avg={d.get('roofline',{}).get('avg_launch_ms',0)*1e3:.1f} |", " ".join(f"{n}={v*1e3:.1f}" for n,v in k.items()))
 PY
   done
 done
