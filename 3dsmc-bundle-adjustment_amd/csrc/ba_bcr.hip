@@ -1290,6 +1290,10 @@ __device__ __forceinline__ double* ybuf(const BcrWork& Bw, unsigned epoch) { ret
 __device__ __forceinline__ unsigned long long ld_u64(const double* p) {
     return __hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The same protocol carries the factor workgroup's published panels to its helpers (Cf | X slots, two
+// epochs) and, with two helpers, helper B's fill F to the next level's helpers (F / F2 by parity).
+__device__ __forceinline__ double* fbuf(const BcrWork& Bw, unsigned epoch) { return (epoch & 1) ? Bw.F2 : Bw.F; }
+__device__ __forceinline__ bool lower_tile(int e) { return ((e & 63) >> 4) <= ((e >> 6) >> 4); }
 
 static constexpr int NCT8 = (NCONTRIB + NWE - 1) / NWE;  // contribution tiles per wave (all 8 waves)
 __device__ __forceinline__ void contrib_accumulate8(const double* X, int kbk, d4b (&cacc)[NCT8], bool has_r, int wave,
@@ -1385,13 +1389,14 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const int b0 = i * G_DOF;
     const unsigned epoch = Bw.flags[0] + 1;
     unsigned* elim_f = Bw.flags + 16;              // NH = 1: all contributions; NH = 2: helper A's (UL, rL)
-    unsigned* panel_f = Bw.flags + 16 + 2 * nblk;
     unsigned* elimB_f = NH == 2 ? Bw.flags + 16 + 3 * nblk : elim_f;  // helper B's (UR, rR)
     unsigned* fill_f = NH == 2 ? Bw.flags + 16 + 4 * nblk : elim_f;   // F of block i
     unsigned* xl_f = Bw.flags + 16 + 5 * nblk;                         // NH = 2: final XL of block i
     unsigned* ul_f = elim_f;   // producers of UL / rL
     unsigned* ur_f = elimB_f;  // producers of UR / rR
-    double* pg = Bw.Cf + (size_t)i * PANEL_DOUBLES;  // this block's published panels
+    // this block's published panels, by epoch parity (flag-free: F stores, the helpers poll the values)
+    double* pg = Bw.Cf + ((epoch & 1) ? (size_t)nblk * PANEL_DOUBLES : 0) + (size_t)i * PANEL_DOUBLES;
+    double* pg_next = Bw.Cf + ((epoch & 1) ? 0 : (size_t)nblk * PANEL_DOUBLES) + (size_t)i * PANEL_DOUBLES;
     constexpr int NQ = BSZ / TPB_E;
     const int s_i = 1 << mi;
     const bool has_r = !root && i + s_i < nblk;
@@ -1406,6 +1411,15 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             L.T[r * BLD + c] = ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0);
         }
         if (tid < 12) L.sync[tid] = 0;
+        {  // the next epoch's panel slot starts empty (the entries a panel writes: lower tiles, W, 1/diag)
+            unsigned long long* nx = reinterpret_cast<unsigned long long*>(pg_next);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                if (lower_tile(tid + TPB_E * q)) nx[tid + TPB_E * q] = BCR_Y_EMPTY;
+            nx[BB * BB + tid] = BCR_Y_EMPTY;
+            nx[BB * BB + TPB_E + tid] = BCR_Y_EMPTY;
+            if (tid < BB) nx[BB * BB + 4 * 256 + tid] = BCR_Y_EMPTY;
+        }
         for (int m = 0; m < mi; ++m) {
             const int s = 1 << m, a = i - s, b = i + s;
             if (!wait_flags(a >= 0 ? ur_f + a : nullptr, b < nblk ? ul_f + b : nullptr, epoch, &L.ok)) {
@@ -1537,11 +1551,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                 for (int u = 0; u < 4; ++u) st_pub(pg + BB * BB + kb * 256 + lane + 64 * u, L.Wb[lane + 64 * u]);
                 if (lane < 16) st_pub(pg + BB * BB + 4 * 256 + 16 * kb + lane, L.rdiag[16 * kb + lane]);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) {
-                    __hip_atomic_store((gu32*)(panel_f + i), 4 * epoch + kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if constexpr (STAMP) tl[32 * blockIdx.x + 2 + kb] = realtime_now();
-                }
+                if constexpr (STAMP) if (lane == 0) tl[32 * blockIdx.x + 2 + kb] = realtime_now();
             }
         }
         if (!ok) raise_flag(flag, FLAG_TIMEOUT);
@@ -1558,6 +1568,11 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // applies its camera step right after its own back-substitution (no wait for every block).
     if (roleB)  // this block's slot of the next epoch's y buffer starts empty
         reinterpret_cast<unsigned long long*>(ybuf(Bw, epoch + 1))[(size_t)i * RSZ + tid] = BCR_Y_EMPTY;
+    if (NH == 2 && roleB && !root) {  // ... and so does its fill slot
+        unsigned long long* nf = reinterpret_cast<unsigned long long*>(fbuf(Bw, epoch + 1)) + (size_t)i * BSZ;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) nf[tid + TPB_E * q] = BCR_Y_EMPTY;
+    }
     if (root && tid < 14) {  // border inputs [b_k | S_kk packed]
         int q = tid - 4, mm = 0;
         while (q > mm) { q -= mm + 1; ++mm; }
@@ -1596,13 +1611,36 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             return;
         }
         if (last && NH == 2) {
-            const unsigned* ff = roleA ? (a >= 0 ? fill_f + a : nullptr) : (has_r ? fill_f + b : nullptr);
-            if (!wait_flags(ff, nullptr, epoch, &L.ok)) {
+            // the fill of the neighbour this helper's side faces, polled value by value
+            const bool on = roleA ? a >= 0 : has_r;
+            const double* pf = fbuf(Bw, epoch) + (size_t)(on ? (roleA ? a : b) : 0) * BSZ;
+            unsigned long long fv[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) fv[q] = on ? ld_u64(pf + tid + TPB_E * q) : 0ull;
+            int okp = 1;
+            for (unsigned n = 0;; ++n) {
+                bool pend = false;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) pend = pend || fv[q] == BCR_Y_EMPTY;
+                if (!pend) break;
+                if (n > SPIN_LIMIT) { okp = 0; break; }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    if (fv[q] == BCR_Y_EMPTY) fv[q] = ld_u64(pf + tid + TPB_E * q);
+            }
+            if (!__syncthreads_and(okp)) {
                 if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                 return;
             }
-        }
-        if (last) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+                const double v = __longlong_as_double((long long)fv[q]);
+                if (roleA) L.X[r * XW + c] = v;
+                else L.X[c * XW + BB + r] = v;
+            }
+        } else if (last) {
             double fl[NQ], fr[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -1693,45 +1731,52 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // runs behind the factor workgroup, the flags of panel kb + 1 are already set by the end of the
     // X update of panel kb: its loads are then issued before the contributions of panel kb, which
     // hide their latency (one poll round trip + one load round trip per panel otherwise).
-    double pv[6];
+    unsigned long long pv[4];
+    auto paddr = [&](int k, int u) -> const double* {  // this thread's value u of panel k (nullptr: none)
+        if (u < 2) {
+            const int e = tid + TPB_E * u;
+            return e < (4 - k) * 256 ? pg + (16 * k + (e >> 4)) * BB + 16 * k + (e & 15) : nullptr;
+        }
+        if (u == 2) return tid < 256 ? pg + BB * BB + k * 256 + tid : nullptr;
+        return tid < 16 ? pg + BB * BB + 4 * 256 + 16 * k + tid : nullptr;
+    };
     auto issue = [&](int k) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + TPB_E * u;
-            const int r = 16 * k + (e >> 4), c = 16 * k + (e & 15);
-            pv[u] = e < (4 - k) * 256 ? ld_pub(pg + r * BB + c) : 0.0;
+        for (int u = 0; u < 4; ++u) {
+            const double* a = paddr(k, u);
+            pv[u] = a ? ld_u64(a) : 0ull;
         }
-        pv[2] = tid < 256 ? ld_pub(pg + BB * BB + k * 256 + tid) : 0.0;
-        pv[3] = tid < 16 ? ld_pub(pg + BB * BB + 4 * 256 + 16 * k + tid) : 0.0;
     };
-    auto commit = [&](int k) {
+    auto commit = [&](int k) -> int {  // polls the values still empty, then stores them to LDS
+        int ok = 1;
+        for (unsigned n = 0;; ++n) {
+            bool pend = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pend = pend || pv[u] == BCR_Y_EMPTY;
+            if (!pend) break;
+            if (n > SPIN_LIMIT) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (pv[u] == BCR_Y_EMPTY) pv[u] = ld_u64(paddr(k, u));
+        }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + TPB_E * u;
-            if (e < (4 - k) * 256) L.L[(16 * k + (e >> 4)) * BLD + 16 * k + (e & 15)] = pv[u];
+            if (e < (4 - k) * 256) L.L[(16 * k + (e >> 4)) * BLD + 16 * k + (e & 15)] = __longlong_as_double((long long)pv[u]);
         }
-        if (tid < 256) L.W[k][tid] = pv[2];
-        if (tid < 16) L.rdiag[16 * k + tid] = pv[3];
+        if (tid < 256) L.W[k][tid] = __longlong_as_double((long long)pv[2]);
+        if (tid < 16) L.rdiag[16 * k + tid] = __longlong_as_double((long long)pv[3]);
+        return ok;
     };
-    bool have = false;  // panel kb's loads already issued (prefetched)
+    issue(0);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-        if (!have) {
-            if (!wait_ge(panel_f + i, 4 * epoch + kb, &L.ok)) {
-                if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-                return;
-            }
-            issue(kb);
-        }
         TLS(2 + 2 * kb);
-        commit(kb);
-        // early flag reads for the prefetch test (consumed after the X update)
-        // (lane 0 of wave 7: in the two-helper layout it has no work in the X-update phase of panels 0-2,
-        // so the flag loads' latency stays off the waves that compute)
-        constexpr int TPOLL = 7 * 64;
-        unsigned fpan = 0;
-        if (kb < 3 && tid == TPOLL) fpan = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
+        if (!__syncthreads_and(commit(kb))) {
+            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
+            return;
+        }
         TLS(16 + 4 * kb);
         if (NH == 2 && wave == 4 + kb) {  // x_kb <- W_kb x_kb (LDS row block, 8 valid columns)
             double aw[4], bx[4];
@@ -1777,16 +1822,10 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                 for (int g = 0; g < 4; ++g) st_pub(xlg + (16 * kb + kk + 4 * g) * BB + 16 * cb + rr, w[g]);
         }
-        // second flag read (its value is tested after the contributions, when the first test failed)
-        unsigned fpan2 = 0;
-        if (kb < 3 && tid == TPOLL) {
-            L.pre = fpan >= 4 * epoch + kb + 1;
-            fpan2 = __hip_atomic_load((gu32*)(panel_f + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         __syncthreads();
         TLS(17 + 4 * kb);
-        have = kb < 3 && L.pre;
-        if (have) issue(kb + 1);
+        // next panel's loads in flight under the contributions (values still empty are polled at its commit)
+        if (kb < 3) issue(kb + 1);
         if (NH == 2 && wave > 4 + kb) {  // x_ii -= L(ii,kb) x_kb, ii = wave - 4
             const int ii = wave - 4;
             double al[4], bx[4];
@@ -1826,14 +1865,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 for (int q = 0; q < NCT8; ++q)
                     if (hm.tiles[q] >= 0)
                         cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][s4], bv[q][s4], cacc[q], 0, 0, 0);
-        }
-        const bool late = kb < 3 && !have;
-        if (late && tid == TPOLL)
-            L.pre = fpan2 >= 4 * epoch + kb + 1;
-        if (late) __syncthreads();
-        if (late && L.pre) {  // panel kb + 1 arrived during the contributions: no poll round trip
-            issue(kb + 1);
-            have = true;
         }
         if constexpr (STAMP) __syncthreads();
         TLS(3 + 2 * kb);
@@ -1930,7 +1961,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 const ContribTile ct = contrib_tile(20 + wave + NWE * q, true);
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
-                    st_pub(Bw.F + (size_t)i * BSZ + (size_t)(16 * ct.ib + kk + 4 * g) * BB + 16 * ct.cb + rr, -facc[q][g]);
+                    st_pub(fbuf(Bw, epoch) + (size_t)i * BSZ + (size_t)(16 * ct.ib + kk + 4 * g) * BB + 16 * ct.cb + rr, -facc[q][g]);
             }
         }
         publish_flag(fill_f + i, epoch);
@@ -2008,6 +2039,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 }
 #undef TLS
 static_assert(PANEL_DOUBLES <= BCR_BLOCK_DOUBLES, "published panels fit the block's workspace");
+static_assert(2 * PANEL_DOUBLES <= BB * BB + BB * XW, "two epochs' panels fit the Cf | X slots");
 
 #define CKB(x)                            \
     do {                                  \

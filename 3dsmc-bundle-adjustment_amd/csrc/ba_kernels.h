@@ -117,6 +117,7 @@ static constexpr int BCR_CAMS = 10;
 // plus one global slot: bk = [b_k (4) | S_kk lower (10)].
 struct BcrWork {
     double *Cf, *X, *UL, *UR, *F, *rL, *rR, *Dacc, *Racc, *Y, *Bp, *rd, *bk;
+    double* F2;  // k_bcr_split (two helpers): the fill F of odd epochs (flag-free hand-off)
     // persistent path: flags[0] = call epoch, flags[16 + i] = block i eliminated (helper A's part
     // when split 3-way), flags[16 + nblk + i] = block i back-substituted, [16 + 2 nblk + i] panels
     // published, [16 + 3 nblk + i] helper B's part, [16 + 4 nblk + i] fill F, [16 + 5 nblk + i] XL

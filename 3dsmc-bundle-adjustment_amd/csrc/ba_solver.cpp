@@ -824,7 +824,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         }
     }
     if (P.solver == 2) {
-        const size_t bytes = sizeof(double) * (BCR_BLOCK_DOUBLES * bcr_nblk + 16) + sizeof(unsigned) * (16 + 6 * bcr_nblk);
+        const size_t bytes = sizeof(double) * ((BCR_BLOCK_DOUBLES + 64 * 64) * bcr_nblk + 16) + sizeof(unsigned) * (16 + 6 * bcr_nblk);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
         // upper tiles of UL/UR are never written and must read as zero
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
@@ -852,10 +852,15 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         Bw.Y = Bw.Racc + b8;
         Bw.Bp = Bw.Y + b8;
         Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
-        Bw.bk = Bw.rd + (size_t)64 * bcr_nblk;
+        Bw.F2 = Bw.rd + (size_t)64 * bcr_nblk;
+        Bw.bk = Bw.F2 + b64;
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
-        // k_bcr_split's y hand-off buffers (Racc | Y, epoch parity) start empty (BCR_Y_EMPTY)
+        // k_bcr_split's flag-free hand-off buffers start empty (BCR_Y_EMPTY): y (Racc | Y, epoch parity),
+        // the published panels (Cf | X slots, two epochs) and the odd epochs' fill
         HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Racc, BCR_Y_EMPTY_D32, 4 * b8, ctx->stream));
+        HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Cf, BCR_Y_EMPTY_D32, 2 * (b64 + (size_t)64 * BCR_XW * bcr_nblk),
+                                        ctx->stream));
+        HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.F2, BCR_Y_EMPTY_D32, 2 * b64, ctx->stream));
         Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
