@@ -1727,10 +1727,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             }
         }
     };
-    // Panel data of panel kb (and helper B's XL_{kb-2} rows) -> registers, then LDS. When the helper
-    // runs behind the factor workgroup, the flags of panel kb + 1 are already set by the end of the
-    // X update of panel kb: its loads are then issued before the contributions of panel kb, which
-    // hide their latency (one poll round trip + one load round trip per panel otherwise).
+    // Panel data of panel kb -> registers, then LDS. The loads of panel kb + 1 are issued right after
+    // the X update of panel kb, so their latency hides under the contributions; values that were still
+    // empty (the factor workgroup had not stored them yet) are polled again at the panel's commit.
     unsigned long long pv[4];
     auto paddr = [&](int k, int u) -> const double* {  // this thread's value u of panel k (nullptr: none)
         if (u < 2) {
