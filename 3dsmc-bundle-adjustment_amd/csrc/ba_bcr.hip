@@ -985,19 +985,20 @@ __device__ __forceinline__ void publish_flag(unsigned* f, unsigned epoch) {
 // polls before a hand-off wait gives up (bcr_set_spin_limit; tests force a tiny bound)
 __device__ unsigned g_spin_limit = 1u << 22;
 #define SPIN_LIMIT g_spin_limit
-// ONE lane polls fa then fb (either may be null); uniform result, false on timeout.
+// ONE lane polls fa and fb together (either may be null: both loads in flight per round trip, so two
+// flags that are already set cost one round trip, not two); uniform result, false on timeout.
 __device__ bool wait_flags(const unsigned* fa, const unsigned* fb, unsigned epoch, int* lds_ok) {
     if (threadIdx.x == 0) {
         int ok = 1;
-        const unsigned* fs[2] = {fa, fb};
-        for (int k = 0; k < 2 && ok; ++k) {
-            if (!fs[k]) continue;
-            unsigned n = 0;
-            while (__hip_atomic_load((gu32*)const_cast<unsigned*>(fs[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                   epoch) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++n > SPIN_LIMIT) { ok = 0; break; }
-            }
+        unsigned n = 0;
+        for (;;) {
+            const unsigned va =
+                fa ? __hip_atomic_load((gu32*)const_cast<unsigned*>(fa), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : epoch;
+            const unsigned vb =
+                fb ? __hip_atomic_load((gu32*)const_cast<unsigned*>(fb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : epoch;
+            if (va == epoch && vb == epoch) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (++n > SPIN_LIMIT) { ok = 0; break; }
         }
         *lds_ok = ok;
     }
@@ -1247,9 +1248,11 @@ __device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok, const u
     if (threadIdx.x == 0) {
         int ok = 1;
         unsigned n = 0;
-        while (__hip_atomic_load((gu32*)const_cast<unsigned*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target ||
-               (f2 && __hip_atomic_load((gu32*)const_cast<unsigned*>(f2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                          target2)) {
+        for (;;) {  // both loads in flight per round trip
+            const unsigned v = __hip_atomic_load((gu32*)const_cast<unsigned*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned v2 =
+                f2 ? __hip_atomic_load((gu32*)const_cast<unsigned*>(f2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target2;
+            if (v >= target && v2 >= target2) break;
             __builtin_amdgcn_s_sleep(2);
             if (++n > SPIN_LIMIT) { ok = 0; break; }
         }
