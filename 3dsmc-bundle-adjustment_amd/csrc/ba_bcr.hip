@@ -1904,9 +1904,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
         trsm_t_lanes(L.L, L.rdiag, Yl);  // ends with a barrier
         st_pub(ybuf(Bw, epoch) + (size_t)i * RSZ + tid, ((tid & 7) == 5 && tid < 4 * RC) ? L.byk[tid >> 3] : Yl[tid]);
-        // next call's epoch: every workgroup has read this one (all helper-B flags were waited on above,
-        // and each helper B waited on its factor workgroup's panels)
-        if (tid == 0) Bw.flags[0] += 1;
+        // (the next call's epoch is advanced by k_final, after every workgroup of this launch has exited)
         TLS(14);
         block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, true, Yl, L.byk, L.bybl);
         return;
@@ -2063,19 +2061,64 @@ static inline int n_elim(int nblk, int m) {
         CKB(hipGetLastError());           \
     } while (0)
 
+// k_bcr_split as a cooperative launch: its workgroups wait on each other, so the grid must be co-resident,
+// and a cooperative launch refuses a grid that cannot be (hipErrorCooperativeLaunchTooLarge) instead of
+// letting it run into the hand-off timeouts. MIBA_BCR_COOP=0: an ordinary launch (same kernel).
+static bool bcr_coop() {
+    static const int on = [] {
+        const char* e = getenv("MIBA_BCR_COOP");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return on != 0;
+}
+template <bool STAMP, int NH>
+static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
+                               unsigned long long* stamps, Prof* pf) {
+    const dim3 grid((NH + 1) * Bw.nblk), block(TPB_E);
+    if (!bcr_coop()) {
+        BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw, W.chol_flag,
+            stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
+        return hipSuccess;
+    }
+    const LmState* a_st = W.st;
+    DevProblem a_P = P;
+    const double* a_S = W.S;
+    double* a_rhs = W.rhs;
+    BcrWork a_Bw = Bw;
+    int* a_flag = W.chol_flag;
+    unsigned long long* a_tl = stamps;
+    BaConsts a_c = c;
+    const double* a_scale = W.scale;
+    const double* a_camdata = W.camdata;
+    const double* a_lin = W.lin;
+    double* a_delta = W.delta;
+    double* a_part = W.part;
+    void* args[] = {&a_st, &a_P, &a_S, &a_rhs, &a_Bw, &a_flag, &a_tl, &a_c, &a_scale, &a_camdata, &a_lin, &a_delta, &a_part};
+    if (pf) pf->begin(K_BCR_PERSIST, s);
+    const hipError_t e = hipLaunchCooperativeKernel((const void*)k_bcr_split<STAMP, NH>, grid, block, args, sizeof(HLds), s);
+    if (pf) pf->end(s);
+    return e;
+}
+
 template <bool STAMP>
-static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
+static hipError_t launch_per_level(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
+                                   unsigned long long* stamps, Prof* pf);
+
+template <bool STAMP>
+static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
     if (Bw.persist >= 2) {
         // the border solve and the camera step run inside the split kernel (no k_bcr_border launch)
-        if (Bw.persist == 3)
-            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 2>), dim3(3 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
-                Bw, W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
-        else
-            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, 1>), dim3(2 * nblk), dim3(TPB_E), sizeof(HLds), s, W.st, P, W.S, W.rhs,
-                Bw, W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
-        return hipSuccess;
+        const hipError_t e = Bw.persist == 3 ? launch_split<STAMP, 2>(P, c, W, Bw, s, stamps, pf)
+                                             : launch_split<STAMP, 1>(P, c, W, Bw, s, stamps, pf);
+        if (e == hipSuccess) return hipSuccess;
+        (void)hipGetLastError();  // the refused launch's error is not sticky: clear it
+        if (e != hipErrorCooperativeLaunchTooLarge) return e;
+        // the grid cannot be co-resident on this device: this context uses the per-level launches
+        // (the k_final of this iteration sees persist == 0 and advances no epoch)
+        Bw.persist = 0;
+        return launch_per_level<STAMP>(P, c, W, Bw, s, stamps, pf);
     }
     if (Bw.persist) {
         BPL(K_BCR_PERSIST, k_bcr_persist<STAMP>, dim3(nblk), dim3(TPB_E), sizeof(PersistLds), s, W.st, P, W.S, W.rhs,
@@ -2084,6 +2127,14 @@ static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& 
             W.camdata, W.lin, W.delta, W.part);
         return hipSuccess;
     }
+    return launch_per_level<STAMP>(P, c, W, Bw, s, stamps, pf);
+}
+
+// the reference arithmetic: one launch per level (no inter-workgroup waits)
+template <bool STAMP>
+static hipError_t launch_per_level(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
+                                   unsigned long long* stamps, Prof* pf) {
+    const int nblk = Bw.nblk;
     for (int m = 0; m < Bw.levels; ++m) {
         const int nel = n_elim(nblk, m);
         const int nacc = m >= 1 ? (nblk + (2 << m) - 1) / (2 << m) : 0;
@@ -2142,7 +2193,7 @@ int bcr_persist_ok(int nblk) {
     return per_cu >= 1 && nblk <= per_cu * ncu ? 1 : 0;
 }
 
-hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf) {
+hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s, Prof* pf) {
     static bool attr = false;
     static unsigned long long* stamps = nullptr;
     if (!attr) {

@@ -1,7 +1,6 @@
 // ba_common.h — device-side helpers shared by the libmiba kernel translation units
-// (ba_kernels.hip: the multi-launch LM iteration; ba_small.hip: the single-workgroup solve of
-// small windows): reductions, the per-point Schur algebra, the in-register 16x16 Cholesky and the
-// Ceres 2.0 trust-region decision.
+// (ba_kernels.hip: the LM iteration; ba_bcr.hip: the reduced camera solve): reductions, the per-point
+// Schur algebra, the in-register 16x16 Cholesky and the Ceres 2.0 trust-region decision.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -319,14 +318,15 @@ __device__ __forceinline__ void lm_decide_local(LmState& S, const LmParams& prm,
         S.done = 1; S.termination = 0; S.msg = MSG_MIN_RADIUS; S.msg_a = S.radius; S.msg_b = prm.min_radius;
     }
     if (S.done) return;
-    S.iter += 1;
-    double* lg = log + S.iter * LOG_W;
-    if (scal[SC_BAD] >= SC_BAD_TIMEOUT) {  // a BCR hand-off timed out: no valid step; end the solve loudly
-        S.n_unsucc += 1;
-        S.done = 1; S.termination = 2; S.msg = MSG_TIMEOUT;
-        lg[0] = S.x_cost; lg[1] = 0.0; lg[3] = 0.0; lg[4] = 0.0; lg[5] = S.radius; lg[6] = 0.0;
+    if (scal[SC_BAD] >= SC_BAD_TIMEOUT) {
+        // a BCR hand-off timed out (the resident workgroups were not co-resident): this iteration computed no
+        // step. Stop the device loop WITHOUT a termination (termination -1, the iteration not counted, x /
+        // radius untouched): the host re-runs it with the per-level BCR launches and resumes the solve.
+        S.done = 1; S.termination = -1; S.msg = MSG_TIMEOUT;
         return;
     }
+    S.iter += 1;
+    double* lg = log + S.iter * LOG_W;
     const double mcc = scal[SC_MCC];
     const bool lsf = scal[SC_BAD] >= 2.0;  // linear solver failure (point block or Cholesky not PD)
     const bool valid = !lsf && isfinite(mcc) && mcc > 0.0;

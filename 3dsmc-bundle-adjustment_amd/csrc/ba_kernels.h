@@ -122,7 +122,7 @@ struct BcrWork {
     // when split 3-way), flags[16 + nblk + i] = block i back-substituted, [16 + 2 nblk + i] panels
     // published, [16 + 3 nblk + i] helper B's part, [16 + 4 nblk + i] fill F, [16 + 5 nblk + i] XL
     // (each holds the epoch that set it; panels 4 * epoch + panel)
-    unsigned* flags;
+    unsigned* flags;  // flags[0] (the epoch) is advanced by k_final after every BCR launch that ran
     int nblk, levels;
     int voff, vroot, vlevels;  // k_bcr_split: balanced tree on v = i + voff, root block vroot, depth vlevels + 1
     int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
@@ -131,7 +131,10 @@ struct BcrWork {
 };
 // k_bcr_split's flag-free back-substitution hand-off: y rows double-buffered by epoch parity (Y even,
 // Racc odd — Racc belongs to the per-level path only); an empty slot holds this signalling-NaN pattern,
-// which no f64 operation produces (they return quiet NaNs).
+// which no f64 operation produces (they return quiet NaNs). INVARIANT: every value published through a
+// flag-free slot (y rows, panels, fills) is the result of f64 arithmetic in the producing kernel, never
+// raw input bits copied through (an input holding this exact pattern would read as "not yet stored");
+// a future publication of copied values must canonicalise them first (v + 0.0 quiets a signalling NaN).
 static constexpr unsigned BCR_Y_EMPTY_D32 = 0xFFF7A5A5u;
 static constexpr unsigned long long BCR_Y_EMPTY = 0xFFF7A5A5FFF7A5A5ull;
 // [XL | XR | x] row stride (136 columns; padding to 144 for conflict-free operand rows measured no gain)
@@ -219,7 +222,8 @@ enum LmMsg { MSG_NONE = 0, MSG_MAX_ITER, MSG_GRAD_TOL, MSG_MIN_RADIUS, MSG_PARAM
              MSG_EVAL_FAIL, MSG_TIMEOUT };
 // chol_flag bits: the reduced-system factorisation hit a non-positive pivot (a linear-solver failure,
 // Ceres' invalid step), or an inter-workgroup hand-off of the resident BCR kernels timed out (the
-// workgroups were not co-resident: a device-level failure that ends the solve with BA_E_INTERNAL)
+// workgroups were not co-resident: the decision stops the device loop without a termination and the host
+// re-runs that iteration with the per-level BCR launches, which have no inter-workgroup waits)
 static constexpr int FLAG_NOT_PD = 1;
 static constexpr int FLAG_TIMEOUT = 2;
 // scal[SC_BAD] >= SC_BAD_TIMEOUT: some workgroup's hand-off timed out
@@ -228,28 +232,6 @@ static constexpr double SC_BAD_TIMEOUT = 8.0;
 static constexpr int RED_X = 16;
 // per-iteration log row: cost, cost_change, |gradient|_inf, |step|, tr_ratio, tr_radius, accepted
 static constexpr int LOG_W = 8;
-
-// Small windows (ba_small.hip): the whole solve in one resident workgroup, the reduced system in LDS.
-// Eligible when npad <= SMALL_NPAD (<= 15 active cameras) and the observation / pair-entry counts stay
-// below the caps; the reference's TUM windows (10-keyframe windows, main.cpp:163-168) are of this size.
-static constexpr int SMALL_NPAD = 96;
-static constexpr int SMALL_MAX_OBS = 32768;
-static constexpr int SMALL_MAX_ENTRIES = 262144;
-static constexpr int SMALL_TPB = 512;
-struct SmallWork {
-    double* wc;   // [n_adm][18] W_o = Jc^T Jp (unscaled) of the last linearisation, point-major obs order
-    double* zb;   // [n_adm][18] Z_o = W~_o G^T of the current step (W~ = s_c W_o s_p, G = chol(V~)^-1)
-    double* pv;   // [n_ap][21] undamped point sums of the last linearisation: V packed (6) | e (3) | Kt (12)
-    double* zk;   // [n_ap][15] Zk = K~ G^T (12) | ze = G e~ (3) of the current step
-    // Schur tasks (one wave each): kind 0 = camera-pair block (a, b), a >= b, entries = ordered observation
-    // pairs (u, v) of one point with ac_u = a, ac_v = b (both orders when a == b and u != v); kind 1 =
-    // border of camera a (S_ka, rhs_a), entries (u, u) over the camera's observations
-    const int4* task;   // (a, b, kind, first entry)
-    const int* task_end;  // one past the last entry of each task
-    const int2* entry;
-    int n_task;
-    int on;  // this window runs the small-window path
-};
 
 struct DevWork {
     double* camdata;
@@ -284,7 +266,6 @@ struct DevWork {
     // nullptr: the tiles flush with f64 atomics
     double* det_tbuf = nullptr;
     const int2* det_trange = nullptr;
-    SmallWork sm{};
     // fused LM-loop linearisation (unsharded, default mode): k_lin_point (point side + camera side in one
     // launch), the envelope tiles as atomic adds inside k_schur_tile onto an S / rhs zeroed by the previous
     // iteration's k_backsub_chunk / k_final
@@ -295,12 +276,12 @@ struct DevWork {
 enum KernelId {
     K_CAM_SIDE = 0, K_LIN_FINALIZE, K_POINT_COLNORM, K_SCALE, K_MEMSET_S, K_ASSEMBLE, K_POINT_PREP, K_SCHUR_TILE,
     K_OBS_PAIRS, K_CHOL, K_UPDATE_CAMS, K_BACKSUB_EVAL, K_FINAL, K_DECIDE, K_XNORM, K_BCR_ELIM, K_BCR_CONTRIB,
-    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_SMALL, K_LIN_POINT, K_COUNT
+    K_BCR_BACK, K_BCR_BORDER, K_COMM, K_CAM_REDUCE, K_BCR_PERSIST, K_PP_REDUCE, K_DUMMY, K_LIN_POINT, K_COUNT
 };
 static const char* const kKernelNames[K_COUNT] = {
     "cam_side", "lin_finalize", "point_colnorm", "scale", "memset_S", "assemble", "point_prep", "schur_tile",
     "obs_pairs", "chol", "update_cams", "backsub_eval", "final", "lm_decide", "xnorm", "bcr_elim", "bcr_contrib",
-    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy", "small_solve", "lin_point"};
+    "bcr_back", "bcr_border", "comm", "cam_reduce", "bcr_persist", "pp_reduce", "dummy", "lin_point"};
 
 // Records an event pair around each launch on the launch stream.
 struct Prof {
@@ -328,6 +309,18 @@ hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevW
 // progress: the host-mapped LM progress word (LmParams::progress), published with the done bit when the
 // initial evaluation is non-finite (nullptr: none)
 hipError_t launch_init_state(const DevProblem& P, DevWork& W, unsigned* progress, hipStream_t s, Prof* pf);
+// ba_prepare's device side: the raw window as the caller passed it + the host plan's orderings (ba_plan.h)
+struct PrepRaw {
+    const int* cam;       // [n_obs] obs_cam
+    const int* pt;        // [n_obs] obs_pt
+    const double2* uv;    // [n_obs]
+    const double* depth;  // [n_obs]
+    const int* cam_ac;    // [n_cams] camera -> active index or -1
+    const int* po_orig;   // [n_adm] point-major slot -> observation
+    const int* co_orig;   // [n_adm] camera-major slot -> observation
+};
+// fills P.po_* (and po_ap / po_pt from pt_ptr / pt_idx) and P.co_* from R
+hipError_t launch_prep_gather(const DevProblem& P, const PrepRaw& R, hipStream_t s);
 // solve start: x and candidate slots <- prepared initial parameters, LM state <- st0
 hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
                         const double* K0, int n_cams, int n_points, hipStream_t s);
@@ -337,7 +330,8 @@ hipError_t launch_factor(const DevProblem& P, const BaConsts& c, DevWork& W, hip
 hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, hipStream_t s,
                          Prof* pf);
 hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, hipStream_t s, Prof* pf);
-hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s, Prof* pf);
+// (Bw.persist drops to 0 when the device refuses the split kernel's cooperative launch)
+hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s, Prof* pf);
 // 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);
@@ -346,11 +340,6 @@ int bcr_persist_ok(int nblk);
 hipError_t bcr_set_spin_limit(unsigned limit);
 // workgroups of k_schur_tile resident at once on the current device (CUs x blocks per CU)
 int schur_tile_slots();
-// Small windows (W.sm.on): iteration 0 and the whole LM loop in ONE launch of one workgroup
-// (ba_small.hip); the decisions land in W.st / W.log as with the multi-launch path.
-hipError_t launch_small(const DevProblem& P, const BaConsts& c, const LmParams& prm, int jacobi, DevWork& W,
-                        hipStream_t s, Prof* pf);
-size_t small_lds_bytes(int npad);
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s);
 

@@ -1894,7 +1894,7 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
                                                int nblk_bs, const double* __restrict__ part,
                                                const int* __restrict__ chol_flag, double* __restrict__ scal,
                                                LmParams prm, const double* __restrict__ lin, double* __restrict__ log,
-                                               double* __restrict__ rhs_z) {
+                                               double* __restrict__ rhs_z, unsigned* __restrict__ bcr_epoch) {
     __shared__ double lds[NW_F * 4];
     __shared__ double out[4];
     __shared__ double red[NW_F];
@@ -1934,6 +1934,9 @@ __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restri
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
     }
     if (done) return;
+    // k_bcr_split ran this iteration (it skips exactly when done | stop_next): the next launch's epoch. Advanced
+    // here, in stream order behind it, so no workgroup of that launch can still be reading the current one.
+    if (bcr_epoch && threadIdx.x == 0 && !S0.stop_next) *bcr_epoch += 1;
     if (rhs_z)  // fused path: y has been consumed; rhs is the next assembly's atomic target
         for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
     block_sum_nw<NW_F, 4>(acc, lds, out);
@@ -2056,7 +2059,8 @@ template <int UNR>
 __global__ __launch_bounds__(TPB_F) void k_final_shard(DevProblem P, const LmState* __restrict__ st, int nblk_pt,
                                                        int nblk_upd, int nblk_bs, const double* __restrict__ part,
                                                        const int* __restrict__ chol_flag, double* __restrict__ red,
-                                                       double* __restrict__ rhs_z, int nranks) {
+                                                       double* __restrict__ rhs_z, int nranks,
+                                                       unsigned* __restrict__ bcr_epoch) {
     __shared__ double lds[NW_F * 8];
     __shared__ double out[8];
     __shared__ double rl[NW_F];
@@ -2087,6 +2091,7 @@ __global__ __launch_bounds__(TPB_F) void k_final_shard(DevProblem P, const LmSta
         bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
     }
     if (done) return;
+    if (bcr_epoch && threadIdx.x == 0 && !st->stop_next) *bcr_epoch += 1;  // as in k_final
     if (rhs_z)  // fused path: y has been consumed; rhs is the next local assembly's atomic target
         for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
     // one SUM all-reduce carries both the sums and the maxima: each rank writes its two maxima into its own
@@ -2367,6 +2372,44 @@ __global__ __launch_bounds__(TPB) void k_reset(DevProblem P, LmState st0, LmStat
     for (size_t e = t; e < nS2; e += stride) reinterpret_cast<double2*>(S)[e] = double2{0.0, 0.0};
 }
 
+// ba_prepare: the observation layouts from the raw window (uploaded as the caller passed it) and the host plan's
+// orderings (ba_plan.cpp) — workgroups [0, nbq): point-major slot q (obs po_orig[q]); [nbq, nbq + nbc): camera-
+// major slot q (obs co_orig[q]); the rest: one active point per thread, its slots' point indices.
+__global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, int nbq, int nbc) {
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (b < nbq) {
+        const int q = b * TPB + tid;
+        if (q >= P.n_adm) return;
+        const int k = R.po_orig[q];
+        const int cam = R.cam[k];
+        const_cast<int*>(P.po_cam)[q] = cam;
+        const_cast<int*>(P.po_ac)[q] = R.cam_ac[cam];
+        const_cast<double2*>(P.po_uv)[q] = R.uv[k];
+        const_cast<double*>(P.po_depth)[q] = R.depth[k];
+    } else if (b < nbq + nbc) {
+        const int q = (b - nbq) * TPB + tid;
+        if (q >= P.n_adm) return;
+        const int k = R.co_orig[q];
+        const_cast<int*>(P.co_pt)[q] = R.pt[k];
+        const_cast<double2*>(P.co_uv)[q] = R.uv[k];
+        const_cast<double*>(P.co_depth)[q] = R.depth[k];
+    } else {
+        const int a = (b - nbq - nbc) * TPB + tid;
+        if (a >= P.n_ap) return;
+        const int pi = P.pt_idx[a];
+        for (int q = P.pt_ptr[a]; q < P.pt_ptr[a + 1]; ++q) {
+            const_cast<int*>(P.po_ap)[q] = a;
+            const_cast<int*>(P.po_pt)[q] = pi;
+        }
+    }
+}
+
+hipError_t launch_prep_gather(const DevProblem& P, const PrepRaw& R, hipStream_t s) {
+    const int nbq = nblocks(P.n_adm, TPB), nba = nblocks(P.n_ap, TPB);
+    if (nbq + nbq + nba > 0) hipLaunchKernelGGL(k_prep_gather, dim3(2 * nbq + nba), dim3(TPB), 0, s, P, R, nbq, nbq);
+    return hipGetLastError();
+}
+
 hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
                         const double* K0, int n_cams, int n_points, hipStream_t s) {
     const int ncd = 7 * n_cams, npd = 3 * n_points;
@@ -2557,13 +2600,15 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
         PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     const int nb_pt = pp_parts(P);
+    // the split BCR kernel's call epoch (the persistent kernel's is advanced by k_bcr_border)
+    unsigned* const ep = (P.solver == 2 && W.bcr.persist >= 2) ? W.bcr.flags : nullptr;
     if (!W.comm.on()) {
         PL(K_FINAL, k_final<2>, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
-           W.chol_flag, W.scal, prm, W.lin, W.log, W.fused ? W.rhs : (double*)nullptr);
+           W.chol_flag, W.scal, prm, W.lin, W.log, W.fused ? W.rhs : (double*)nullptr, ep);
         return hipSuccess;
     }
     PL(K_FINAL, k_final_shard<1>, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
-       W.chol_flag, W.red, W.fused ? W.rhs : (double*)nullptr, W.comm.nranks);
+       W.chol_flag, W.red, W.fused ? W.rhs : (double*)nullptr, W.comm.nranks, ep);
     COMM(W.red + RED_X, W.red + RED_X, 4 + 2 * W.comm.nranks, COMM_F64, COMM_SUM);  // in place
     PL(K_FINAL, k_combine, dim3(1), dim3(64), 0, s, W.st, W.red, W.scal, prm, W.lin, W.log, W.comm.nranks);
     return hipSuccess;

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -23,6 +24,7 @@
 #include "../../include/ba.h"
 #include "ba_host.h"
 #include "ba_kernels.h"
+#include "ba_plan.h"
 
 using namespace miba;
 
@@ -56,12 +58,11 @@ struct DevBuf {
 
 enum BufId {
     B_CAMS0, B_CAMS1, B_PTS0, B_PTS1, B_K0, B_K1, B_PRIOR,
-    B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PO_PT, B_PT_PTR, B_PT_IDX,
-    B_CO_PT, B_CO_UV, B_CO_DEP, B_SEG_PTR, B_SEG_CAM, B_SEG_AC, B_AC_CAM,
+    B_PO_CAM, B_PO_AC, B_PO_UV, B_PO_DEP, B_PO_AP, B_PO_PT,
+    B_CO_PT, B_CO_UV, B_CO_DEP, B_RAW_CAM, B_RAW_PT, B_RAW_UV, B_RAW_DEP, B_PLAN,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
-    B_FCOL, B_RPTR, B_ROWS, B_BCR, B_CAMDATA_LOC, B_ENV_TILE, B_ENV_LOC, B_RED, B_PREP, B_BS_CHUNK, B_AC_SEG, B_CAMPART, B_STATE, B_LOG, B_TILE_CHUNK, B_TILE_BASE, B_TILE_SPAN, B_CHUNK_AP, B_OVF_OBS, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
-    B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_DET_TRANGE,
-    B_SM_WC, B_SM_ZB, B_SM_PV, B_SM_ZK, B_SM_TASK, B_SM_TEND, B_SM_ENTRY,
+    B_BCR, B_CAMDATA_LOC, B_ENV_LOC, B_RED, B_PREP, B_CAMPART, B_STATE, B_LOG, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
+    B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF,
     B_COUNT
 };
 
@@ -78,9 +79,12 @@ struct ba_context {
     size_t hres_cap = 0;        // its capacity in doubles
     DevBuf buf[B_COUNT];
     std::string err;
-    // host-side structure of the last prepared problem
-    std::vector<int> po_orig;  // point-major admissible obs -> original obs index
+    // host-side structure of the last prepared problem (ba_plan.h; plan.po_orig: point-major admissible obs ->
+    // original obs index)
+    Plan plan;
     std::vector<int> pt_idx, ac_cam;
+    char* stage = nullptr;  // pinned staging of ba_prepare's uploads
+    size_t stage_cap = 0;
     DevProblem P{};
     DevWork W{};
     BaConsts C{};
@@ -102,6 +106,8 @@ struct ba_context {
         double intr[4], prior[4];
     } gw;
     bool bcr_fallback = false;  // a resident BCR kernel timed out: per-level launches from then on
+    unsigned long long bcr_launches = 0;  // split-kernel launches since the BCR workspace was initialised
+    int bcr_retries = 0;        // iterations re-run with the per-level launches after a hand-off timeout
     // per-kernel profiling
     Prof prof;
     bool prof_events = false;
@@ -196,7 +202,7 @@ void ba_default_options(ba_options* o) {
     o->device = -1;
     o->deterministic = 0;
     o->shard_min_obs = 262144;
-    o->small_window = 0;
+    o->small_window = 0;          // ignored (the single-workgroup small-window kernel was removed)
 }
 
 ba_context* ba_create(const ba_options* opts) {
@@ -251,6 +257,7 @@ void ba_destroy(ba_context* ctx) {
         for (int i = 0; i < 2 * Prof::MAXP; ++i) hipEventDestroy(ctx->prof.ev[i]);
     if (ctx->hprog) hipHostFree(ctx->hprog);
     if (ctx->hres) hipHostFree(ctx->hres);
+    if (ctx->stage) hipHostFree(ctx->stage);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -402,6 +409,35 @@ static int prepare_gathered(ba_context* ctx, const ba_problem* p) {
     return 1;
 }
 
+// Landmark shards replicate the window's cameras, intrinsics, prior and gauge: every rank must pass the same
+// values (each would otherwise solve a different window and still report success). FNV-1a over their bytes,
+// MIN and MAX all-reduced: a mismatch anywhere gives every rank the same BA_E_INVALID.
+static int shard_replicas_agree(ba_context* ctx, const ba_problem* p) {
+    unsigned long long h = 1469598103934665603ull;
+    auto mix = [&](const void* d, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(d);
+        for (size_t k = 0; k < n; ++k) h = (h ^ b[k]) * 1099511628211ull;
+    };
+    const bool ok = p && p->n_cams >= 0 && (!p->n_cams || p->cams) && p->intr && p->intr_prior;
+    if (ok) {
+        mix(&p->n_cams, sizeof(p->n_cams));
+        mix(&p->fixed_cam, sizeof(p->fixed_cam));
+        mix(p->cams, sizeof(double) * 7 * (size_t)p->n_cams);
+        mix(p->intr, sizeof(double) * 4);
+        mix(p->intr_prior, sizeof(double) * 4);
+    }
+    int lo[2] = {(int)(unsigned)h, (int)(unsigned)(h >> 32)}, hi[2] = {lo[0], lo[1]};
+    int rc = host_allreduce_i32(ctx, lo, 2, COMM_MIN);
+    if (rc == BA_OK) rc = host_allreduce_i32(ctx, hi, 2, COMM_MAX);
+    if (rc != BA_OK) return rc;
+    if (lo[0] != hi[0] || lo[1] != hi[1]) {
+        ctx->err = "landmark shards disagree on the window cameras / intrinsics / prior / fixed_cam (every rank must "
+                   "pass the same replicated values)";
+        return BA_E_INVALID;
+    }
+    return BA_OK;
+}
+
 static int prepare(ba_context* ctx, const ba_problem* p) {
     if (ctx->comm_parked.on()) {  // the last window ran gathered: the communicator is back for this one
         ctx->W.comm = ctx->comm_parked;
@@ -409,6 +445,8 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     }
     ctx->gather_off = 0;
     ctx->dev_np = p && p->n_points > 0 ? p->n_points : 0;
+    if (ctx->W.comm.on())
+        if (int rc = shard_replicas_agree(ctx, p)) return rc;
     if (ctx->W.comm.on() && ctx->opts.shard_min_obs > 0) {
         const int rc = prepare_gathered(ctx, p);
         if (rc != 0) return rc < 0 ? rc : BA_OK;
@@ -416,9 +454,55 @@ static int prepare(ba_context* ctx, const ba_problem* p) {
     return prepare_core(ctx, p, false);
 }
 
+static size_t bcr_bytes(int nblk) {
+    return sizeof(double) * ((BCR_BLOCK_DOUBLES + 64 * 64) * nblk + 16) + sizeof(unsigned) * (16 + 6 * nblk);
+}
+
+// k_bcr_split's hand-off state: the flags (epoch 0) and the flag-free buffers, which start empty (BCR_Y_EMPTY):
+// y (Racc | Y, epoch parity), the published panels (Cf | X slots, two epochs) and the odd epochs' fill
+static int bcr_init_handoffs(ba_context* ctx) {
+    const BcrWork& Bw = ctx->W.bcr;
+    const size_t b64 = (size_t)64 * 64 * Bw.nblk, b8 = (size_t)64 * 8 * Bw.nblk;
+    hipStream_t s = ctx->stream;
+    HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
+    HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Racc, BCR_Y_EMPTY_D32, 4 * b8, s));
+    HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Cf, BCR_Y_EMPTY_D32, 2 * (b64 + (size_t)64 * BCR_XW * Bw.nblk), s));
+    HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.F2, BCR_Y_EMPTY_D32, 2 * b64, s));
+    ctx->bcr_launches = 0;
+    return BA_OK;
+}
+
+// Pinned host staging of ba_prepare's uploads (grown on demand, kept by the context): the raw window is copied
+// in by the host threads and DMA'd while the plan is built; the plan's index arrays follow in one DMA.
+static int stage_ensure(ba_context* ctx, size_t bytes) {
+    if (ctx->stage_cap >= bytes) return BA_OK;
+    if (ctx->stage) HIPCHECK(ctx, hipHostFree(ctx->stage));
+    ctx->stage = nullptr;
+    ctx->stage_cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    HIPCHECK(ctx, hipHostMalloc((void**)&ctx->stage, want, hipHostMallocDefault));
+    ctx->stage_cap = want;
+    return BA_OK;
+}
+
+// parallel memcpy (the host pool) of several arrays into the staging buffer
+struct StageCopy { void* dst; const void* src; size_t bytes; };
+static void stage_copy(const std::vector<StageCopy>& v) {
+    size_t total = 0;
+    for (const StageCopy& c : v) total += c.bytes;
+    const int T = (int)std::max<size_t>(1, std::min<size_t>(4 * (size_t)host_threads(), total >> 18));
+    host_parallel(T, [&](int t) {
+        for (const StageCopy& c : v) {
+            const size_t lo = c.bytes * t / T, hi = c.bytes * (t + 1) / T;
+            if (hi > lo) std::memcpy(static_cast<char*>(c.dst) + lo, static_cast<const char*>(c.src) + lo, hi - lo);
+        }
+    });
+}
+
 static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     const ba_options& o = ctx->opts;
     const bool shard = ctx->W.comm.on();
+    const double tp0 = now_ms();
     // validation: with landmark shards every rank must reach the same verdict before any
     // further collective (a rank that bailed out alone would leave the others waiting)
     int verdict[3] = {0, 0, 0};  // [0] error code (max), [1] n_cams (min), [2] -n_cams (min)
@@ -430,18 +514,35 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         verdict[0] = 1;
     }
     const int nc = verdict[0] ? 0 : p->n_cams, np = verdict[0] ? 0 : p->n_points, no = verdict[0] ? 0 : p->n_obs;
-    std::vector<int> cam_cnt(nc, 0), pt_cnt(np, 0);
-    std::vector<char> adm(no, 0);
-    int n_adm = 0;
-    for (int k = 0; k < no && !verdict[0]; ++k) {
-        const int ci = p->obs_cam[k], pi = p->obs_pt[k];
-        if (ci < 0 || ci >= nc || pi < 0 || pi >= np) { local_err = "observation index out of range"; verdict[0] = 1; break; }
-        if (!(p->obs_depth[k] > 1e-15)) continue;
-        adm[k] = 1;
-        ++n_adm;
-        ++cam_cnt[ci];
-        ++pt_cnt[pi];
+    hipStream_t s = ctx->stream;
+    // the raw observations -> pinned staging -> HBM, in flight while the host builds the plan
+    const size_t raw_bytes = (size_t)no * (16 + 8 + 4 + 4);
+    if (!verdict[0] && no > 0) {
+        if (int rc = stage_ensure(ctx, raw_bytes)) return rc;
+        char* sg = ctx->stage;
+        double* s_uv = reinterpret_cast<double*>(sg);
+        double* s_dep = s_uv + 2 * (size_t)no;
+        int* s_cam = reinterpret_cast<int*>(s_dep + no);
+        int* s_pt = s_cam + no;
+        stage_copy({{s_uv, p->obs_uv, 16 * (size_t)no}, {s_dep, p->obs_depth, 8 * (size_t)no},
+                    {s_cam, p->obs_cam, 4 * (size_t)no}, {s_pt, p->obs_pt, 4 * (size_t)no}});
+        HIPCHECK(ctx, ctx->buf[B_RAW_UV].ensure(16 * (size_t)no));
+        HIPCHECK(ctx, ctx->buf[B_RAW_DEP].ensure(8 * (size_t)no));
+        HIPCHECK(ctx, ctx->buf[B_RAW_CAM].ensure(4 * (size_t)no));
+        HIPCHECK(ctx, ctx->buf[B_RAW_PT].ensure(4 * (size_t)no));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, s_uv, 16 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, s_dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, s_cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_PT].p, s_pt, 4 * (size_t)no, hipMemcpyHostToDevice, s));
     }
+    const double tp_raw = now_ms();
+    Plan& pl = ctx->plan;
+    PlanInput in;
+    in.nc = nc; in.np = np; in.no = no;
+    in.fixed_cam = verdict[0] ? -1 : p->fixed_cam;
+    if (!verdict[0]) { in.obs_cam = p->obs_cam; in.obs_pt = p->obs_pt; in.obs_depth = p->obs_depth; }
+    plan_count(in, pl);
+    if (!verdict[0] && !pl.err.empty()) { local_err = pl.err; verdict[0] = 1; }
     if (shard) {
         verdict[1] = nc;
         verdict[2] = -nc;
@@ -457,248 +558,132 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->err = local_err;
         return BA_E_INVALID;
     }
+    const int n_adm = pl.n_adm;
     // active cameras (Ceres removes unused blocks; the gauge block is constant, :299): a camera
     // is active when any shard observes it; N (the 1/N weights, :280/:290) counts every shard
     std::vector<int> cam_seen(nc);
-    for (int i = 0; i < nc; ++i) cam_seen[i] = cam_cnt[i] > 0;
+    for (int i = 0; i < nc; ++i) cam_seen[i] = pl.cam_cnt[i] > 0;
     int n_adm_all = n_adm;
     if (shard) {
         int rc = host_allreduce_i32(ctx, cam_seen.data(), nc, COMM_MAX);
         if (rc == BA_OK) rc = host_allreduce_i32(ctx, &n_adm_all, 1, COMM_SUM);
         if (rc != BA_OK) return rc;
     }
-    std::vector<int> cam_ac(nc, -1);
-    ctx->ac_cam.clear();
-    for (int i = 0; i < nc; ++i)
-        if (cam_seen[i] && i != p->fixed_cam) { cam_ac[i] = (int)ctx->ac_cam.size(); ctx->ac_cam.push_back(i); }
-    const int nac = (int)ctx->ac_cam.size();
-    // CSR of admissible obs by original point index, each list sorted by active camera
-    std::vector<int> pptr(np + 1, 0);
-    for (int k = 0; k < no; ++k)
-        if (adm[k]) ++pptr[p->obs_pt[k] + 1];
-    for (int i = 0; i < np; ++i) pptr[i + 1] += pptr[i];
-    std::vector<int> plist(n_adm);
-    {
-        std::vector<int> f(pptr.begin(), pptr.end() - 1);
-        for (int k = 0; k < no; ++k)
-            if (adm[k]) plist[f[p->obs_pt[k]]++] = k;
-    }
-    std::vector<int> pmin(np, INT32_MAX), pmax(np, -1);
-    std::vector<char> pclass(np, -1);  // 0 tiled, 1 overflow (Schur via atomics), 2 gauge-only
-    for (int i = 0; i < np; ++i) {
-        if (pt_cnt[i] == 0) continue;
-        std::stable_sort(plist.begin() + pptr[i], plist.begin() + pptr[i + 1],
-                         [&](int x, int y) { return cam_ac[p->obs_cam[x]] < cam_ac[p->obs_cam[y]]; });
-        bool dup = false;
-        int prev = -2;
-        for (int q = pptr[i]; q < pptr[i + 1]; ++q) {
-            const int a = cam_ac[p->obs_cam[plist[q]]];
-            if (a < 0) continue;
-            pmin[i] = std::min(pmin[i], a);
-            pmax[i] = std::max(pmax[i], a);
-            if (a == prev) dup = true;
-            prev = a;
-        }
-        if (pmax[i] < 0) pclass[i] = 2;
-        else if (dup || pmax[i] - pmin[i] + 1 > TILE_WIN || pt_cnt[i] > CHUNK_OBS) pclass[i] = 1;
-        else pclass[i] = 0;
-    }
-    std::vector<int> cls[3];
-    for (int i = 0; i < np; ++i)
-        if (pclass[i] >= 0) cls[(int)pclass[i]].push_back(i);
-    for (int k = 0; k < 2; ++k)
-        std::stable_sort(cls[k].begin(), cls[k].end(), [&](int a, int b) { return pmin[a] < pmin[b]; });
-    // tiles over the tiled points: window [base, base + span), span <= TILE_WIN, <= TILE_PTS points;
-    // chunks of <= CHUNK_PTS points and <= CHUNK_OBS observations. TILE_PTS spreads the points over
-    // one wave of resident workgroups (no second, partly empty wave of tiles), grown until the tile
-    // count fits the resident slots.
-    std::vector<int> tile_chunk, tile_base, tile_span, chunk_ap;
-    auto build_tiles = [&](int tile_pts) {
-        tile_chunk.assign(1, 0); tile_base.clear(); tile_span.clear(); chunk_ap.assign(1, 0);
-        const std::vector<int>& T = cls[0];
-        const int n0 = (int)T.size();
-        int i = 0;
-        while (i < n0) {
-            const int base = pmin[T[i]];
-            int j = i, hi = base;
-            while (j < n0 && j - i < tile_pts && pmax[T[j]] - base < TILE_WIN) { hi = std::max(hi, pmax[T[j]]); ++j; }
-            int c0 = i;
-            while (c0 < j) {
-                int c1 = c0, nob = 0;
-                while (c1 < j && c1 - c0 < CHUNK_PTS && nob + pt_cnt[T[c1]] <= CHUNK_OBS) { nob += pt_cnt[T[c1]]; ++c1; }
-                chunk_ap.push_back(c1);
-                c0 = c1;
-            }
-            tile_chunk.push_back((int)chunk_ap.size() - 1);
-            tile_base.push_back(base);
-            tile_span.push_back(hi - base + 1);
-            i = j;
-        }
-    };
-    {
-        const int slots = schur_tile_slots() - 1;  // one resident slot for the intrinsics-term workgroup
-        int tile_pts = 128;
-        if (slots > 0) tile_pts = std::max(CHUNK_PTS, (int)((cls[0].size() + slots - 1) / slots));
-        const char* e = std::getenv("MIBA_TILE_PTS");
-        if (e) tile_pts = std::max(1, std::atoi(e));
-        build_tiles(tile_pts);
-        for (int grow = 0; !e && slots > 0 && (int)tile_base.size() > slots && grow < 16; ++grow) {
-            tile_pts += std::max(1, tile_pts / 8);
-            build_tiles(tile_pts);
-        }
-    }
-    // active point order: tiled (tile order), overflow, gauge-only
-    ctx->pt_idx.clear();
-    for (int k = 0; k < 3; ++k) ctx->pt_idx.insert(ctx->pt_idx.end(), cls[k].begin(), cls[k].end());
-    const int n_ap = (int)ctx->pt_idx.size();
-    const int n_tiled = (int)cls[0].size();
-    // point-major obs in that order
-    std::vector<int> pt_ptr(n_ap + 1, 0);
-    ctx->po_orig.clear();
-    ctx->po_orig.reserve(n_adm);
-    for (int a = 0; a < n_ap; ++a) {
-        const int i = ctx->pt_idx[a];
-        ctx->po_orig.insert(ctx->po_orig.end(), plist.begin() + pptr[i], plist.begin() + pptr[i + 1]);
-        pt_ptr[a + 1] = (int)ctx->po_orig.size();
-    }
-    std::vector<int> po_cam(n_adm), po_ac(n_adm), po_ap(n_adm), po_pt(n_adm), ovf_obs;
-    std::vector<double> po_uv(2 * (size_t)n_adm), po_dep(n_adm);
-    for (int a = 0; a < n_ap; ++a)
-        for (int q = pt_ptr[a]; q < pt_ptr[a + 1]; ++q) {
-            const int k = ctx->po_orig[q];
-            po_cam[q] = p->obs_cam[k];
-            po_ac[q] = cam_ac[p->obs_cam[k]];
-            po_ap[q] = a;
-            po_pt[q] = ctx->pt_idx[a];
-            po_uv[2 * (size_t)q] = p->obs_uv[2 * (size_t)k];
-            po_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
-            po_dep[q] = p->obs_depth[k];
-            if (a >= n_tiled && po_ac[q] >= 0) ovf_obs.push_back(q);
-        }
-    // back-substitution chunks over all active points: <= BS_PTS points and <= BS_OBS observations
-    std::vector<int> bs_chunk(1, 0);
-    for (int a = 0; a < n_ap;) {
-        int b = a + 1;
-        while (b < n_ap && b - a < BS_PTS && pt_ptr[b + 1] - pt_ptr[a] <= BS_OBS) ++b;
-        bs_chunk.push_back(b);
-        a = b;
-    }
-    const int n_bs_chunks = (int)bs_chunk.size() - 1;
-    // camera-major obs: one segment per camera with admissible obs (gauge included)
-    std::vector<int> seg_ptr(1, 0), seg_cam, seg_ac;
-    std::vector<int> cstart(nc + 1, 0);
-    for (int i = 0; i < nc; ++i) cstart[i + 1] = cstart[i] + cam_cnt[i];
-    std::vector<int> cfill(cstart.begin(), cstart.end() - 1);
-    std::vector<int> co_pt(n_adm);
-    std::vector<double> co_uv(2 * (size_t)n_adm), co_dep(n_adm);
-    for (int k = 0; k < no; ++k)
-        if (adm[k]) {
-            const int q = cfill[p->obs_cam[k]]++;
-            co_pt[q] = p->obs_pt[k];
-            co_uv[2 * (size_t)q] = p->obs_uv[2 * (size_t)k];
-            co_uv[2 * (size_t)q + 1] = p->obs_uv[2 * (size_t)k + 1];
-            co_dep[q] = p->obs_depth[k];
-        }
-    // sub-segments of <= SUBSEG_OBS observations (one workgroup each); ac_seg[ac] = the
-    // sub-segment range of active camera ac (empty when this shard has no observation of it)
-    std::vector<int2> ac_seg(std::max(nac, 1), make_int2(0, 0));
+    PlanParams pp;
+    pp.tile_win = TILE_WIN;
+    pp.chunk_pts = CHUNK_PTS;
+    pp.chunk_obs = CHUNK_OBS;
+    pp.tile_slots = schur_tile_slots();
+    if (const char* e = std::getenv("MIBA_TILE_PTS")) pp.tile_pts_env = std::max(1, std::atoi(e));
+    pp.bs_pts = BS_PTS;
+    pp.bs_obs = BS_OBS;
     // sub-segment size: ~6.5 observations per thread on large windows (C4 rocprof, fused linearisation:
     // 34.2 us at 1700 vs 36.1 at 1024, 42.7 at 512, 34.7 at 2500); MIBA_SUBSEG overrides (tuning)
-    int subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : SUBSEG_OBS;
-    if (const char* e = getenv("MIBA_SUBSEG")) subseg = std::max(64, atoi(e));
-    for (int i = 0; i < nc; ++i)
-        if (cam_cnt[i] > 0) {
-            const int first = (int)seg_cam.size();
-            // equal sub-segments of <= subseg observations
-            const int cnt = cstart[i + 1] - cstart[i], nseg = (cnt + subseg - 1) / subseg;
-            for (int k = 1; k <= nseg; ++k) {
-                seg_cam.push_back(i);
-                seg_ac.push_back(cam_ac[i]);
-                seg_ptr.push_back(cstart[i] + (int)(((long long)cnt * k) / nseg));
-            }
-            if (cam_ac[i] >= 0) ac_seg[cam_ac[i]] = make_int2(first, (int)seg_cam.size());
-        }
-    // envelope of S: first co-visible active camera of each active camera
-    std::vector<int> fc(nac);
-    for (int a = 0; a < nac; ++a) fc[a] = a;
-    for (int q = 0; q < n_adm; ++q) {
-        const int a = po_ac[q];
-        if (a >= 0) fc[a] = std::min(fc[a], pmin[ctx->pt_idx[po_ap[q]]]);
-    }
+    pp.subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : SUBSEG_OBS;
+    if (const char* e = std::getenv("MIBA_SUBSEG")) pp.subseg = std::max(64, std::atoi(e));
+    plan_order(in, cam_seen, pp, pl);
+    const int nac = pl.nac;
     if (shard) {  // envelope / band of the summed S: union over the shards
-        const int rc = host_allreduce_i32(ctx, fc.data(), nac, COMM_MIN);
+        const int rc = host_allreduce_i32(ctx, pl.fc.data(), nac, COMM_MIN);
         if (rc != BA_OK) return rc;
     }
-    const int n = 6 * nac + 4;
-    const int npad = (n + 15) / 16 * 16;
-    const int nb = npad / 16;
-    std::vector<int> fcol(nb, INT32_MAX);
-    for (int r = 0; r < npad; ++r) {
-        const int first = (r < 6 * nac) ? 6 * fc[r / 6] : 0;
-        fcol[r / 16] = std::min(fcol[r / 16], first / 16);
+    plan_envelope(pl);
+    const double tp_plan = now_ms();
+    const int n_ap = pl.n_ap(), n_tiled = pl.n_tiled;
+    const int n = pl.n, npad = pl.npad, nb = pl.nb, band_w = pl.band_w, cam_band = pl.cam_band;
+    const int n_bs_chunks = (int)pl.bs_chunk.size() - 1;
+    const int n_seg = (int)pl.seg_cam.size();
+    const int n_env = (int)pl.env_tile.size() / 2;
+    const bool det = (o.deterministic || force_det) && !pl.tile_base.empty();
+    std::vector<int> trange;  // deterministic mode: each active camera's Schur tile range
+    if (det) {
+        trange.assign(2 * (size_t)std::max(nac, 1), 0);
+        const int nt = (int)pl.tile_base.size();
+        for (int a = 0, lo = 0, hi = 0; a < nac; ++a) {
+            while (lo < nt && pl.tile_base[lo] < a - (TILE_WIN - 1)) ++lo;
+            while (hi < nt && pl.tile_base[hi] <= a) ++hi;
+            trange[2 * a] = lo;
+            trange[2 * a + 1] = std::max(lo, hi);
+        }
     }
-    int cam_band = 0;
-    for (int a = 0; a < nac; ++a) cam_band = std::max(cam_band, a - fc[a]);
-    // band width (in 16-tiles) of the camera part; the last block row is the dense border
-    int band_w = 0;
-    for (int i = 0; i + 1 < nb; ++i) band_w = std::max(band_w, i - fcol[i]);
-    std::vector<int> rptr(nb + 1, 0), rows;
-    for (int k = 0; k < nb; ++k) {
-        for (int i = k + 1; i < nb; ++i)
-            if (fcol[i] <= k) rows.push_back(i);
-        rptr[k + 1] = (int)rows.size();
+    // ---- uploads: the plan's index arrays in one staged DMA (each array 256-byte aligned in B_PLAN)
+    struct Part { const int* src; size_t n; size_t off; };
+    std::vector<Part> parts = {
+        {pl.po_orig.data(), (size_t)n_adm, 0}, {pl.co_orig.data(), (size_t)n_adm, 0}, {pl.cam_ac.data(), (size_t)nc, 0},
+        {pl.pt_ptr.data(), (size_t)n_ap + 1, 0}, {pl.pt_idx.data(), (size_t)n_ap, 0},
+        {pl.seg_ptr.data(), pl.seg_ptr.size(), 0}, {pl.seg_cam.data(), pl.seg_cam.size(), 0},
+        {pl.seg_ac.data(), pl.seg_ac.size(), 0}, {pl.ac_seg.data(), pl.ac_seg.size(), 0},
+        {pl.ac_cam.data(), (size_t)nac, 0}, {pl.fcol.data(), (size_t)nb, 0},
+        {pl.tile_chunk.data(), pl.tile_chunk.size(), 0}, {pl.tile_base.data(), pl.tile_base.size(), 0},
+        {pl.tile_span.data(), pl.tile_span.size(), 0}, {pl.chunk_ap.data(), pl.chunk_ap.size(), 0},
+        {pl.bs_chunk.data(), pl.bs_chunk.size(), 0}, {pl.ovf_obs.data(), pl.ovf_obs.size(), 0},
+        {pl.rptr.data(), (size_t)nb + 1, 0}, {pl.rows.data(), pl.rows.size(), 0},
+        {pl.env_tile.data(), pl.env_tile.size(), 0}, {trange.data(), trange.size(), 0}};
+    enum { PO_ORIG, CO_ORIG, CAM_AC, PT_PTR, PT_IDX, SEG_PTR, SEG_CAM, SEG_AC, AC_SEG, AC_CAM, FCOL, TILE_CHUNK,
+           TILE_BASE, TILE_SPAN, CHUNK_AP, BS_CHUNK, OVF_OBS, RPTR, ROWS, ENV_TILE, TRANGE };
+    size_t plan_ints = 0;
+    for (Part& q : parts) {
+        q.off = plan_ints;
+        plan_ints += (q.n + 63) / 64 * 64 + 64;
     }
-    // ---- uploads
-    hipStream_t s = ctx->stream;
+    const size_t raw_off = (raw_bytes + 255) / 256 * 256;  // after the raw region, which may still be in flight
+    if (ctx->stage_cap < raw_off + 4 * plan_ints) {
+        HIPCHECK(ctx, hipStreamSynchronize(s));  // growing frees the buffer the raw DMA reads
+        if (int rc = stage_ensure(ctx, raw_off + 4 * plan_ints)) return rc;
+    }
+    int* sp = reinterpret_cast<int*>(ctx->stage + raw_off);
+    {
+        std::vector<StageCopy> cp;
+        for (const Part& q : parts)
+            if (q.n) cp.push_back({sp + q.off, q.src, 4 * q.n});
+        stage_copy(cp);
+    }
+    HIPCHECK(ctx, ctx->buf[B_PLAN].ensure(4 * plan_ints));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PLAN].p, sp, 4 * plan_ints, hipMemcpyHostToDevice, s));
+    int* dp = ctx->buf[B_PLAN].as<int>();
+    auto dptr = [&](int k) { return dp + parts[k].off; };
+    // parameters: one upload each, the other slots copied on the device
     HIPCHECK(ctx, upload(ctx, B_CAMS0, p->cams, 7 * (size_t)nc));
-    HIPCHECK(ctx, upload(ctx, B_CAMS1, p->cams, 7 * (size_t)nc));
     HIPCHECK(ctx, upload(ctx, B_PTS0, p->points, 3 * (size_t)np));
-    HIPCHECK(ctx, upload(ctx, B_PTS1, p->points, 3 * (size_t)np));
     HIPCHECK(ctx, upload(ctx, B_K0, p->intr, 4));
-    HIPCHECK(ctx, upload(ctx, B_K1, p->intr, 4));
     HIPCHECK(ctx, upload(ctx, B_PRIOR, p->intr_prior, 4));
-    HIPCHECK(ctx, upload(ctx, B_CAMS_INIT, p->cams, 7 * (size_t)nc));
-    HIPCHECK(ctx, upload(ctx, B_PTS_INIT, p->points, 3 * (size_t)np));
-    HIPCHECK(ctx, upload(ctx, B_K_INIT, p->intr, 4));
-    HIPCHECK(ctx, upload(ctx, B_PO_CAM, po_cam.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_PO_AC, po_ac.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_PO_UV, po_uv.data(), 2 * (size_t)n_adm));
-    HIPCHECK(ctx, upload(ctx, B_PO_DEP, po_dep.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_PO_AP, po_ap.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_PO_PT, po_pt.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_PT_PTR, pt_ptr.data(), n_ap + 1));
-    HIPCHECK(ctx, upload(ctx, B_PT_IDX, ctx->pt_idx.data(), n_ap));
-    HIPCHECK(ctx, upload(ctx, B_CO_PT, co_pt.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_CO_UV, co_uv.data(), 2 * (size_t)n_adm));
-    HIPCHECK(ctx, upload(ctx, B_CO_DEP, co_dep.data(), n_adm));
-    HIPCHECK(ctx, upload(ctx, B_SEG_PTR, seg_ptr.data(), seg_ptr.size()));
-    HIPCHECK(ctx, upload(ctx, B_SEG_CAM, seg_cam.data(), seg_cam.size()));
-    HIPCHECK(ctx, upload(ctx, B_SEG_AC, seg_ac.data(), seg_ac.size()));
-    HIPCHECK(ctx, upload(ctx, B_AC_SEG, ac_seg.data(), ac_seg.size()));
-    HIPCHECK(ctx, upload(ctx, B_AC_CAM, ctx->ac_cam.data(), nac));
-    HIPCHECK(ctx, upload(ctx, B_FCOL, fcol.data(), nb));
-    HIPCHECK(ctx, upload(ctx, B_TILE_CHUNK, tile_chunk.data(), tile_chunk.size()));
-    HIPCHECK(ctx, upload(ctx, B_TILE_BASE, tile_base.data(), tile_base.size()));
-    HIPCHECK(ctx, upload(ctx, B_TILE_SPAN, tile_span.data(), tile_span.size()));
-    HIPCHECK(ctx, upload(ctx, B_CHUNK_AP, chunk_ap.data(), chunk_ap.size()));
-    HIPCHECK(ctx, upload(ctx, B_BS_CHUNK, bs_chunk.data(), bs_chunk.size()));
-    HIPCHECK(ctx, upload(ctx, B_OVF_OBS, ovf_obs.data(), ovf_obs.size()));
-    HIPCHECK(ctx, upload(ctx, B_RPTR, rptr.data(), nb + 1));
-    HIPCHECK(ctx, upload(ctx, B_ROWS, rows.data(), rows.size()));
-    const int n_seg = (int)seg_cam.size();
+    HIPCHECK(ctx, ctx->buf[B_CAMS1].ensure(sizeof(double) * std::max<size_t>(7 * (size_t)nc, 1)));
+    HIPCHECK(ctx, ctx->buf[B_CAMS_INIT].ensure(sizeof(double) * std::max<size_t>(7 * (size_t)nc, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PTS1].ensure(sizeof(double) * std::max<size_t>(3 * (size_t)np, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PTS_INIT].ensure(sizeof(double) * std::max<size_t>(3 * (size_t)np, 1)));
+    HIPCHECK(ctx, ctx->buf[B_K1].ensure(sizeof(double) * 4));
+    HIPCHECK(ctx, ctx->buf[B_K_INIT].ensure(sizeof(double) * 4));
+    if (nc) {
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_CAMS1].p, ctx->buf[B_CAMS0].p, 56 * (size_t)nc, hipMemcpyDeviceToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_CAMS_INIT].p, ctx->buf[B_CAMS0].p, 56 * (size_t)nc, hipMemcpyDeviceToDevice, s));
+    }
+    if (np) {
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PTS1].p, ctx->buf[B_PTS0].p, 24 * (size_t)np, hipMemcpyDeviceToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PTS_INIT].p, ctx->buf[B_PTS0].p, 24 * (size_t)np, hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_K1].p, ctx->buf[B_K0].p, 32, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_K_INIT].p, ctx->buf[B_K0].p, 32, hipMemcpyDeviceToDevice, s));
+    // the observation layouts, gathered on the device from the raw window and the plan's orderings
+    HIPCHECK(ctx, ctx->buf[B_PO_CAM].ensure(4 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PO_AC].ensure(4 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PO_AP].ensure(4 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_PO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_CO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_CO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
+    HIPCHECK(ctx, ctx->buf[B_CO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
+    ctx->ac_cam = pl.ac_cam;
+    ctx->pt_idx = pl.pt_idx;
+    const std::vector<int>& tile_base = pl.tile_base;
+    const std::vector<int>& ovf_obs = pl.ovf_obs;
     const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
     const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS, 1});
     HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
-    // landmark sharding: envelope tile list of S, pack buffers, exchange scalars
-    // envelope tiles of S: every solver reads only these; the per-iteration clear of S covers
-    // only them (the rest is zeroed once here), and the shard all-reduce packs them
-    std::vector<int2> env_tile;
-    for (int i = 0; i < nb; ++i)
-        for (int j = fcol[i]; j <= i; ++j) env_tile.push_back(make_int2(i, j));
-    HIPCHECK(ctx, upload(ctx, B_ENV_TILE, env_tile.data(), env_tile.size()));
+    // landmark sharding: pack buffers of the envelope tiles of S, exchange scalars
     if (shard) {
         // envelope tiles + rhs (+ the camera and intrinsics sums of the folded exchange)
-        const size_t ne = env_tile.size() * 256 + (size_t)npad + (size_t)nac * CAMDATA + SEGINTR + 1;
+        const size_t ne = (size_t)n_env * 256 + (size_t)npad + (size_t)nac * CAMDATA + SEGINTR + 1;
         HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
         HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
@@ -732,23 +717,34 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     P.po_cam = ctx->buf[B_PO_CAM].as<int>(); P.po_ac = ctx->buf[B_PO_AC].as<int>();
     P.po_uv = ctx->buf[B_PO_UV].as<double2>(); P.po_depth = ctx->buf[B_PO_DEP].as<double>();
     P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.po_pt = ctx->buf[B_PO_PT].as<int>();
-    P.pt_ptr = ctx->buf[B_PT_PTR].as<int>();
-    P.pt_idx = ctx->buf[B_PT_IDX].as<int>();
+    P.pt_ptr = dptr(PT_PTR);
+    P.pt_idx = dptr(PT_IDX);
     P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
     P.co_depth = ctx->buf[B_CO_DEP].as<double>();
-    P.seg_ptr = ctx->buf[B_SEG_PTR].as<int>(); P.seg_cam = ctx->buf[B_SEG_CAM].as<int>();
-    P.seg_ac = ctx->buf[B_SEG_AC].as<int>(); P.ac_cam = ctx->buf[B_AC_CAM].as<int>();
-    P.ac_seg = ctx->buf[B_AC_SEG].as<int2>();
-    P.tile_chunk = ctx->buf[B_TILE_CHUNK].as<int>(); P.tile_base = ctx->buf[B_TILE_BASE].as<int>();
-    P.tile_span = ctx->buf[B_TILE_SPAN].as<int>(); P.chunk_ap = ctx->buf[B_CHUNK_AP].as<int>();
-    P.ovf_obs = ctx->buf[B_OVF_OBS].as<int>();
-    P.bs_chunk = ctx->buf[B_BS_CHUNK].as<int>();
+    P.seg_ptr = dptr(SEG_PTR); P.seg_cam = dptr(SEG_CAM);
+    P.seg_ac = dptr(SEG_AC); P.ac_cam = dptr(AC_CAM);
+    P.ac_seg = reinterpret_cast<const int2*>(dptr(AC_SEG));
+    P.tile_chunk = dptr(TILE_CHUNK); P.tile_base = dptr(TILE_BASE);
+    P.tile_span = dptr(TILE_SPAN); P.chunk_ap = dptr(CHUNK_AP);
+    P.ovf_obs = dptr(OVF_OBS);
+    P.bs_chunk = dptr(BS_CHUNK);
     P.n_bs_chunks = n_bs_chunks;
     P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
     ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
     P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
     P.n = n; P.npad = npad; P.kb = 6 * nac;
     P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
+    {
+        PrepRaw R;
+        R.cam = ctx->buf[B_RAW_CAM].as<int>();
+        R.pt = ctx->buf[B_RAW_PT].as<int>();
+        R.uv = ctx->buf[B_RAW_UV].as<double2>();
+        R.depth = ctx->buf[B_RAW_DEP].as<double>();
+        R.cam_ac = dptr(CAM_AC);
+        R.po_orig = dptr(PO_ORIG);
+        R.co_orig = dptr(CO_ORIG);
+        HIPCHECK(ctx, launch_prep_gather(P, R, s));
+    }
     P.part_stride = part_stride;
     P.band_w = (nb >= 2 && nb <= 2048 && band_w <= 6) ? std::max(band_w, 1) : 0;
     P.cam_band = cam_band;
@@ -764,67 +760,8 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         else if (!std::strcmp(e, "bcr") && cam_band < BCR_CAMS && bcr_nblk >= 1) P.solver = 2;
     }
     if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
-    // small windows: the whole solve in one workgroup (ba_small.hip), unless a solver is forced
-    const char* e_small = std::getenv("MIBA_SMALL");
-    const bool small = !shard && o.small_window && npad <= SMALL_NPAD && n_adm <= SMALL_MAX_OBS &&
-                       !std::getenv("MIBA_SOLVER") && !std::getenv("MIBA_DENSE_CHOL") && !(e_small && e_small[0] == '0');
-    ctx->W.sm.on = 0;
-    if (small) {
-        // Schur tasks: camera-pair blocks (a >= b) over the ordered observation pairs of each point, and
-        // each camera's border rows over its observations (point-major obs indices, point order)
-        std::vector<std::vector<int2>> blk((size_t)nac * nac), brd(nac);
-        size_t n_entries = 0;
-        for (int a = 0; a < n_ap && n_entries <= (size_t)SMALL_MAX_ENTRIES; ++a)
-            for (int q = pt_ptr[a]; q < pt_ptr[a + 1]; ++q) {
-                const int ai = po_ac[q];
-                if (ai < 0) continue;
-                brd[ai].push_back(make_int2(q, q));
-                for (int r = pt_ptr[a]; r < pt_ptr[a + 1]; ++r) {
-                    const int aj = po_ac[r];
-                    if (aj < 0 || aj > ai) continue;
-                    blk[(size_t)ai * nac + aj].push_back(make_int2(q, r));
-                    ++n_entries;
-                }
-                ++n_entries;
-            }
-        if (n_entries <= (size_t)SMALL_MAX_ENTRIES) {
-            struct T { int a, b, kind; const std::vector<int2>* e; };
-            std::vector<T> tasks;
-            for (int a = 0; a < nac; ++a)
-                for (int b = 0; b <= a; ++b)
-                    if (!blk[(size_t)a * nac + b].empty()) tasks.push_back({a, b, 0, &blk[(size_t)a * nac + b]});
-            for (int a = 0; a < nac; ++a)
-                if (!brd[a].empty()) tasks.push_back({a, a, 1, &brd[a]});
-            std::vector<int4> tk;
-            std::vector<int> tend;
-            std::vector<int2> ent;
-            for (const T& t : tasks) {
-                tk.push_back(make_int4(t.a, t.b, t.kind, (int)ent.size()));
-                ent.insert(ent.end(), t.e->begin(), t.e->end());
-                tend.push_back((int)ent.size());
-            }
-            HIPCHECK(ctx, upload(ctx, B_SM_TASK, tk.data(), tk.size()));
-            HIPCHECK(ctx, upload(ctx, B_SM_TEND, tend.data(), tend.size()));
-            HIPCHECK(ctx, upload(ctx, B_SM_ENTRY, ent.data(), ent.size()));
-            HIPCHECK(ctx, ctx->buf[B_SM_WC].ensure(sizeof(double) * 18 * std::max(n_adm, 1)));
-            HIPCHECK(ctx, ctx->buf[B_SM_ZB].ensure(sizeof(double) * 18 * std::max(n_adm, 1)));
-            HIPCHECK(ctx, ctx->buf[B_SM_PV].ensure(sizeof(double) * 21 * std::max(n_ap, 1)));
-            HIPCHECK(ctx, ctx->buf[B_SM_ZK].ensure(sizeof(double) * 15 * std::max(n_ap, 1)));
-            SmallWork& Z = ctx->W.sm;
-            Z.wc = ctx->buf[B_SM_WC].as<double>();
-            Z.zb = ctx->buf[B_SM_ZB].as<double>();
-            Z.pv = ctx->buf[B_SM_PV].as<double>();
-            Z.zk = ctx->buf[B_SM_ZK].as<double>();
-            Z.task = ctx->buf[B_SM_TASK].as<int4>();
-            Z.task_end = ctx->buf[B_SM_TEND].as<int>();
-            Z.entry = ctx->buf[B_SM_ENTRY].as<int2>();
-            Z.n_task = (int)tk.size();
-            Z.on = 1;
-            P.solver = BA_LS_SMALL;
-        }
-    }
     if (P.solver == 2) {
-        const size_t bytes = sizeof(double) * ((BCR_BLOCK_DOUBLES + 64 * 64) * bcr_nblk + 16) + sizeof(unsigned) * (16 + 6 * bcr_nblk);
+        const size_t bytes = bcr_bytes(bcr_nblk);
         HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
         // upper tiles of UL/UR are never written and must read as zero
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
@@ -855,12 +792,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         Bw.F2 = Bw.rd + (size_t)64 * bcr_nblk;
         Bw.bk = Bw.F2 + b64;
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
-        // k_bcr_split's flag-free hand-off buffers start empty (BCR_Y_EMPTY): y (Racc | Y, epoch parity),
-        // the published panels (Cf | X slots, two epochs) and the odd epochs' fill
-        HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Racc, BCR_Y_EMPTY_D32, 4 * b8, ctx->stream));
-        HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Cf, BCR_Y_EMPTY_D32, 2 * (b64 + (size_t)64 * BCR_XW * bcr_nblk),
-                                        ctx->stream));
-        HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.F2, BCR_Y_EMPTY_D32, 2 * b64, ctx->stream));
+        if (int rc = bcr_init_handoffs(ctx)) return rc;
         Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
@@ -872,8 +804,8 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
     W.camdata_loc = shard ? ctx->buf[B_CAMDATA_LOC].as<double>() : W.camdata;
     W.camdata_part = ctx->buf[B_CAMPART].as<double>();
-    W.env_tile = ctx->buf[B_ENV_TILE].as<int2>();
-    W.n_env = (int)env_tile.size();
+    W.env_tile = reinterpret_cast<const int2*>(dptr(ENV_TILE));
+    W.n_env = n_env;
     W.env_loc = shard ? ctx->buf[B_ENV_LOC].as<double>() : nullptr;
     W.red = shard ? ctx->buf[B_RED].as<double>() : nullptr;
     P.rank = W.comm.rank;
@@ -883,22 +815,15 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     W.S = ctx->buf[B_S].as<double>(); W.rhs = ctx->buf[B_RHS].as<double>();
     W.delta = ctx->buf[B_DELTA].as<double>(); W.part = ctx->buf[B_PART].as<double>();
     W.scal = ctx->buf[B_SCAL].as<double>(); W.chol_flag = ctx->buf[B_FLAG].as<int>();
-    W.fcol = ctx->buf[B_FCOL].as<int>(); W.rptr = ctx->buf[B_RPTR].as<int>(); W.rows = ctx->buf[B_ROWS].as<int>();
+    W.fcol = dptr(FCOL); W.rptr = dptr(RPTR); W.rows = dptr(ROWS);
     W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
     // deterministic mode: the Schur tiles write per-tile slabs, summed in tile order per element of S
     W.det_tbuf = nullptr;
     W.det_trange = nullptr;
-    if ((o.deterministic || force_det) && P.n_tiles > 0) {
+    if (det) {
         HIPCHECK(ctx, ctx->buf[B_DET_TBUF].ensure(sizeof(double) * SCH_TBUF * (size_t)P.n_tiles));
-        std::vector<int2> trange(std::max(nac, 1));
-        for (int a = 0, lo = 0, hi = 0; a < nac; ++a) {
-            while (lo < P.n_tiles && tile_base[lo] < a - (TILE_WIN - 1)) ++lo;
-            while (hi < P.n_tiles && tile_base[hi] <= a) ++hi;
-            trange[a] = make_int2(lo, std::max(lo, hi));
-        }
-        HIPCHECK(ctx, upload(ctx, B_DET_TRANGE, trange.data(), trange.size()));
         W.det_tbuf = ctx->buf[B_DET_TBUF].as<double>();
-        W.det_trange = ctx->buf[B_DET_TRANGE].as<int2>();
+        W.det_trange = reinterpret_cast<const int2*>(dptr(TRANGE));
     }
     // fused LM-loop linearisation (k_lin_point + envelope tiles in k_schur_tile, S / rhs zeroed by the previous
     // iteration): the unsharded default-mode path with points and camera segments
@@ -907,7 +832,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         const bool off = e && e[0] == '0';
         // landmark shards: the same choice on every rank (it fixes the collective sequence), so only uniform inputs
         W.fused = (shard ? (!o.deterministic && !off)
-                         : (!W.det_tbuf && n_ap > 0 && n_seg > 0 && P.solver != BA_LS_SMALL && !off)) ? 1 : 0;
+                         : (!W.det_tbuf && n_ap > 0 && n_seg > 0 && !off)) ? 1 : 0;
     }
     BaConsts& C = ctx->C;
     ctx->n_adm_all = n_adm_all;
@@ -928,7 +853,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     {
         const double A = n_adm, Pn = n_ap, Cn = nac, Sg = n_seg;
         double env = 0;  // envelope tiles of the reduced system
-        for (int k = 0; k < nb; ++k) env += (double)(rptr[k + 1] - rptr[k]) + 1.0;
+        for (int k = 0; k < nb; ++k) env += (double)(pl.rptr[k + 1] - pl.rptr[k]) + 1.0;
         const double env_bytes = env * 16 * 16 * 8;
         double* kb = ctx->k_bytes;
         double* kf = ctx->k_flops;
@@ -938,7 +863,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         kb[K_LIN_FINALIZE] = Sg * SEGINTR * 8 + Cn * (56 + 48) + LIN_N * 8;
         kb[K_POINT_COLNORM] = A * 28 + Pn * (8 + 24 + 24);
         kb[K_SCALE] = (6 * Cn + 3 * Pn + 4) * 16;
-        kb[K_MEMSET_S] = (double)env_tile.size() * 256 * 8;
+        kb[K_MEMSET_S] = (double)n_env * 256 * 8;
         kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
         kb[K_POINT_PREP] = A * 28 + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
         kf[K_POINT_PREP] = A * 300 + Pn * 200;
@@ -948,7 +873,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         kb[K_CHOL] = 2 * env_bytes + 3 * npad * 8.0;
         kf[K_CHOL] = 0;
         for (int k = 0; k < nb; ++k) {
-            const double r = rptr[k + 1] - rptr[k];
+            const double r = pl.rptr[k + 1] - pl.rptr[k];
             kf[K_CHOL] += (r * (r + 1) / 2) * 2.0 * 16 * 16 * 16 + r * 16 * 16 * 16 + 16 * 16 * 16 / 3.0;
         }
         if (P.solver == 2) {
@@ -991,6 +916,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step
         kf[K_LIN_POINT] = kf[K_CAM_SIDE] + kf[K_POINT_PREP];
     }
+    if (std::getenv("MIBA_PREP_TIMES"))  // diagnostic: host phases of ba_prepare (the device work is still in flight)
+        std::fprintf(stderr, "prepare: raw staging %.3f ms, plan %.3f ms, plan staging + enqueue %.3f ms (%d host threads)\n",
+                     tp_raw - tp0, tp_plan - tp_raw, now_ms() - tp_plan, host_threads());
     return BA_OK;
 }
 
@@ -1029,14 +957,44 @@ static void print_row(int it, double cost, double dc, double g, double st, doubl
     std::fflush(stdout);
 }
 
+// The spin bound is a per-device global of the BCR module: remembered per device, set under the context's
+// device (the caller has made it current), serialised across contexts / threads.
 static int apply_spin_limit(ba_context* ctx) {
-    static unsigned applied = 0;
+    static std::mutex mu;
+    static std::vector<unsigned> applied;  // per device; 0 = not yet set
     const char* e = std::getenv("MIBA_BCR_SPIN_LIMIT");  // tests: force the hand-off timeout path
-    const unsigned want = e ? (unsigned)std::strtoul(e, nullptr, 10) : (1u << 22);
-    if (want != applied) {
+    unsigned want = e ? (unsigned)std::strtoul(e, nullptr, 10) : (1u << 22);
+    if (want == 0) want = 1;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)applied.size() <= ctx->device) applied.resize(ctx->device + 1, 0u);
+    if (applied[ctx->device] != want) {
         HIPCHECK(ctx, bcr_set_spin_limit(want));
-        applied = want;
+        applied[ctx->device] = want;
     }
+    return BA_OK;
+}
+
+// A hand-off of the resident BCR kernel timed out (its workgroups were not all co-resident: another context
+// or process held CUs). The decision stopped the device loop without a termination and without counting the
+// iteration (x, radius and the trust-region state untouched): from now on this context runs the per-level
+// launches (no inter-workgroup waits), and the host re-enqueues the iteration. The in-flight iterations behind
+// the decision were no-ops. S / rhs were cleared for the next assembly by that iteration's own kernels.
+static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
+    hipStream_t s = ctx->stream;
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    BcrWork& Bw = ctx->W.bcr;
+    Bw.persist = 0;
+    ctx->bcr_fallback = true;
+    if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
+    S.done = 0;
+    S.termination = -1;
+    S.msg = MSG_NONE;
+    static thread_local LmState h_retry;
+    h_retry = S;
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->W.st, &h_retry, sizeof(LmState), hipMemcpyHostToDevice, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    if (ctx->hprog) __atomic_store_n(ctx->hprog, (unsigned)S.n_decide, __ATOMIC_RELEASE);
+    ++ctx->bcr_retries;
     return BA_OK;
 }
 
@@ -1078,6 +1036,7 @@ extern "C" int32_t ba_solve_prepared(ba_context* ctx, ba_problem* p, ba_summary*
 
 static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, double t0) {
     std::memset(sum, 0, sizeof(*sum));
+    ctx->err.clear();  // ba_last_error() describes this solve from here on
     const ba_options& o = ctx->opts;
     Prof* pf = ctx->pf();
     DevProblem& P = ctx->P;
@@ -1089,6 +1048,10 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     W.log = ctx->buf[B_LOG].as<double>();
     static thread_local LmState h_state;  // host staging (outlives the async copies)
     h_state = fresh_state(o, o.initial_trust_region_radius);
+    // the split BCR kernel's flags hold 4 * epoch + panel (one epoch per launch): re-initialise the hand-off
+    // state long before 4 * epoch wraps (2^30 launches) on a context that re-solves one prepared window forever
+    if (P.solver == 2 && ctx->bcr_launches > (1ull << 28))
+        if (int rc = bcr_init_handoffs(ctx)) return rc;
     // start from the parameters of the last ba_prepare() (device-to-device) and a fresh state
     HIPCHECK(ctx, launch_reset(P, W, h_state, ctx->buf[B_CAMS_INIT].as<double>(), ctx->buf[B_PTS_INIT].as<double>(),
                                ctx->buf[B_K_INIT].as<double>(), p->n_cams, ctx->dev_np, s));
@@ -1117,16 +1080,15 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
 
     // fused path: S and rhs, the atomic targets of the first assembly (later ones are zeroed in-loop), were
     // zeroed by k_reset
-    // IterationZero: cost, gradient, column norms -> Jacobi scale, |x| (the small-window kernel does its own)
-    if (!W.sm.on) {
-        HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
-        HIPCHECK(ctx, launch_scale(P, C, o.jacobi_scaling, W, s, pf));
-        HIPCHECK(ctx, launch_init_state(P, W, ctx->hprog ? ctx->dprog : nullptr, s, pf));
-    }
+    // IterationZero: cost, gradient, column norms -> Jacobi scale, |x|
+    HIPCHECK(ctx, launch_linearize(P, C, 0, W, s, pf));
+    HIPCHECK(ctx, launch_scale(P, C, o.jacobi_scaling, W, s, pf));
+    HIPCHECK(ctx, launch_init_state(P, W, ctx->hprog ? ctx->dprog : nullptr, s, pf));
     // LM iterations: fixed launch sequence, device-side decisions; the host follows the device.
     // Iterations enqueued after the termination are no-ops (their kernels exit at once).
     int launched = 0;
     int batch = 2;
+    int retries = 0;  // decisions that re-ran an iteration after a BCR hand-off timeout (not LM iterations)
     LmState& S = h_state;
     const bool shard = W.comm.on();
     auto launch_iter = [&]() -> int {
@@ -1134,18 +1096,15 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         HIPCHECK(ctx, launch_build(P, C, W, s, pf));
         HIPCHECK(ctx, launch_factor(P, C, W, s, pf));
         HIPCHECK(ctx, launch_update(P, C, prm, W, s, pf));
+        if (P.solver == 2 && W.bcr.persist >= 2) ++ctx->bcr_launches;
         ++launched;
         return BA_OK;
     };
-    if (W.sm.on) {
-        // small window: iteration 0 and the whole LM loop in one launch (ba_small.hip)
-        LmParams ps = prm;
-        ps.progress = nullptr;
-        HIPCHECK(ctx, launch_small(P, C, ps, o.jacobi_scaling, W, s, pf));
-        HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
-        HIPCHECK(ctx, hipStreamSynchronize(s));
-        flush_prof(ctx);
-    } else if (!pf && ctx->hprog) {
+    // at most max_iter + 1 iterations can run (max_iter steps, then the terminal re-linearisation of the
+    // stop_next iteration), plus one per re-run iteration
+    auto launch_cap = [&]() { return max_iter + 1 + retries; };
+    auto is_retry = [](const LmState& st) { return st.done && st.msg == MSG_TIMEOUT && st.termination < 0; };
+    if (!pf && ctx->hprog) {
         // Unprofiled: keep LM_AHEAD iterations in flight and follow the device through the host-mapped
         // progress word (n_decide | done << 31, written by every decision and by a failed initial
         // evaluation) instead of synchronising the stream per batch: the GPU never waits for the host.
@@ -1156,57 +1115,69 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
         // issued every 256 spins.)
         constexpr int LM_AHEAD = 2;
         volatile unsigned* hp = ctx->hprog;
-        unsigned w = 0, w_seen = ~0u;
-        auto t_seen = std::chrono::steady_clock::now();
         for (;;) {
-            w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
-            if (w >> 31) break;
-            const auto t_now = std::chrono::steady_clock::now();
-            if (w != w_seen) { w_seen = w; t_seen = t_now; }
-            // at most max_iter + 1 iterations can run (max_iter steps, then the terminal re-linearisation of the
-            // stop_next iteration): no look-ahead launch past that one
-            if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD && launched < max_iter + 1) {
-                if (int rc = launch_iter()) return rc;
-            } else if (t_now - t_seen > std::chrono::milliseconds(2)) {
-                t_seen = t_now;
-                const hipError_t q = hipStreamQuery(s);
-                if (q == hipSuccess) {  // idle: re-read the word once (it is written before the kernel ends)
-                    w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
-                    break;
+            unsigned w = 0, w_seen = ~0u;
+            auto t_seen = std::chrono::steady_clock::now();
+            for (;;) {
+                w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
+                if (w >> 31) break;
+                const auto t_now = std::chrono::steady_clock::now();
+                if (w != w_seen) { w_seen = w; t_seen = t_now; }
+                // no look-ahead launch past the last iteration that can run
+                if (launched - (int)(w & 0x7fffffffu) < LM_AHEAD && launched < launch_cap()) {
+                    if (int rc = launch_iter()) return rc;
+                } else if (t_now - t_seen > std::chrono::milliseconds(2)) {
+                    t_seen = t_now;
+                    const hipError_t q = hipStreamQuery(s);
+                    if (q == hipSuccess) {  // idle: re-read the word once (it is written before the kernel ends)
+                        w = __atomic_load_n(hp, __ATOMIC_ACQUIRE);
+                        break;
+                    }
+                    if (q != hipErrorNotReady) HIPCHECK(ctx, q);
+                    std::this_thread::yield();
+                } else {
+                    std::this_thread::yield();
                 }
-                if (q != hipErrorNotReady) HIPCHECK(ctx, q);
-                std::this_thread::yield();
-            } else {
-                std::this_thread::yield();
             }
-        }
-        // Landmark shards: every iteration issues collectives, so every rank must enqueue the same number
-        // of iterations. The decisions are identical on all ranks; the host has enqueued between d and
-        // d + LM_AHEAD - 1 iterations when it sees the terminating decision d: pad to d + LM_AHEAD - 1.
-        if (shard && (w >> 31)) {
-            const int target = std::min((int)(w & 0x7fffffffu) + LM_AHEAD - 1, max_iter + 1);
-            while (launched < target)
-                if (int rc = launch_iter()) return rc;
-        }
-        if (w >> 31) {  // the terminal state was stored to the host-mapped block before the done bit
-            std::memcpy(&S, reinterpret_cast<const char*>(ctx->hprog) + PROG_STATE_OFF, sizeof(LmState));
-        } else {
-            HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
-            HIPCHECK(ctx, hipStreamSynchronize(s));
+            // Landmark shards: every iteration issues collectives, so every rank must enqueue the same number
+            // of iterations. The decisions are identical on all ranks; the host has enqueued between d and
+            // d + LM_AHEAD - 1 iterations when it sees the terminating (or re-run) decision d: pad to
+            // d + LM_AHEAD - 1.
+            if (shard && (w >> 31)) {
+                const int target = std::min((int)(w & 0x7fffffffu) + LM_AHEAD - 1, launch_cap());
+                while (launched < target)
+                    if (int rc = launch_iter()) return rc;
+            }
+            if (w >> 31) {  // the terminal state was stored to the host-mapped block before the done bit
+                std::memcpy(&S, reinterpret_cast<const char*>(ctx->hprog) + PROG_STATE_OFF, sizeof(LmState));
+            } else {
+                HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
+                HIPCHECK(ctx, hipStreamSynchronize(s));
+            }
+            if (!is_retry(S)) break;
+            if (int rc = bcr_timeout_retry(ctx, S)) return rc;
+            ++retries;
+            launched = S.n_decide;  // every enqueued iteration has run (the ones behind the decision as no-ops)
         }
     }
     // profiled (HIP events around every launch) or no host-mapped word: batches of iterations, one
     // stream synchronisation per batch (the same batch sizes on every landmark shard)
     for (; !S.done;) {
-        for (int i = 0; i < batch && launched <= max_iter + 1; ++i)
+        for (int i = 0; i < batch && launched <= launch_cap(); ++i)
             if (int rc = launch_iter()) return rc;
         HIPCHECK(ctx, hipMemcpyAsync(&S, W.st, sizeof(LmState), hipMemcpyDeviceToHost, s));
         HIPCHECK(ctx, hipStreamSynchronize(s));
         flush_prof(ctx);
-        if (S.done || launched > max_iter + 1) break;
+        if (is_retry(S)) {
+            if (int rc = bcr_timeout_retry(ctx, S)) return rc;
+            ++retries;
+            launched = S.n_decide;
+            continue;
+        }
+        if (S.done || launched > launch_cap()) break;
         batch = std::min(batch * 2, 8);
     }
-    if (!S.done) {  // cannot happen (max_iter bounds the loop); report defensively
+    if (!S.done || S.msg == MSG_TIMEOUT) {  // cannot happen (max_iter bounds the loop; timeouts are re-run)
         ctx->err = "LM loop did not terminate";
         return BA_E_INTERNAL;
     }
@@ -1248,19 +1219,10 @@ static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, d
     const double t1 = now_ms();
     sum->time_lm_ms = t1 - tl0;
     sum->time_total_ms = t1 - t0;
-    if (S.msg == MSG_TIMEOUT) {
-        // loud failure: the resident BCR kernels' workgroups were not all co-resident (another context or
-        // process held CUs). The flags of the aborted hand-offs are stale: clear them, and run the
-        // per-level launches (no inter-workgroup waits) for every later solve of this context.
-        BcrWork& Bw = W.bcr;
-        if (P.solver == 2 && Bw.flags)
-            HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
-        HIPCHECK(ctx, hipStreamSynchronize(s));
-        Bw.persist = 0;
-        ctx->bcr_fallback = true;
-        ctx->err = std::string(sum->message) + " The context falls back to the per-level BCR launches.";
-        return BA_E_INTERNAL;
-    }
+    if (retries)  // informational (rc stays BA_OK): ba_last_error() says why the context left the resident kernel
+        ctx->err = std::to_string(retries) + " LM iteration(s) re-run with the per-level BCR launches after an "
+                   "inter-workgroup hand-off of the resident BCR kernel timed out; the context keeps the per-level "
+                   "launches from now on.";
     auto dk = [&](int k) { return ctx->k_ms[k] - kms0[k]; };
     sum->time_linearize_ms = dk(K_CAM_SIDE) + dk(K_LIN_FINALIZE) + dk(K_POINT_COLNORM) + dk(K_SCALE);
     sum->time_schur_ms = dk(K_MEMSET_S) + dk(K_ASSEMBLE) + dk(K_POINT_PREP) + dk(K_SCHUR_TILE) + dk(K_OBS_PAIRS);
@@ -1303,7 +1265,7 @@ extern "C" int32_t ba_debug_linearize(ba_context* ctx, const ba_problem* p, doub
     if (jpt) std::memset(jpt, 0, sizeof(double) * 9 * no);
     if (jint) std::memset(jint, 0, sizeof(double) * 8 * no);
     for (size_t q = 0; q < na; ++q) {
-        const size_t k = ctx->po_orig[q];
+        const size_t k = ctx->plan.po_orig[q];
         if (res) std::memcpy(res + 3 * k, &r[3 * q], sizeof(double) * 3);
         if (jcam) std::memcpy(jcam + 18 * k, &jc[18 * q], sizeof(double) * 18);
         if (jpt) std::memcpy(jpt + 9 * k, &jp[9 * q], sizeof(double) * 9);
@@ -1369,7 +1331,9 @@ extern "C" int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, i
     int n = 0;
     for (int k = 0; k < K_COUNT && n < max_n; ++k, ++n) {
         std::memset(&out[n], 0, sizeof(ba_kernel_stat));
-        std::snprintf(out[n].name, sizeof(out[n].name), "%s", kKernelNames[k]);
+        // the resident BCR id times whichever resident kernel the window runs: name it after that kernel
+        const char* nm = (k == K_BCR_PERSIST && ctx->W.bcr.persist >= 2) ? "bcr_split" : kKernelNames[k];
+        std::snprintf(out[n].name, sizeof(out[n].name), "%s", nm);
         out[n].launches = ctx->k_launches[k];
         out[n].total_ms = ctx->k_ms[k];
         out[n].bytes_per_launch = ctx->k_bytes[k];

@@ -65,6 +65,10 @@ class Solver:
             msg = (self._L.ba_last_error(self._h) or b"").decode()
             raise MibaError(f"{what} failed ({rc}): {msg}")
 
+    def last_error(self) -> str:
+        """ba_last_error() of this context: the error of the last failed call, or a note of the last solve."""
+        return (self._L.ba_last_error(self._h) or b"").decode()
+
     def solve(self, prob: ProblemArrays) -> dict:
         s = BaSummary()
         ps = prob.struct()

@@ -90,12 +90,8 @@ typedef struct ba_options {
                                 over all shards is gathered onto every rank at ba_prepare and solved there
                                 alone (no per-iteration collectives, deterministic mode), each rank keeping
                                 its own points; 0 = always run the sharded exchange. Default 262144 */
-    int32_t small_window;    /* 1 = windows with <= 15 active cameras and <= 32768 admissible observations run
-                                the single-workgroup solve (BA_LS_SMALL: iteration 0 and every LM iteration in
-                                one launch, reduced system in LDS, bitwise reproducible); 0 (default) = the
-                                multi-launch path, which measured faster (C1: 84 vs 127 us per LM iteration:
-                                one workgroup cannot hide the L2 latency of the dependent per-point chains).
-                                Landmark-sharded contexts never take it */
+    int32_t small_window;    /* ignored: kept for layout compatibility (the round-2 single-workgroup small-window
+                                kernel measured slower than the multi-launch path and was removed) */
     int32_t reserved[2];
 } ba_options;
 
@@ -123,7 +119,6 @@ typedef struct ba_problem {
 #define BA_LS_DENSE 0 /* dense-envelope LDS Cholesky */
 #define BA_LS_BAND 1  /* banded LDS Cholesky (6x6 block band <= 6) */
 #define BA_LS_BCR 2   /* block cyclic reduction over 64-dof camera blocks */
-#define BA_LS_SMALL 3 /* small window: the whole solve in one workgroup, dense reduced system in LDS */
 
 typedef struct ba_summary {
     double initial_cost;
@@ -136,7 +131,7 @@ typedef struct ba_summary {
     int32_t num_active_cams;
     int32_t num_active_points;
     int32_t reduced_system_size;    /* 6*active_cams + 4 */
-    int32_t linear_solver;          /* reduced-system solver used: BA_LS_DENSE / _BAND / _BCR / _SMALL */
+    int32_t linear_solver;          /* reduced-system solver used: BA_LS_DENSE / _BAND / _BCR */
     int32_t camera_band;            /* max |cam_a - cam_b| over coupled active cameras */
     double time_setup_ms;           /* host prep + H2D + structure build */
     double time_lm_ms;              /* LM loop wall time (device work + host control) */
@@ -159,6 +154,8 @@ void ba_default_options(ba_options* opts);
 typedef struct ba_context ba_context;
 ba_context* ba_create(const ba_options* opts);
 void ba_destroy(ba_context* ctx);
+/* Text of the context's last failed call; after a successful ba_solve / ba_solve_prepared it is empty, or a
+ * note (e.g. LM iterations re-run with the per-level BCR launches after a resident-kernel hand-off timeout). */
 const char* ba_last_error(const ba_context* ctx);
 /* Replace the solver options of a live context (device buffers are kept;
  * opts->device must equal the context's device or be -1). */

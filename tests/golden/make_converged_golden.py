@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/{c4,c5}_oracle.json: converged-solve fixtures of the CPU oracle
-(TEST INFRASTRUCTURE) on BASELINE.json's headline windows, for the -m gpu parity tests
+"""Generate tests/golden/{c3,c4,c5}_oracle.json: converged-solve fixtures of the CPU oracle
+(TEST INFRASTRUCTURE) on BASELINE.json's windows, for the -m gpu parity tests
 (tests/test_converged_parity.py).
 
+- C3 (50 cams / 4k points / 8k obs, synthetic.make_config("C3"), the stand-in for BASELINE
+  configs[2]'s 50-keyframe fr2/desk window): the reference's solver settings, to termination
+  (every point seen by 2 keyframes, so most residuals sit in the Huber linear zone and the solve
+  runs to max_num_iterations = 75).
 - C4 (200 cams / 100k points / 1M obs, synthetic.make_config("C4")): the reference's own
   solver settings, i.e. ceres::Solve run to termination with the default tolerances and
   max_num_iterations = 75 (/root/reference/src/OptimizationUtils.cpp:300,
@@ -14,7 +18,7 @@ Checker configuration of the oracle: 1 thread (fixed summation order); C4 uses t
 reduced-camera Cholesky, C5 the co-visibility profile Cholesky (same factorisation, fill
 confined to the envelope; the dense 5998^2 system is too slow to iterate on a CPU).
 
-Run from the repository root:  python tests/golden/make_converged_golden.py [C4] [C5]
+Run from the repository root:  python tests/golden/make_converged_golden.py [C3] [C4] [C5]
 """
 from __future__ import annotations
 
@@ -33,6 +37,7 @@ from oracle import oracle  # noqa: E402
 
 NO_TOL = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
 SPECS = {
+    "C3": dict(profile=False, options={}),
     "C4": dict(profile=False, options={}),
     "C5": dict(profile=True, options=dict(max_num_iterations=12, **NO_TOL)),
 }

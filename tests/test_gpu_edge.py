@@ -1,8 +1,11 @@
 """Edge cases of the C-ABI on the GPU: a non-finite initial evaluation (Ceres FAILURE with
 "Residual and Jacobian evaluation failed.", rc 0, no hang of the progress-word loop), windows
 without any admissible observation (only the IntrinsicsPrior block, OptimizationUtils.cpp:236-241,
-solved like Ceres), and a forced inter-workgroup hand-off timeout of the resident BCR kernel
-(loud BA_E_INTERNAL, then a per-level-launch fallback that still matches the oracle)."""
+solved like Ceres), a forced inter-workgroup hand-off timeout of the resident BCR kernel (the
+iteration is re-run with the per-level launches inside the same solve: BA_OK, oracle parity), and
+two contexts solving concurrently on one GPU."""
+import threading
+
 import numpy as np
 import pytest
 
@@ -65,21 +68,55 @@ def test_window_without_admissible_observations_solves_the_prior(kind):
     np.testing.assert_array_equal(p.cams, cams0)  # no residual on any pose
 
 
-def test_bcr_handoff_timeout_is_loud_then_falls_back(monkeypatch):
-    from miba.solver import MibaError
+def test_bcr_handoff_timeout_reruns_the_iteration_in_the_same_solve(monkeypatch):
     p = synthetic.make_config("C2")
-    with _solver(max_num_iterations=5) as s:
-        monkeypatch.setenv("MIBA_BCR_SPIN_LIMIT", "1")
-        with pytest.raises(MibaError, match="timed out"):
-            s.solve(p.copy())
-        monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
-        q = p.copy()
-        sg = s.solve(q)  # per-level launches from now on
-    assert sg["linear_solver"] == 2
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=5))
-    assert sg["num_iterations"] == so["num_iterations"]
-    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sg, so)
+    with _solver(max_num_iterations=5) as s:
+        monkeypatch.setenv("MIBA_BCR_SPIN_LIMIT", "1")  # every inter-workgroup wait times out at once
+        q = p.copy()
+        sg = s.solve(q)  # BA_OK: the first iteration's reduced solve re-runs with the per-level launches
+        note = s.last_error()
+        monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
+        q2 = p.copy()
+        sg2 = s.solve(q2)  # the context keeps the per-level launches
+    assert "re-run with the per-level BCR launches" in note, note
+    for g in (sg, sg2):
+        assert g["linear_solver"] == 2
+        assert g["termination"] == so["termination"]
+        assert g["num_iterations"] == so["num_iterations"]
+        assert g["num_successful_steps"] == so["num_successful_steps"]
+        assert abs(g["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (g, so)
+    np.testing.assert_allclose(q.cams, q2.cams, rtol=0, atol=1e-12)
     # a fresh context uses the resident kernels again (the spin limit is back to its default)
     with _solver(max_num_iterations=5) as s2:
-        sg2 = s2.solve(p.copy())
-    assert abs(sg2["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+        sg3 = s2.solve(p.copy())
+        assert s2.last_error() == ""
+    assert abs(sg3["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+
+
+def test_two_contexts_solve_concurrently_on_one_gpu():
+    """Two host threads, one context each, solving C2 windows at the same time on GPU 0: both resident BCR
+    grids and every other launch share the device; both solves return BA_OK and match the oracle."""
+    probs = [synthetic.make_config("C2"), synthetic.make_config("C2", seed=12)]
+    want = [oracle.solve(p.copy()) for p in probs]
+    out, errs = [None, None], []
+
+    def run(k):
+        try:
+            with _solver() as s:
+                for _ in range(3):  # overlapping solves, not one after the other
+                    q = probs[k].copy()
+                    out[k] = (s.solve(q), q)
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    for (sg, q), so in zip(out, want):
+        assert sg["termination"] == so["termination"], (sg, so)
+        assert sg["num_iterations"] == so["num_iterations"]
+        assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)

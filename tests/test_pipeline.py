@@ -46,7 +46,9 @@ def test_pipeline_global_ba_schedule():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,n_kf,wsize,freq", [(0, 36, 10, 10), (3, 64, 20, 10)])
+# (5, 90, 50, 10): BASELINE configs[2]'s sliding window — window_size = 50 > frame_frequency = 10
+# (BundleAdjustmentConfig.h:52-53, main.cpp:163-168): windows (0,49), (10,59), ..., (40,89)
+@pytest.mark.parametrize("seed,n_kf,wsize,freq", [(0, 36, 10, 10), (3, 64, 20, 10), (5, 90, 50, 10)])
 def test_pipeline_gpu_matches_oracle_ate_rpe(seed, n_kf, wsize, freq):
     from miba.solver import Solver
     with Solver() as s:
@@ -54,6 +56,8 @@ def test_pipeline_gpu_matches_oracle_ate_rpe(seed, n_kf, wsize, freq):
     _, txt_c, summ_c, K_c = _run(_oracle_solve(), seed=seed, n_keyframes=n_kf, window_size=wsize,
                                  frame_frequency=freq)
     assert [(a, b) for a, b, _ in summ_g] == [(a, b) for a, b, _ in summ_c]
+    if wsize == 50:
+        assert [(a, b) for a, b, _ in summ_c] == [(0, 49), (10, 59), (20, 69), (30, 79), (40, 89)]
     for (_, _, sg), (_, _, sc) in zip(summ_g, summ_c):
         assert abs(sg["final_cost"] - sc["final_cost"]) <= 1e-6 * sc["final_cost"]
     eg, ec = evaluate.ate(gt, txt_g), evaluate.ate(gt, txt_c)
