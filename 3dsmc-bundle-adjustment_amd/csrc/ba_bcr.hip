@@ -2061,15 +2061,15 @@ static inline int n_elim(int nblk, int m) {
         CKB(hipGetLastError());           \
     } while (0)
 
-// k_bcr_split as a cooperative launch: its workgroups wait on each other, so the grid must be co-resident,
-// and a cooperative launch refuses a grid that cannot be (hipErrorCooperativeLaunchTooLarge) instead of
-// letting it run into the hand-off timeouts. MIBA_BCR_COOP=0: an ordinary launch (same kernel).
+// k_bcr_split's workgroups wait on each other, so the grid must be co-resident. MIBA_BCR_COOP=1 launches it
+// cooperatively: the runtime then refuses a grid that cannot be (hipErrorCooperativeLaunchTooLarge -> the
+// per-level launches) instead of letting it run into the hand-off timeouts. Off by default: on MI355X
+// (ROCm 7.2) the cooperative launch of the C4 grid costs ~20 us more per launch (k_bcr_split 108.5 -> 129 us,
+// C4 3719 -> 3359 LM it/s, same-box A/B, profiles/r03_ab_coop_c4.txt); the default relies on the bounded
+// hand-off waits, whose timeout re-runs the iteration with the per-level launches inside the same solve.
 static bool bcr_coop() {
-    static const int on = [] {
-        const char* e = getenv("MIBA_BCR_COOP");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return on != 0;
+    const char* e = getenv("MIBA_BCR_COOP");  // read per launch (tests switch it inside one process)
+    return e && e[0] == '1';
 }
 template <bool STAMP, int NH>
 static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,

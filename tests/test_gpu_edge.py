@@ -120,3 +120,17 @@ def test_two_contexts_solve_concurrently_on_one_gpu():
         assert sg["termination"] == so["termination"], (sg, so)
         assert sg["num_iterations"] == so["num_iterations"]
         assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
+
+
+def test_cooperative_bcr_launch_matches_oracle(monkeypatch):
+    """MIBA_BCR_COOP=1: k_bcr_split as a cooperative launch (the runtime refuses a grid that cannot be co-resident;
+    off by default, it costs ~20 us per launch on MI355X). Same arithmetic: the solve matches the oracle."""
+    monkeypatch.setenv("MIBA_BCR_COOP", "1")
+    p = synthetic.make_config("C2")
+    so = oracle.solve(p.copy())
+    with _solver() as s:
+        sg = s.solve(p.copy())
+        assert s.last_error() == ""
+    assert sg["linear_solver"] == 2
+    assert sg["num_iterations"] == so["num_iterations"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
