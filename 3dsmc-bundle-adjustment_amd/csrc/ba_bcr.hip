@@ -1367,7 +1367,10 @@ __device__ __forceinline__ HelperMap helper_map(int role, int wave, bool root) {
     return h;
 }
 
-template <bool STAMP, int NH>
+// DEFER: the helpers' Schur contributions are formed once after the last panel (16-deep MFMA chains over the
+// finished X in LDS) instead of per row block inside the panel loop, so the panel loop (panel loads + X update)
+// keeps the factor workgroup's pace instead of falling behind it by ~0.8 us per panel.
+template <bool STAMP, int NH, bool DEFER>
 __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__ st, DevProblem P,
                                                      const double* __restrict__ S, double* __restrict__ rhs,
                                                      BcrWork Bw, int* __restrict__ flag,
@@ -1407,11 +1410,22 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     if (role == 0) {
         // ================= F: D_i, pivot side of the factorization
         FLds& L = *reinterpret_cast<FLds*>(smem);
+        {
+            // every load issued before the first LDS store (clamped addresses, selects after): the level-0
+            // factorization starts one memory round trip after the launch, not eight
+            double dv[NQ];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-            const bool ok = c <= r && r < G_DOF && b0 + r < nd;
-            L.T[r * BLD + c] = ok ? S[(size_t)(b0 + r) * ld + b0 + c] : (r == c ? 1.0 : 0.0);
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+                const bool ok = c <= r && r < G_DOF && b0 + r < nd;
+                dv[q] = S[ok ? (size_t)(b0 + r) * ld + b0 + c : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
+                const bool ok = c <= r && r < G_DOF && b0 + r < nd;
+                L.T[r * BLD + c] = ok ? dv[q] : (r == c ? 1.0 : 0.0);
+            }
         }
         if (tid < 12) L.sync[tid] = 0;
         {  // the next epoch's panel slot starts empty (the entries a panel writes: lower tiles, W, 1/diag)
@@ -1576,33 +1590,56 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
         for (int q = 0; q < NQ; ++q) nf[tid + TPB_E * q] = BCR_Y_EMPTY;
     }
+    // level-0 inputs: every global load issued before the first LDS store (clamped addresses, selects after)
+    double bkv = 0.0;
     if (root && tid < 14) {  // border inputs [b_k | S_kk packed]
         int q = tid - 4, mm = 0;
         while (q > mm) { q -= mm + 1; ++mm; }
-        L.bk[tid] = tid < 4 ? rhs[P.kb + tid] : S[(size_t)(P.kb + mm) * ld + P.kb + q];
+        bkv = tid < 4 ? rhs[P.kb + tid] : S[(size_t)(P.kb + mm) * ld + P.kb + q];
     }
     {
         const bool has_r0 = i + 1 < nblk;
+        constexpr int NQX = (NH == 1 ? 2 : 1) * NQ;
+        double xv[NQX];
         if (mi == 0) {
+            // straight-line: the role picks the address (a select, no branch), so the loads stay in flight together
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-                if (NH == 1 || roleA) {
-                    const bool okl = i >= 1 && r < G_DOF && b0 + r < nd && c < G_DOF;
-                    L.X[r * XW + c] = okl ? S[(size_t)(b0 + r) * ld + b0 - G_DOF + c] : 0.0;
-                }
-                if (NH == 1 || roleB) {
-                    const int b1 = b0 + G_DOF;
-                    const bool okr = has_r0 && r < G_DOF && b1 + r < nd && c < G_DOF;
-                    L.X[c * XW + BB + r] = okr ? S[(size_t)(b1 + r) * ld + b0 + c] : 0.0;
+                const int b1 = b0 + G_DOF;
+                const bool okl = i >= 1 && r < G_DOF && b0 + r < nd && c < G_DOF;
+                const bool okr = has_r0 && r < G_DOF && b1 + r < nd && c < G_DOF;
+                const size_t al = okl ? (size_t)(b0 + r) * ld + b0 - G_DOF + c : 0;
+                const size_t ar = okr ? (size_t)(b1 + r) * ld + b0 + c : 0;
+                if constexpr (NH == 1) {
+                    xv[q] = S[al];
+                    xv[NQ + q] = S[ar];
+                } else {
+                    xv[q] = S[roleA ? al : ar];
                 }
             }
         }
         const int r = tid >> 3, c = tid & 7, gr = b0 + r;
-        double rv = 0.0;
-        if (r < G_DOF && gr < nd) rv = c == 0 ? rhs[gr] : (c <= 4 ? S[(size_t)(P.kb + c - 1) * ld + gr] : 0.0);
+        const bool rok = r < G_DOF && gr < nd && c <= 4;
+        double rv = rok ? (c == 0 ? rhs[gr] : S[(size_t)(P.kb + c - 1) * ld + gr]) : 0.0;
+        if (mi == 0) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int e = tid + TPB_E * q, rq = e >> 6, cq = e & 63;
+                if (NH == 1 || roleA) {
+                    const bool okl = i >= 1 && rq < G_DOF && b0 + rq < nd && cq < G_DOF;
+                    L.X[rq * XW + cq] = okl ? xv[q] : 0.0;
+                }
+                if (NH == 1 || roleB) {
+                    const int b1 = b0 + G_DOF;
+                    const bool okr = has_r0 && rq < G_DOF && b1 + rq < nd && cq < G_DOF;
+                    L.X[cq * XW + BB + rq] = okr ? xv[NQX - NQ + q] : 0.0;
+                }
+            }
+        }
         L.X[r * XW + 2 * BB + c] = rv;
     }
+    if (root && tid < 14) L.bk[tid] = bkv;
     for (int m = 0; m < mi; ++m) {
         const int s = 1 << m, a = i - s, b = i + s;
         const bool last = m == mi - 1 && !root;
@@ -1708,6 +1745,30 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     d4b cacc[NCT8];
 #pragma unroll
     for (int q = 0; q < NCT8; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
+    // Schur contributions of the finished X row block kbk: operands of every tile first, then interleaved chains
+    auto contrib_rows = [&](int kbk) {
+        double av[NCT8][4], bv[NCT8][4];
+#pragma unroll
+        for (int q = 0; q < NCT8; ++q) {
+            const int t = hm.tiles[q];
+            const ContribTile ct = contrib_tile(t < 0 ? 0 : t, has_r);
+            const bool on = t >= 0 && ct.valid;
+            const bool bok = on && (!ct.rhs || rr < RC);
+            const bool aok = on && (!ct.gram || rr < RC);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const double* row = L.X + (16 * kbk + 4 * s4 + kk) * XW;
+                av[q][s4] = aok ? row[ct.aoff + 16 * ct.ib + rr] : 0.0;
+                bv[q][s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int q = 0; q < NCT8; ++q)
+                if (hm.tiles[q] >= 0)
+                    cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][s4], bv[q][s4], cacc[q], 0, 0, 0);
+    };
     // NH = 2: helper A stores its finished XL row block kb (sc1) during its X update of panel kb and
     // raises xl_f = 4 epoch + 3 with its contributions; helper B, after publishing its own
     // contributions, loads all of XL (its back-substitution needs it) and, when the block has a right
@@ -1845,33 +1906,15 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                 for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + 2 * BB + rr] = acc[g];
         }
-        if (!root) {  // contributions of row block kb: operands of every tile first, then interleaved chains
-            double av[NCT8][4], bv[NCT8][4];
-#pragma unroll
-            for (int q = 0; q < NCT8; ++q) {
-                const int t = hm.tiles[q];
-                const ContribTile ct = contrib_tile(t < 0 ? 0 : t, has_r);
-                const bool on = t >= 0 && ct.valid;
-                const bool bok = on && (!ct.rhs || rr < RC);
-                const bool aok = on && (!ct.gram || rr < RC);
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    const double* row = L.X + (16 * kb + 4 * s4 + kk) * XW;
-                    av[q][s4] = aok ? row[ct.aoff + 16 * ct.ib + rr] : 0.0;
-                    bv[q][s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
-                }
-            }
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-                for (int q = 0; q < NCT8; ++q)
-                    if (hm.tiles[q] >= 0)
-                        cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][s4], bv[q][s4], cacc[q], 0, 0, 0);
-        }
+        if (!root && !DEFER && !(Bw.diag & 1)) contrib_rows(kb);
         if constexpr (STAMP) __syncthreads();
         TLS(3 + 2 * kb);
     }
     __syncthreads();
+    if (DEFER && !root) {
+#pragma unroll
+        for (int kbk = 0; kbk < 4; ++kbk) contrib_rows(kbk);
+    }
     if (root) {
         double* Yl = L.yt;
         {
@@ -2071,13 +2114,22 @@ static bool bcr_coop() {
     const char* e = getenv("MIBA_BCR_COOP");  // read per launch (tests switch it inside one process)
     return e && e[0] == '1';
 }
+static bool bcr_defer() {  // MIBA_BCR_DEFER=1: contributions after the last panel (measured 5 us slower at C4)
+    const char* e = getenv("MIBA_BCR_DEFER");
+    return e && e[0] == '1';
+}
 template <bool STAMP, int NH>
 static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const dim3 grid((NH + 1) * Bw.nblk), block(TPB_E);
+    const bool defer = bcr_defer();
     if (!bcr_coop()) {
-        BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw, W.chol_flag,
-            stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
+        if (defer)
+            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH, true>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw,
+                W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
+        else
+            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH, false>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw,
+                W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
         return hipSuccess;
     }
     const LmState* a_st = W.st;
@@ -2095,7 +2147,8 @@ static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& 
     double* a_part = W.part;
     void* args[] = {&a_st, &a_P, &a_S, &a_rhs, &a_Bw, &a_flag, &a_tl, &a_c, &a_scale, &a_camdata, &a_lin, &a_delta, &a_part};
     if (pf) pf->begin(K_BCR_PERSIST, s);
-    const hipError_t e = hipLaunchCooperativeKernel((const void*)k_bcr_split<STAMP, NH>, grid, block, args, sizeof(HLds), s);
+    const void* fn = defer ? (const void*)k_bcr_split<STAMP, NH, true> : (const void*)k_bcr_split<STAMP, NH, false>;
+    const hipError_t e = hipLaunchCooperativeKernel(fn, grid, block, args, sizeof(HLds), s);
     if (pf) pf->end(s);
     return e;
 }
@@ -2159,14 +2212,11 @@ static hipError_t bcr_persist_attr() {
                                 (int)sizeof(PersistLds)));
         CKB(hipFuncSetAttribute((const void*)k_bcr_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(PersistLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_split<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(HLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_split<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(HLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_split<false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(HLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_split<true, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(HLds)));
+        const void* fns[] = {(const void*)k_bcr_split<false, 1, false>, (const void*)k_bcr_split<true, 1, false>,
+                             (const void*)k_bcr_split<false, 2, false>, (const void*)k_bcr_split<true, 2, false>,
+                             (const void*)k_bcr_split<false, 1, true>, (const void*)k_bcr_split<true, 1, true>,
+                             (const void*)k_bcr_split<false, 2, true>, (const void*)k_bcr_split<true, 2, true>};
+        for (const void* f : fns) CKB(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(HLds)));
         done = true;
     }
     return hipSuccess;
@@ -2181,10 +2231,10 @@ int bcr_persist_ok(int nblk) {
     int dev = 0, ncu = 0, per_cu = 0, per_cu2 = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 2>, TPB_E, sizeof(HLds)) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 2, true>, TPB_E, sizeof(HLds)) == hipSuccess &&
         per_cu2 >= 1 && 3 * nblk <= per_cu2 * ncu)
         return 3;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 1>, TPB_E, sizeof(HLds)) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 1, true>, TPB_E, sizeof(HLds)) == hipSuccess &&
         per_cu2 >= 1 && 2 * nblk <= per_cu2 * ncu)
         return 2;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist<false>, TPB_E, sizeof(PersistLds)) !=

@@ -98,6 +98,7 @@ struct DevProblem {
     int cam_band;  // max over active cameras of (camera - first co-visible camera)
     int solver;    // 0 dense envelope, 1 band, 2 block cyclic reduction
     int rank, nranks;  // landmark shard of this context (ba_comm_init); rank 0 adds the camera/intrinsics terms
+    int xcd_map;       // camera-side workgroups take the sub-segments by XCD band (xcd_seg, ba_kernels.hip)
 };
 
 // Block cyclic reduction (ba_bcr.hip): nblk blocks of BCR_CAMS cameras (64 dofs).
@@ -125,6 +126,7 @@ struct BcrWork {
     unsigned* flags;  // flags[0] (the epoch) is advanced by k_final after every BCR launch that ran
     int nblk, levels;
     int voff, vroot, vlevels;  // k_bcr_split: balanced tree on v = i + voff, root block vroot, depth vlevels + 1
+    int diag = 0;  // diagnostic (MIBA_BCR_DIAG, timing experiments only; wrong results): 1 = no helper contributions
     int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level

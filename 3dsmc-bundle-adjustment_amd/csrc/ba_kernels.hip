@@ -81,6 +81,23 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
 }
 
 // ---------------------------------------------------------------- camera side
+// XCD-aware sub-segment order: workgroup b of a launch runs on XCD b % 8 (dispatch round-robin; a placement
+// assumption for speed only, never for correctness). The camera-side workgroups [first, first + n) take the
+// sub-segments (camera-major order) so that each XCD gets one contiguous eighth of the cameras: the points a
+// camera band gathers are then cached in ONE XCD's L2 (a point is gathered by its ~10 co-visible cameras),
+// instead of every XCD fetching every point. A bijection on [0, n); each segment's partial keeps its own slot.
+__device__ __forceinline__ int xcd_seg(int b, int first, int n) {
+    const int x = b & 7, j = b - first;
+    int pre = 0;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+        const int j0 = (y - first) & 7;
+        const int cnt = j0 < n ? (n - j0 + 7) >> 3 : 0;
+        pre += y < x ? cnt : 0;
+    }
+    return pre + ((j - ((x - first) & 7)) >> 3);
+}
+
 // One workgroup per sub-segment (<= SUBSEG_OBS observations of one camera) of the
 // camera-major observation list; k_cam_finalize sums a camera's sub-segments in order.
 // camdata (per sub-segment partial here): U upper-packed (21), C (6x4 = 24), g (6)
@@ -144,7 +161,7 @@ __device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaCons
 __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
                                                   double* __restrict__ camdata, double* __restrict__ seg_intr,
                                                   double* __restrict__ gmax_word) {
-    cam_side_block(P, c, st, gated, camdata, seg_intr, gmax_word, blockIdx.x);
+    cam_side_block(P, c, st, gated, camdata, seg_intr, gmax_word, P.xcd_map ? xcd_seg(blockIdx.x, 0, P.n_seg) : (int)blockIdx.x);
 }
 
 // One launch for what follows the camera-side pass (was k_cam_reduce + k_lin_finalize):
@@ -611,7 +628,8 @@ __global__ __launch_bounds__(TPB) void k_lin_point(DevProblem P, BaConsts c, con
                                                    double* __restrict__ cpart, double* __restrict__ seg_intr,
                                                    double* __restrict__ gmax_word, int mode) {
     if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
-    else cam_side_block(P, c, st, mode, cpart, seg_intr, gmax_word, blockIdx.x - nb_pp);
+    else cam_side_block(P, c, st, mode, cpart, seg_intr, gmax_word,
+                        P.xcd_map ? xcd_seg(blockIdx.x, nb_pp, P.n_seg) : (int)blockIdx.x - nb_pp);
 }
 
 // Jacobi scale (Ceres: 1 / (1 + sqrt(squared column norm)), iteration 0 only)
@@ -1773,18 +1791,28 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
     const double* K = P.K[cur];
     const double* Kn = P.K[cur ^ 1];
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cost, bad, |x_cand|^2
+    // each thread's observation records (<= BS_OBS / TPB of them) are read once, in phase 1, and kept in
+    // registers for phase 3 (a single point with more observations re-reads its records in phase 3)
+    constexpr int NR = BS_OBS / TPB;
+    int r_cam[NR], r_ap[NR];
+    double2 r_uv[NR];
+    double r_dep[NR];
     // ---- phase 1
     double bsum[3] = {0.0, 0.0, 0.0};
-    for (int o = ob + tid; o < oe; o += TPB) {
+    int it = 0;
+    for (int o = ob + tid; o < oe; o += TPB, ++it) {
         const int ac = P.po_ac[o];
+        const int cam = P.po_cam[o], ap = P.po_ap[o];
+        const double2 uv = P.po_uv[o];
+        const double dep = P.po_depth[o];
+#pragma unroll
+        for (int k = 0; k < NR; ++k)  // register arrays: constant indices only
+            if (k == it) { r_cam[k] = cam; r_ap[k] = ap; r_uv[k] = uv; r_dep[k] = dep; }
         double v[3] = {0.0, 0.0, 0.0};
         if (ac >= 0) {
-            const int ap = P.po_ap[o];
-            const double2 uv = P.po_uv[o];
             ObsEval ev;
             double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * P.po_cam[o], P.pts[cur] + 3 * P.po_pt[o], K, uv.x, uv.y, P.po_depth[o], ev, jc,
-                    jp, jk);
+            lin_obs(c, P.cams[cur] + 7 * cam, P.pts[cur] + 3 * P.pt_idx[ap], K, uv.x, uv.y, dep, ev, jc, jp, jk);
             const double* sc = scale + 6 * ac;
             const double* yc = y + 6 * ac;
             const double* sp = scale + P.off_pt + 3 * ap;
@@ -1845,12 +1873,20 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
     __syncthreads();
     // ---- phase 3
     (void)delta;
-    for (int o = ob + tid; o < oe; o += TPB) {
-        const int cam = P.po_cam[o];
-        const int pl = P.po_ap[o] - apb;
-        const double2 uv = P.po_uv[o];
-        const double dep = P.po_depth[o];
-        const double* X = P.pts[cur] + 3 * P.po_pt[o];
+    it = 0;
+    for (int o = ob + tid; o < oe; o += TPB, ++it) {
+        int cam, ap;
+        double2 uv;
+        double dep;
+        if (it < NR) {
+#pragma unroll
+            for (int k = 0; k < NR; ++k)  // register arrays: constant indices only
+                if (k == it) { cam = r_cam[k]; ap = r_ap[k]; uv = r_uv[k]; dep = r_dep[k]; }
+        } else {
+            cam = P.po_cam[o]; ap = P.po_ap[o]; uv = P.po_uv[o]; dep = P.po_depth[o];
+        }
+        const int pl = ap - apb;
+        const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
         const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
         ObsEval en;
         eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, uv.x, uv.y, dep, en);

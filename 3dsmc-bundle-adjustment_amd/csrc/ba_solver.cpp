@@ -794,6 +794,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
         if (int rc = bcr_init_handoffs(ctx)) return rc;
         Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
+        Bw.diag = std::getenv("MIBA_BCR_DIAG") ? std::atoi(std::getenv("MIBA_BCR_DIAG")) : 0;
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
             else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
@@ -810,6 +811,10 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     W.red = shard ? ctx->buf[B_RED].as<double>() : nullptr;
     P.rank = W.comm.rank;
     P.nranks = W.comm.nranks;
+    {
+        const char* e = std::getenv("MIBA_XCD_MAP");
+        P.xcd_map = (e && e[0] == '0') ? 0 : 1;
+    }
     W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
     W.cnp = ctx->buf[B_CNP].as<double>(); W.pdata = ctx->buf[B_PDATA].as<double>();
     W.S = ctx->buf[B_S].as<double>(); W.rhs = ctx->buf[B_RHS].as<double>();
