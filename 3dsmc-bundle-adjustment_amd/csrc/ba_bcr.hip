@@ -1367,10 +1367,7 @@ __device__ __forceinline__ HelperMap helper_map(int role, int wave, bool root) {
     return h;
 }
 
-// DEFER: the helpers' Schur contributions are formed once after the last panel (16-deep MFMA chains over the
-// finished X in LDS) instead of per row block inside the panel loop, so the panel loop (panel loads + X update)
-// keeps the factor workgroup's pace instead of falling behind it by ~0.8 us per panel.
-template <bool STAMP, int NH, bool DEFER>
+template <bool STAMP, int NH>
 __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__ st, DevProblem P,
                                                      const double* __restrict__ S, double* __restrict__ rhs,
                                                      BcrWork Bw, int* __restrict__ flag,
@@ -1906,15 +1903,11 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                 for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + 2 * BB + rr] = acc[g];
         }
-        if (!root && !DEFER && !(Bw.diag & 1)) contrib_rows(kb);
+        if (!root) contrib_rows(kb);
         if constexpr (STAMP) __syncthreads();
         TLS(3 + 2 * kb);
     }
     __syncthreads();
-    if (DEFER && !root) {
-#pragma unroll
-        for (int kbk = 0; kbk < 4; ++kbk) contrib_rows(kbk);
-    }
     if (root) {
         double* Yl = L.yt;
         {
@@ -2114,22 +2107,13 @@ static bool bcr_coop() {
     const char* e = getenv("MIBA_BCR_COOP");  // read per launch (tests switch it inside one process)
     return e && e[0] == '1';
 }
-static bool bcr_defer() {  // MIBA_BCR_DEFER=1: contributions after the last panel (measured 5 us slower at C4)
-    const char* e = getenv("MIBA_BCR_DEFER");
-    return e && e[0] == '1';
-}
 template <bool STAMP, int NH>
 static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const dim3 grid((NH + 1) * Bw.nblk), block(TPB_E);
-    const bool defer = bcr_defer();
     if (!bcr_coop()) {
-        if (defer)
-            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH, true>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw,
-                W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
-        else
-            BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH, false>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw,
-                W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
+        BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw, W.chol_flag,
+            stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
         return hipSuccess;
     }
     const LmState* a_st = W.st;
@@ -2147,8 +2131,7 @@ static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& 
     double* a_part = W.part;
     void* args[] = {&a_st, &a_P, &a_S, &a_rhs, &a_Bw, &a_flag, &a_tl, &a_c, &a_scale, &a_camdata, &a_lin, &a_delta, &a_part};
     if (pf) pf->begin(K_BCR_PERSIST, s);
-    const void* fn = defer ? (const void*)k_bcr_split<STAMP, NH, true> : (const void*)k_bcr_split<STAMP, NH, false>;
-    const hipError_t e = hipLaunchCooperativeKernel(fn, grid, block, args, sizeof(HLds), s);
+    const hipError_t e = hipLaunchCooperativeKernel((const void*)k_bcr_split<STAMP, NH>, grid, block, args, sizeof(HLds), s);
     if (pf) pf->end(s);
     return e;
 }
@@ -2212,10 +2195,8 @@ static hipError_t bcr_persist_attr() {
                                 (int)sizeof(PersistLds)));
         CKB(hipFuncSetAttribute((const void*)k_bcr_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(PersistLds)));
-        const void* fns[] = {(const void*)k_bcr_split<false, 1, false>, (const void*)k_bcr_split<true, 1, false>,
-                             (const void*)k_bcr_split<false, 2, false>, (const void*)k_bcr_split<true, 2, false>,
-                             (const void*)k_bcr_split<false, 1, true>, (const void*)k_bcr_split<true, 1, true>,
-                             (const void*)k_bcr_split<false, 2, true>, (const void*)k_bcr_split<true, 2, true>};
+        const void* fns[] = {(const void*)k_bcr_split<false, 1>, (const void*)k_bcr_split<true, 1>,
+                             (const void*)k_bcr_split<false, 2>, (const void*)k_bcr_split<true, 2>};
         for (const void* f : fns) CKB(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(HLds)));
         done = true;
     }
@@ -2231,10 +2212,10 @@ int bcr_persist_ok(int nblk) {
     int dev = 0, ncu = 0, per_cu = 0, per_cu2 = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 2, true>, TPB_E, sizeof(HLds)) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 2>, TPB_E, sizeof(HLds)) == hipSuccess &&
         per_cu2 >= 1 && 3 * nblk <= per_cu2 * ncu)
         return 3;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 1, true>, TPB_E, sizeof(HLds)) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_bcr_split<false, 1>, TPB_E, sizeof(HLds)) == hipSuccess &&
         per_cu2 >= 1 && 2 * nblk <= per_cu2 * ncu)
         return 2;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_persist<false>, TPB_E, sizeof(PersistLds)) !=

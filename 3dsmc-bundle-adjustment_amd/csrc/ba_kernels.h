@@ -126,7 +126,6 @@ struct BcrWork {
     unsigned* flags;  // flags[0] (the epoch) is advanced by k_final after every BCR launch that ran
     int nblk, levels;
     int voff, vroot, vlevels;  // k_bcr_split: balanced tree on v = i + voff, root block vroot, depth vlevels + 1
-    int diag = 0;  // diagnostic (MIBA_BCR_DIAG, timing experiments only; wrong results): 1 = no helper contributions
     int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level

@@ -794,7 +794,6 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
         if (int rc = bcr_init_handoffs(ctx)) return rc;
         Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
-        Bw.diag = std::getenv("MIBA_BCR_DIAG") ? std::atoi(std::getenv("MIBA_BCR_DIAG")) : 0;
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
             else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
