@@ -914,7 +914,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             kb[K_BCR_PERSIST] = p_by;
         }
         kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
-        kb[K_BACKSUB_EVAL] = A * 2 * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read twice
+        kb[K_BACKSUB_EVAL] = A * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read once
         kf[K_BACKSUB_EVAL] = A * 450;
         kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
         kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step
