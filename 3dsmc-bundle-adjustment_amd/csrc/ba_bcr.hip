@@ -984,11 +984,14 @@ __device__ __forceinline__ void publish_flag(unsigned* f, unsigned epoch) {
 }
 // polls before a hand-off wait gives up (bcr_set_spin_limit; tests force a tiny bound)
 __device__ unsigned g_spin_limit = 1u << 22;
-#define SPIN_LIMIT g_spin_limit
+// read once per function into spin_lim (a load of g_spin_limit inside a poll loop puts a memory round trip
+// on every retry)
+#define SPIN_LIMIT spin_lim
 // ONE lane polls fa and fb together (either may be null: both loads in flight per round trip, so two
 // flags that are already set cost one round trip, not two); uniform result, false on timeout.
 __device__ bool wait_flags(const unsigned* fa, const unsigned* fb, unsigned epoch, int* lds_ok) {
     if (threadIdx.x == 0) {
+        const unsigned spin_lim = g_spin_limit;
         int ok = 1;
         unsigned n = 0;
         for (;;) {
@@ -1223,7 +1226,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
 struct FLds {
     double T[BB * BLD];
     double rdiag[BB];
-    double Wb[256];
+    double Lcm[4][256];  // panel kb's diagonal tile, column-major (wave 0 -> wave 5: W_kb = L_kk^-1)
     int ok;
     int sync[12];  // look-ahead flags of the factor workgroup (k_bcr_split)
 };
@@ -1246,6 +1249,7 @@ static constexpr int PANEL_DOUBLES = BB * BB + 4 * 256 + BB;  // per block: L ti
 __device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok, const unsigned* f2 = nullptr,
                         unsigned target2 = 0) {
     if (threadIdx.x == 0) {
+        const unsigned spin_lim = g_spin_limit;
         int ok = 1;
         unsigned n = 0;
         for (;;) {  // both loads in flight per round trip
@@ -1266,6 +1270,7 @@ __device__ bool wait_ge(const unsigned* f, unsigned target, int* lds_ok, const u
 // The payload behind these flags is read with sc1 loads only (ld_pub), so no acquire fence.
 __device__ bool wait_all_eq(const unsigned* f, int n, unsigned epoch, int* lds_ok, int skip = -1) {
     if (threadIdx.x < 64) {
+        const unsigned spin_lim = g_spin_limit;
         int ok = 1;
         for (int j = threadIdx.x; j < n && ok; j += 64) {
             if (j == skip) continue;
@@ -1296,7 +1301,8 @@ __device__ __forceinline__ unsigned long long ld_u64(const double* p) {
 // The same protocol carries the factor workgroup's published panels to its helpers (Cf | X slots, two
 // epochs) and, with two helpers, helper B's fill F to the next level's helpers (F / F2 by parity).
 __device__ __forceinline__ double* fbuf(const BcrWork& Bw, unsigned epoch) { return (epoch & 1) ? Bw.F2 : Bw.F; }
-__device__ __forceinline__ bool lower_tile(int e) { return ((e & 63) >> 4) <= ((e >> 6) >> 4); }
+// lower 16 x 16 tiles of a column-major 64 x 64 slot (element e = column * 64 + row)
+__device__ __forceinline__ bool lower_tile_cm(int e) { return ((e & 63) >> 4) >= ((e >> 6) >> 4); }
 
 static constexpr int NCT8 = (NCONTRIB + NWE - 1) / NWE;  // contribution tiles per wave (all 8 waves)
 __device__ __forceinline__ void contrib_accumulate8(const double* X, int kbk, d4b (&cacc)[NCT8], bool has_r, int wave,
@@ -1378,6 +1384,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                                                      double* __restrict__ part) {
     if (skip_step(st)) return;
     TLS(0);
+    const unsigned spin_lim = g_spin_limit;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nblk = Bw.nblk;
     const int i = blockIdx.x / (NH + 1);
@@ -1425,11 +1432,12 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             }
         }
         if (tid < 12) L.sync[tid] = 0;
-        {  // the next epoch's panel slot starts empty (the entries a panel writes: lower tiles, W, 1/diag)
+        {  // the next epoch's panel slot starts empty (the entries a panel writes: lower tiles, stored
+           // column-major, W, 1/diag)
             unsigned long long* nx = reinterpret_cast<unsigned long long*>(pg_next);
 #pragma unroll
             for (int q = 0; q < NQ; ++q)
-                if (lower_tile(tid + TPB_E * q)) nx[tid + TPB_E * q] = BCR_Y_EMPTY;
+                if (lower_tile_cm(tid + TPB_E * q)) nx[tid + TPB_E * q] = BCR_Y_EMPTY;
             nx[BB * BB + tid] = BCR_Y_EMPTY;
             nx[BB * BB + TPB_E + tid] = BCR_Y_EMPTY;
             if (tid < BB) nx[BB * BB + 4 * 256 + tid] = BCR_Y_EMPTY;
@@ -1517,8 +1525,17 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 if (live)
 #pragma unroll
                     for (int c = 0; c < 16; ++c) T[row * BLD + 16 * kb + c] = (r >= 16 || c <= r) ? a[c] : 0.0;
-                if (r < 16) L.rdiag[16 * kb + r] = my_inv;
+                if (r < 16) {
+                    L.rdiag[16 * kb + r] = my_inv;
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) L.Lcm[kb][c * 16 + r] = a[c];  // strictly-lower part is what W reads
+                }
                 if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // publish the panel's L tiles straight from the chain's registers (column-major: one
+                // coalesced row of 64 per store); W_kb and 1/diag follow from wave 5
+                if (live)
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) st_pub(pg + (16 * kb + c) * BB + row, (r >= 16 || c <= r) ? a[c] : 0.0);
                 TLS(16 + 3 * kb);
             }
             if (bad) raise_flag(flag, FLAG_NOT_PD);
@@ -1546,25 +1563,25 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         } else if (wave == 5) {
             for (int kb = 0; kb < 4; ++kb) {
                 if (!spin_ge(0, kb + 1)) { ok = false; break; }
-                const double* Tkk = T + (16 * kb) * BLD + 16 * kb;
+                // W_kb = L_kk^-1, column `lane` per lane (lanes 0-15): forward substitution of e_lane against the
+                // column-major diagonal tile (uniform LDS reads, contiguous per column), published straight from
+                // registers (row m of W_kb: 16 consecutive doubles), then 1/diag (the panel's L tiles: wave 0)
                 if (lane < 16) {
+                    const double* Lc = L.Lcm[kb];
+                    const double* rd = L.rdiag + 16 * kb;
                     double v[16];
 #pragma unroll
                     for (int m = 0; m < 16; ++m) v[m] = (m == lane) ? 1.0 : 0.0;
-                    fwd16(v, Tkk, L.rdiag + 16 * kb);
 #pragma unroll
-                    for (int m = 0; m < 16; ++m) L.Wb[m * 16 + lane] = v[m];
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // publish column panel kb: tiles (ii, kb) for ii >= kb, W_kb, 1/diag
-                for (int e = lane; e < (4 - kb) * 256; e += 64) {
-                    const int r = 16 * kb + (e >> 4), c = 16 * kb + (e & 15);
-                    st_pub(pg + r * BB + c, T[r * BLD + c]);
-                }
+                    for (int m = 0; m < 16; ++m) {
+                        v[m] *= rd[m];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) st_pub(pg + BB * BB + kb * 256 + lane + 64 * u, L.Wb[lane + 64 * u]);
-                if (lane < 16) st_pub(pg + BB * BB + 4 * 256 + 16 * kb + lane, L.rdiag[16 * kb + lane]);
+                        for (int j = m + 1; j < 16; ++j) v[j] = __builtin_fma(-Lc[m * 16 + j], v[m], v[j]);
+                    }
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) st_pub(pg + BB * BB + kb * 256 + m * 16 + lane, v[m]);
+                    st_pub(pg + BB * BB + 4 * 256 + 16 * kb + lane, rd[lane]);
+                }
                 if constexpr (STAMP) if (lane == 0) tl[32 * blockIdx.x + 2 + kb] = realtime_now();
             }
         }
@@ -1576,6 +1593,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const bool roleB = NH == 1 || role == 2;  // owns XR, the fill and the back-substitution
     if (root && roleA) return;                // the root has only the x columns (helper B)
     HLds& L = *reinterpret_cast<HLds*>(smem);
+    // the wave index as a scalar: role and tile branches below are uniform (no exec masking around the
+    // LDS operand loads and MFMAs of the contributions)
+    const int wu = __builtin_amdgcn_readfirstlane(wave);
     // Border without a second pass (was k_bcr_border): every block's helper B publishes the Gram of its
     // forward-solved x = [b_a | B] with its contributions; the root sums them with its own, solves the
     // 4x4 border system before its back-substitution and publishes y_k with y_root, so each block
@@ -1723,11 +1743,11 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // layout of a 16x16x4 step), so the forward substitution of its columns (X_kb <- W_kb X_kb,
     // X_ii -= L(ii,kb) X_kb) needs no barrier and no LDS round trip; only the finished row block kb
     // is stored to LDS, for the Schur contributions of all waves.
-    const HelperMap hm = helper_map<NH>(role, wave, root);
+    const HelperMap hm = helper_map<NH>(role, wu, root);
     constexpr int MAXOWN = NH == 1 ? 2 : 1;
     int own_cb[MAXOWN];
     own_cb[0] = hm.cb;
-    if constexpr (MAXOWN > 1) own_cb[1] = (!root && wave == 0) ? 8 : -1;
+    if constexpr (MAXOWN > 1) own_cb[1] = (!root && wu == 0) ? 8 : -1;
     d4b xt[MAXOWN][4];
     __syncthreads();
 #pragma unroll
@@ -1742,27 +1762,31 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     d4b cacc[NCT8];
 #pragma unroll
     for (int q = 0; q < NCT8; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
-    // Schur contributions of the finished X row block kbk: operands of every tile first, then interleaved chains
+    // Schur contributions of the finished X row block kbk: operands of every tile first (in-bounds addresses,
+    // selects after: no branch around an LDS load), then interleaved chains. NH = 2: two slots per wave.
+    constexpr int NQA = NH == 2 ? 2 : NCT8;
     auto contrib_rows = [&](int kbk) {
-        double av[NCT8][4], bv[NCT8][4];
+        double av[NQA][4], bv[NQA][4];
 #pragma unroll
-        for (int q = 0; q < NCT8; ++q) {
+        for (int q = 0; q < NQA; ++q) {
             const int t = hm.tiles[q];
             const ContribTile ct = contrib_tile(t < 0 ? 0 : t, has_r);
             const bool on = t >= 0 && ct.valid;
             const bool bok = on && (!ct.rhs || rr < RC);
             const bool aok = on && (!ct.gram || rr < RC);
+            const int ia = ct.aoff + 16 * ct.ib + (aok ? rr : 0), ib = ct.boff + 16 * ct.cb + (bok ? rr : 0);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const double* row = L.X + (16 * kbk + 4 * s4 + kk) * XW;
-                av[q][s4] = aok ? row[ct.aoff + 16 * ct.ib + rr] : 0.0;
-                bv[q][s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
+                const double a_ = row[ia], b_ = row[ib];
+                av[q][s4] = aok ? a_ : 0.0;
+                bv[q][s4] = bok ? b_ : 0.0;
             }
         }
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-            for (int q = 0; q < NCT8; ++q)
+            for (int q = 0; q < NQA; ++q)
                 if (hm.tiles[q] >= 0)
                     cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][s4], bv[q][s4], cacc[q], 0, 0, 0);
     };
@@ -1779,7 +1803,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     auto fill_rows = [&](int kbk) {  // facc += XR_kbk^T XL_kbk for F tiles 20 + wave + 8 q
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const ContribTile ct = contrib_tile(20 + wave + NWE * q, true);
+            const ContribTile ct = contrib_tile(20 + wu + NWE * q, true);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const double* row = L.X + (16 * kbk + 4 * s4 + kk) * XW;
@@ -1793,9 +1817,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     // empty (the factor workgroup had not stored them yet) are polled again at the panel's commit.
     unsigned long long pv[4];
     auto paddr = [&](int k, int u) -> const double* {  // this thread's value u of panel k (nullptr: none)
-        if (u < 2) {
-            const int e = tid + TPB_E * u;
-            return e < (4 - k) * 256 ? pg + (16 * k + (e >> 4)) * BB + 16 * k + (e & 15) : nullptr;
+        if (u < 2) {  // L tiles (ii, k), ii >= k, column-major: thread -> (row, column) = (16 k + e % nr, 16 k + e / nr)
+            const int e = tid + TPB_E * u, nr = 64 - 16 * k;
+            return e < (4 - k) * 256 ? pg + (16 * k + e / nr) * BB + 16 * k + e % nr : nullptr;
         }
         if (u == 2) return tid < 256 ? pg + BB * BB + k * 256 + tid : nullptr;
         return tid < 16 ? pg + BB * BB + 4 * 256 + 16 * k + tid : nullptr;
@@ -1822,8 +1846,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int e = tid + TPB_E * u;
-            if (e < (4 - k) * 256) L.L[(16 * k + (e >> 4)) * BLD + 16 * k + (e & 15)] = __longlong_as_double((long long)pv[u]);
+            const int e = tid + TPB_E * u, nr = 64 - 16 * k;
+            if (e < (4 - k) * 256) L.L[(16 * k + e % nr) * BLD + 16 * k + e / nr] = __longlong_as_double((long long)pv[u]);
         }
         if (tid < 256) L.W[k][tid] = __longlong_as_double((long long)pv[2]);
         if (tid < 16) L.rdiag[16 * k + tid] = __longlong_as_double((long long)pv[3]);
@@ -1838,7 +1862,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             return;
         }
         TLS(16 + 4 * kb);
-        if (NH == 2 && wave == 4 + kb) {  // x_kb <- W_kb x_kb (LDS row block, 8 valid columns)
+        if (NH == 2 && wu == 4 + kb) {  // x_kb <- W_kb x_kb (LDS row block, 8 valid columns)
             double aw[4], bx[4];
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
@@ -1886,8 +1910,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         TLS(17 + 4 * kb);
         // next panel's loads in flight under the contributions (values still empty are polled at its commit)
         if (kb < 3) issue(kb + 1);
-        if (NH == 2 && wave > 4 + kb) {  // x_ii -= L(ii,kb) x_kb, ii = wave - 4
-            const int ii = wave - 4;
+        if (NH == 2 && wu > 4 + kb) {  // x_ii -= L(ii,kb) x_kb, ii = wave - 4
+            const int ii = wu - 4;
             double al[4], bx[4];
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
@@ -1994,7 +2018,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             for (int kbk = 0; kbk < 4; ++kbk) fill_rows(kbk);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const ContribTile ct = contrib_tile(20 + wave + NWE * q, true);
+                const ContribTile ct = contrib_tile(20 + wu + NWE * q, true);
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
                     st_pub(fbuf(Bw, epoch) + (size_t)i * BSZ + (size_t)(16 * ct.ib + kk + 4 * g) * BB + 16 * ct.cb + rr, -facc[q][g]);
