@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 
@@ -1223,10 +1224,13 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
 // block kb; it publishes the contributions, then runs the back-substitution from its copy of L.
 // F's pivot chain thus no longer shares its CU's f64 pipes with the 136-column MFMA work.
 // Hand-offs as in k_bcr_persist; panel flags hold 4 * epoch + kb (monotone, polled with >=).
+static constexpr int SG_LD = 66;         // LDS row stride of pulled 64-column row blocks (pull_rows)
+static constexpr int SG_W = 16 * SG_LD;  // one staged 16 x 64 row block
 struct FLds {
     double T[BB * BLD];
     double rdiag[BB];
     double Lcm[4][256];  // panel kb's diagonal tile, column-major (wave 0 -> wave 5: W_kb = L_kk^-1)
+    double sg[2 * SG_W];  // pulled row blocks XR_a, XL_b of the survived levels
     int ok;
     int sync[12];  // look-ahead flags of the factor workgroup (k_bcr_split)
 };
@@ -1299,78 +1303,123 @@ __device__ __forceinline__ unsigned long long ld_u64(const double* p) {
     return __hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The same protocol carries the factor workgroup's published panels to its helpers (Cf | X slots, two
-// epochs) and, with two helpers, helper B's fill F to the next level's helpers (F / F2 by parity).
-__device__ __forceinline__ double* fbuf(const BcrWork& Bw, unsigned epoch) { return (epoch & 1) ? Bw.F2 : Bw.F; }
+// epochs).
 // lower 16 x 16 tiles of a column-major 64 x 64 slot (element e = column * 64 + row)
 __device__ __forceinline__ bool lower_tile_cm(int e) { return ((e & 63) >> 4) >= ((e >> 6) >> 4); }
 
-static constexpr int NCT8 = (NCONTRIB + NWE - 1) / NWE;  // contribution tiles per wave (all 8 waves)
-__device__ __forceinline__ void contrib_accumulate8(const double* X, int kbk, d4b (&cacc)[NCT8], bool has_r, int wave,
-                                                    int rr, int kk) {
+// Pull hand-off between the levels (k_bcr_split). The eliminated block's helpers publish every finished row
+// block kb of their forward-substituted columns — XL and XR (16 x 64 each), x (16 x 8) — into epoch-parity
+// slots, flag-free (no drain: consumers poll the values, an empty slot holds BCR_Y_EMPTY). Each survivor's
+// workgroups then form the Schur terms they need themselves, row block by row block, as the rows arrive
+// (a = j - s, b = j + s are eliminated at level m):
+//   factor F(j):  D_j -= XR_a^T XR_a + XL_b^T XL_b
+//   helpers:      x_j -= XR_a^T x_a + XL_b^T x_b; at j's last survived level the couplings of its own level,
+//                 XL_j = -XR_a^T XL_a (helper A) and XR_j = -XL_b^T XR_b (helper B) (the fills)
+// The eliminated block's helpers thus run only the forward substitution (at the factor's pace), and the
+// next level's factor starts one row-block hand-off after the last panel instead of after the contribution
+// tiles, their publication and their flag.
+__device__ __forceinline__ double* pub_xl(const BcrWork& Bw, unsigned e) { return (e & 1) ? Bw.F : Bw.UL; }
+__device__ __forceinline__ double* pub_xr(const BcrWork& Bw, unsigned e) { return (e & 1) ? Bw.F2 : Bw.UR; }
+__device__ __forceinline__ double* pub_x(const BcrWork& Bw, unsigned e) { return (e & 1) ? Bw.rR : Bw.rL; }
+template <int NW, int NX>
+struct PullSrc {
+    const double* w[NW];               // 64-column sources (64 x 64 row-major); nullptr: staged as zeros
+    const double* x[NX > 0 ? NX : 1];  // 8-column sources (64 x 8)
+};
+// Row block kb of every source -> LDS sg (64-column sources at sg + k SG_W, row stride SG_LD, then the
+// 8-column ones, 128 each). ONE lane first waits for each live source's last entry of the row block (so the
+// workgroup does not load the memory path the producers store through while it waits), then every thread
+// loads its entries and re-polls those still empty. Also the barrier that ends the previous row block's
+// reads of sg. Uniform result; false on timeout.
+template <int NW, int NX>
+__device__ bool pull_rows(const PullSrc<NW, NX>& ps, int kb, double* sg, int* lds_ok, unsigned spin_lim) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {  // every live source's probe in flight per round trip
+        const double* pp[NW + NX];
+        unsigned long long pv[NW + NX];
 #pragma unroll
-    for (int q = 0; q < NCT8; ++q) {
-        const int t = wave + NWE * q;
-        if (t >= NCONTRIB) continue;
-        const ContribTile ct = contrib_tile(t, has_r);
-        if (!ct.valid) continue;
-        const bool bok = !ct.rhs || rr < RC;
-        double av[4], bv[4];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const double* row = X + (16 * kbk + 4 * s4 + kk) * XW;
-            av[s4] = row[ct.aoff + 16 * ct.ib + rr];
-            bv[s4] = bok ? row[ct.boff + 16 * ct.cb + rr] : 0.0;
+        for (int k = 0; k < NW + NX; ++k) {
+            const double* p = k < NW ? ps.w[k] : ps.x[k - NW];
+            pp[k] = p ? p + (k < NW ? (16 * kb + 15) * BB + BB - 1 : (16 * kb + 15) * RC + RC - 1) : nullptr;
+            pv[k] = pp[k] ? ld_u64(pp[k]) : 0ull;
         }
+        int ok = 1;
+        for (unsigned n = 0;; ++n) {
+            bool pend = false;
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], cacc[q], 0, 0, 0);
+            for (int k = 0; k < NW + NX; ++k) pend = pend || pv[k] == BCR_Y_EMPTY;
+            if (!pend) break;
+            if (n > SPIN_LIMIT) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+            for (int k = 0; k < NW + NX; ++k)
+                if (pv[k] == BCR_Y_EMPTY) pv[k] = ld_u64(pp[k]);
+        }
+        *lds_ok = ok;
     }
+    __syncthreads();
+    if (!*lds_ok) return false;
+    constexpr int NE = NW * 1024 + NX * 128, NU = (NE + TPB_E - 1) / TPB_E;
+    // the source of entry u is uniform over the workgroup (64-column part) or a wave (8-column part)
+    auto gaddr = [&](int u) -> const double* {
+        const int e = tid + TPB_E * u;
+        if (e < NW * 1024) {
+            const double* p = ps.w[e >> 10];
+            return p ? p + (16 * kb + ((e >> 6) & 15)) * BB + (e & 63) : nullptr;
+        }
+        if constexpr (NX > 0) {
+            const int f = e - NW * 1024;
+            if (f < NX * 128) {
+                const double* p = ps.x[f >> 7];
+                return p ? p + (16 * kb + ((f >> 3) & 15)) * RC + (f & 7) : nullptr;
+            }
+        }
+        return nullptr;
+    };
+    unsigned long long v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const double* a = gaddr(u);
+        v[u] = a ? ld_u64(a) : 0ull;
+    }
+    int ok = 1;
+    for (unsigned n = 0;; ++n) {
+        bool pend = false;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) pend = pend || v[u] == BCR_Y_EMPTY;
+        if (!pend) break;
+        if (n > SPIN_LIMIT) { ok = 0; break; }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+            if (v[u] == BCR_Y_EMPTY) v[u] = ld_u64(gaddr(u));
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int e = tid + TPB_E * u;
+        const double d = __longlong_as_double((long long)v[u]);
+        if (e < NW * 1024) sg[(e >> 10) * SG_W + ((e >> 6) & 15) * SG_LD + (e & 63)] = d;
+        else if (e < NE) sg[NW * SG_W + (e - NW * 1024)] = d;
+    }
+    return __syncthreads_and(ok);
 }
 
 #define TLS(k)                                                                                     \
     do {                                                                                           \
         if constexpr (STAMP) if (threadIdx.x == 0) tl[32 * blockIdx.x + (k)] = realtime_now();      \
     } while (0)
-// Helper roles: NH = 1 -> one helper H per block owning all of [XL | XR | x] and every contribution;
-// NH = 2 -> helper A owns [XL | x] (UL, rL), helper B owns [XR | x] (UR, rR); A then publishes its
-// final XL and B forms the fill F = -XR^T XL, the back-substitution data [P | Q | u] and y_i.
+// Helper roles: NH = 1 -> one helper H per block owning all of [XL | XR | x]; NH = 2 -> helper A owns
+// [XL | x], helper B owns [XR | x], the Gram of x and the back-substitution data [P | Q | u] and y_i.
 // x (8 columns) is forward-substituted by both (same arithmetic, bitwise identical copies): its row
 // block r lives in LDS and belongs to wave 4 + r (waves 0-3 hold the four XL / XR column tiles, one
-// per SIMD), so x_kb <- W_kb x_kb runs beside the column tiles and x_ii -= L(ii,kb) x_kb beside the
-// contributions.
-struct HelperMap {
-    int cb;                // column tile of [XL | XR | x] owned by this wave (-1: none)
-    int ntile;             // contribution tiles of this helper
-    int tiles[NCT8];       // contribution tile ids (contrib_tile map) of this wave
-};
+// per SIMD), so x_kb <- W_kb x_kb runs beside the column tiles and x_ii -= L(ii,kb) x_kb after them.
+// Column tile of [XL | XR | x] (16 columns) a helper wave keeps in registers (-1: none); NH = 1 also keeps
+// the x columns (tile 8) on wave 0. The root has only the x columns (NH = 1: wave 0; NH = 2: LDS rows).
 template <int NH>
-__device__ __forceinline__ HelperMap helper_map(int role, int wave, bool root) {
-    HelperMap h{-1, 0, {}};
-    if (root) {  // root: only the x columns (NH = 1: wave 0 of the helper; NH = 2: LDS rows, below)
-        h.cb = (NH == 1 && wave == 0) ? 0 : -1;
-        return h;
-    }
-    if (NH == 1) {
-        h.cb = wave;  // + the x tile (cb 8) on wave 0, handled by own2
-#pragma unroll
-        for (int q = 0; q < NCT8; ++q) {
-            const int t = (NWE - 1 - wave) + NWE * q;
-            h.tiles[q] = t <= GRAM_TILE ? t : -1;  // tile 44 (the Gram) lands on wave 3, which has 5 others
-        }
-        return h;
-    }
-    const bool B = role == 2;
-    h.cb = wave < 4 ? (B ? 4 + wave : wave) : -1;  // one XL / XR tile per SIMD; x rows: x_rows_* below
-    // A: UL (0..9) + rL (36..39); B: UR (10..19) + rR (40..43) + the Gram (entry 14: wave 6);
-    // entry w and w + 8 of the list
-#pragma unroll
-    for (int q = 0; q < NCT8; ++q) {
-        const int e = wave + NWE * q;
-        int t = -1;
-        if (q < 2 && e < 14) t = e < 10 ? (B ? 10 + e : e) : (B ? 40 + e - 10 : 36 + e - 10);
-        if (q < 2 && e == 14 && B) t = GRAM_TILE;
-        h.tiles[q] = t;
-    }
-    return h;
+__device__ __forceinline__ int helper_cb(bool roleB, int wave, bool root) {
+    if (root) return (NH == 1 && wave == 0) ? 0 : -1;
+    if (NH == 1) return wave;
+    return wave < 4 ? (roleB ? 4 + wave : wave) : -1;
 }
 
 template <bool STAMP, int NH>
@@ -1398,12 +1447,8 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     const int nd = 6 * P.nac;
     const int b0 = i * G_DOF;
     const unsigned epoch = Bw.flags[0] + 1;
-    unsigned* elim_f = Bw.flags + 16;              // NH = 1: all contributions; NH = 2: helper A's (UL, rL)
-    unsigned* elimB_f = NH == 2 ? Bw.flags + 16 + 3 * nblk : elim_f;  // helper B's (UR, rR)
-    unsigned* fill_f = NH == 2 ? Bw.flags + 16 + 4 * nblk : elim_f;   // F of block i
-    unsigned* xl_f = Bw.flags + 16 + 5 * nblk;                         // NH = 2: final XL of block i
-    unsigned* ul_f = elim_f;   // producers of UL / rL
-    unsigned* ur_f = elimB_f;  // producers of UR / rR
+    // block i's Gram of x (Bp) published by helper B (NH = 2) / H (NH = 1): the root sums them all
+    unsigned* gram_f = NH == 2 ? Bw.flags + 16 + 3 * nblk : Bw.flags + 16;
     // this block's published panels, by epoch parity (flag-free: F stores, the helpers poll the values)
     double* pg = Bw.Cf + ((epoch & 1) ? (size_t)nblk * PANEL_DOUBLES : 0) + (size_t)i * PANEL_DOUBLES;
     double* pg_next = Bw.Cf + ((epoch & 1) ? 0 : (size_t)nblk * PANEL_DOUBLES) + (size_t)i * PANEL_DOUBLES;
@@ -1442,24 +1487,52 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             nx[BB * BB + TPB_E + tid] = BCR_Y_EMPTY;
             if (tid < BB) nx[BB * BB + 4 * 256 + tid] = BCR_Y_EMPTY;
         }
+        // survived levels: D_i -= XR_a^T XR_a + XL_b^T XL_b, pulled row block by row block from the rows the
+        // eliminated neighbours' helpers publish (pull_rows); lower tiles wq and wq + 8 on wave wq
         for (int m = 0; m < mi; ++m) {
             const int s = 1 << m, a = i - s, b = i + s;
-            if (!wait_flags(a >= 0 ? ur_f + a : nullptr, b < nblk ? ul_f + b : nullptr, epoch, &L.ok)) {
-                if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-                return;
-            }
-            double ua[NQ], ub[NQ];
+            PullSrc<2, 0> ps;
+            ps.w[0] = a >= 0 ? pub_xr(Bw, epoch) + (size_t)a * BSZ : nullptr;
+            ps.w[1] = b < nblk ? pub_xl(Bw, epoch) + (size_t)b * BSZ : nullptr;
+            ps.x[0] = nullptr;
+            const int wq = __builtin_amdgcn_readfirstlane(wave);
+            int tib[2], tjb[2];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int e = tid + TPB_E * q;
-                const bool lower = ((e & 63) >> 4) <= ((e >> 6) >> 4);
-                ua[q] = a >= 0 && lower ? ld_pub(Bw.UR + (size_t)a * BSZ + e) : 0.0;
-                ub[q] = b < nblk && lower ? ld_pub(Bw.UL + (size_t)b * BSZ + e) : 0.0;
+            for (int q = 0; q < 2; ++q) {
+                int t = wq + NWE * q, ib = 0;
+                while (t > ib) { t -= ib + 1; ++ib; }
+                tib[q] = ib;
+                tjb[q] = t;
+            }
+            d4b acc[2] = {d4b{0.0, 0.0, 0.0, 0.0}, d4b{0.0, 0.0, 0.0, 0.0}};
+            for (int kb = 0; kb < 4; ++kb) {
+                if (!pull_rows(ps, kb, L.sg, &L.ok, spin_lim)) {
+                    if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
+                    return;
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    if (wq + NWE * q >= 10) continue;
+#pragma unroll
+                    for (int src = 0; src < 2; ++src) {
+                        if (!ps.w[src]) continue;
+                        const double* sgs = L.sg + src * SG_W;
+                        double av[4], bv[4];
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4) {
+                            av[s4] = sgs[(4 * s4 + kk) * SG_LD + 16 * tib[q] + rr];
+                            bv[s4] = sgs[(4 * s4 + kk) * SG_LD + 16 * tjb[q] + rr];
+                        }
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc[q], 0, 0, 0);
+                    }
+                }
             }
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-                L.T[r * BLD + c] = (L.T[r * BLD + c] - ua[q]) - ub[q];
+            for (int q = 0; q < 2; ++q) {
+                if (wq + NWE * q >= 10) continue;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) L.T[(16 * tib[q] + kk + 4 * g) * BLD + 16 * tjb[q] + rr] -= acc[q][g];
             }
         }
         __syncthreads();
@@ -1588,24 +1661,37 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         if (!ok) raise_flag(flag, FLAG_TIMEOUT);
         return;
     }
-    // ================= helpers: panel application, contributions, back-substitution
-    const bool roleA = NH == 2 && role == 1;  // NH = 2: XL side (exits after publishing XL)
-    const bool roleB = NH == 1 || role == 2;  // owns XR, the fill and the back-substitution
+    // ================= helpers: survived levels (pulls), panel application, back-substitution
+    const bool roleA = NH == 2 && role == 1;  // NH = 2: XL side (exits after its forward substitution)
+    const bool roleB = NH == 1 || role == 2;  // owns XR, the Gram and the back-substitution
     if (root && roleA) return;                // the root has only the x columns (helper B)
     HLds& L = *reinterpret_cast<HLds*>(smem);
-    // the wave index as a scalar: role and tile branches below are uniform (no exec masking around the
-    // LDS operand loads and MFMAs of the contributions)
+    // the wave index as a scalar: role and tile branches below are uniform
     const int wu = __builtin_amdgcn_readfirstlane(wave);
+    // rows this helper publishes for the next level (pull hand-off): XL if the block has a left neighbour,
+    // XR if it has a right one, x if either (helper A / H; helper B's x is the same)
+    const bool pubL = !root && (NH == 1 || roleA) && has_l;
+    const bool pubR = !root && roleB && has_r;
+    const bool pubX = !root && (NH == 1 || roleA) && (has_l || has_r);
+    double* const xl_pub = pub_xl(Bw, epoch) + (size_t)i * BSZ;
+    double* const xr_pub = pub_xr(Bw, epoch) + (size_t)i * BSZ;
+    double* const x_pub = pub_x(Bw, epoch) + (size_t)i * RSZ;
     // Border without a second pass (was k_bcr_border): every block's helper B publishes the Gram of its
-    // forward-solved x = [b_a | B] with its contributions; the root sums them with its own, solves the
-    // 4x4 border system before its back-substitution and publishes y_k with y_root, so each block
-    // applies its camera step right after its own back-substitution (no wait for every block).
-    if (roleB)  // this block's slot of the next epoch's y buffer starts empty
-        reinterpret_cast<unsigned long long*>(ybuf(Bw, epoch + 1))[(size_t)i * RSZ + tid] = BCR_Y_EMPTY;
-    if (NH == 2 && roleB && !root) {  // ... and so does its fill slot
-        unsigned long long* nf = reinterpret_cast<unsigned long long*>(fbuf(Bw, epoch + 1)) + (size_t)i * BSZ;
+    // forward-solved x = [b_a | B]; the root sums them with its own, solves the 4x4 border system before its
+    // back-substitution and publishes y_k with y_root, so each block applies its camera step right after its
+    // own back-substitution (no wait for every block).
+    // This block's slots of the next epoch's buffers start empty (y, published rows).
+    if (roleB) reinterpret_cast<unsigned long long*>(ybuf(Bw, epoch + 1))[(size_t)i * RSZ + tid] = BCR_Y_EMPTY;
+    {
+        unsigned long long* nl = reinterpret_cast<unsigned long long*>(pub_xl(Bw, epoch + 1) + (size_t)i * BSZ);
+        unsigned long long* nr = reinterpret_cast<unsigned long long*>(pub_xr(Bw, epoch + 1) + (size_t)i * BSZ);
+        if (pubL)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) nf[tid + TPB_E * q] = BCR_Y_EMPTY;
+            for (int q = 0; q < NQ; ++q) nl[tid + TPB_E * q] = BCR_Y_EMPTY;
+        if (pubR)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) nr[tid + TPB_E * q] = BCR_Y_EMPTY;
+        if (pubX) reinterpret_cast<unsigned long long*>(pub_x(Bw, epoch + 1) + (size_t)i * RSZ)[tid] = BCR_Y_EMPTY;
     }
     // level-0 inputs: every global load issued before the first LDS store (clamped addresses, selects after)
     double bkv = 0.0;
@@ -1657,70 +1743,93 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         L.X[r * XW + 2 * BB + c] = rv;
     }
     if (root && tid < 14) L.bk[tid] = bkv;
-    for (int m = 0; m < mi; ++m) {
-        const int s = 1 << m, a = i - s, b = i + s;
-        const bool last = m == mi - 1 && !root;
-        // x -= rR(a) + rL(b); at the last survived level the fills F(a) -> XL, F(b)^T -> XR
-        const unsigned* fa = a >= 0 ? ur_f + a : nullptr;
-        const unsigned* fb = b < nblk ? ul_f + b : nullptr;
-        if (!wait_flags(fa, fb, epoch, &L.ok)) {
-            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-            return;
+    // Survived levels: the Schur terms of the level's eliminated neighbours a = i - s, b = i + s, pulled row
+    // block by row block (pull_rows; staging in L / rdiag / W, which hold nothing before the first panel):
+    //   x -= XR_a^T x_a + XL_b^T x_b              (x waves: row block wu - xw0; one chain over the row blocks)
+    //   last level: XL = -XR_a^T XL_a (helper A / H waves 0-3: column tile wu)
+    //               XR = -XL_b^T XR_b (helper B waves 0-3 / H waves 4-7: column tile wu & 3)
+    {
+        static_assert(4 * SG_W + 2 * RSZ / 4 <= (int)((offsetof(HLds, Bl) - offsetof(HLds, L)) / sizeof(double)),
+                      "pulled row blocks fit L / rdiag / W");
+        double* const sg = L.L;
+        const double* const sx = sg + 4 * SG_W;
+        constexpr int xw0 = NH == 2 ? 4 : 0;
+        const bool xwave = wu >= xw0 && wu < xw0 + 4;
+        const int xr = wu - xw0;
+        const bool sideA = NH == 1 ? wu < 4 : roleA;                    // fill side of this wave
+        const bool fwave = NH == 1 ? true : wu < 4;                      // waves holding a fill column tile
+        for (int m = 0; m < mi; ++m) {
+            const int s = 1 << m, a = i - s, b = i + s;
+            const bool ha = a >= 0, hb = b < nblk;
+            const bool last = m == mi - 1 && !root;
+            const bool fa = last && has_l && (NH == 1 || roleA), fb = last && has_r && roleB;
+            PullSrc<4, 2> ps;
+            ps.w[0] = ha ? pub_xr(Bw, epoch) + (size_t)a * BSZ : nullptr;
+            ps.w[1] = hb ? pub_xl(Bw, epoch) + (size_t)b * BSZ : nullptr;
+            ps.w[2] = fa ? pub_xl(Bw, epoch) + (size_t)a * BSZ : nullptr;
+            ps.w[3] = fb ? pub_xr(Bw, epoch) + (size_t)b * BSZ : nullptr;
+            ps.x[0] = ha ? pub_x(Bw, epoch) + (size_t)a * RSZ : nullptr;
+            ps.x[1] = hb ? pub_x(Bw, epoch) + (size_t)b * RSZ : nullptr;
+            const bool fon = fwave && (sideA ? fa : fb);
+            d4b xacc = {0.0, 0.0, 0.0, 0.0};
+            d4b facc[4];
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) facc[ii] = d4b{0.0, 0.0, 0.0, 0.0};
+            for (int kb = 0; kb < 4; ++kb) {
+                if (!pull_rows(ps, kb, sg, &L.ok, spin_lim)) {
+                    if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
+                    return;
+                }
+                if (xwave) {
+#pragma unroll
+                    for (int src = 0; src < 2; ++src) {
+                        if (!(src ? hb : ha)) continue;
+                        double av[4], bv[4];
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4) {
+                            av[s4] = sg[src * SG_W + (4 * s4 + kk) * SG_LD + 16 * xr + rr];
+                            const double xb_ = sx[src * RSZ / 4 + (4 * s4 + kk) * RC + (rr & 7)];
+                            bv[s4] = rr < RC ? xb_ : 0.0;
+                        }
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4) xacc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], xacc, 0, 0, 0);
+                    }
+                }
+                if (fon) {
+                    const double* sa = sg + (sideA ? 0 : 1) * SG_W;  // XR_a (A) / XL_b (B): row tiles of the fill
+                    const double* sb = sg + (sideA ? 2 : 3) * SG_W;  // XL_a (A) / XR_b (B): its column tile
+                    double av[4][4], bv[4];
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4) {
+                        bv[s4] = sb[(4 * s4 + kk) * SG_LD + 16 * (wu & 3) + rr];
+#pragma unroll
+                        for (int ii = 0; ii < 4; ++ii) av[ii][s4] = sa[(4 * s4 + kk) * SG_LD + 16 * ii + rr];
+                    }
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                        for (int ii = 0; ii < 4; ++ii)
+                            facc[ii] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ii][s4], bv[s4], facc[ii], 0, 0, 0);
+                }
+            }
+            if (xwave && rr < RC)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) L.X[(16 * xr + kk + 4 * g) * XW + 2 * BB + rr] -= xacc[g];
+            if (last && fwave) {
+                // this side's coupling of level mi (zero without the neighbour)
+                const int col = sideA ? 16 * (wu & 3) : BB + 16 * (wu & 3);
+                const bool f = sideA ? fa : fb;
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + col + rr] = f ? -facc[ii][g] : 0.0;
+            }
         }
-        if (last && NH == 2) {
-            // the fill of the neighbour this helper's side faces, polled value by value
-            const bool on = roleA ? a >= 0 : has_r;
-            const double* pf = fbuf(Bw, epoch) + (size_t)(on ? (roleA ? a : b) : 0) * BSZ;
-            unsigned long long fv[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) fv[q] = on ? ld_u64(pf + tid + TPB_E * q) : 0ull;
-            int okp = 1;
-            for (unsigned n = 0;; ++n) {
-                bool pend = false;
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) pend = pend || fv[q] == BCR_Y_EMPTY;
-                if (!pend) break;
-                if (n > SPIN_LIMIT) { okp = 0; break; }
-                __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                for (int q = 0; q < NQ; ++q)
-                    if (fv[q] == BCR_Y_EMPTY) fv[q] = ld_u64(pf + tid + TPB_E * q);
-            }
-            if (!__syncthreads_and(okp)) {
-                if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-                return;
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-                const double v = __longlong_as_double((long long)fv[q]);
-                if (roleA) L.X[r * XW + c] = v;
-                else L.X[c * XW + BB + r] = v;
-            }
-        } else if (last) {
-            double fl[NQ], fr[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int e = tid + TPB_E * q;
-                fl[q] = (NH == 1 || roleA) && a >= 0 ? ld_pub(Bw.F + (size_t)a * BSZ + e) : 0.0;
-                fr[q] = (NH == 1 || roleB) && has_r ? ld_pub(Bw.F + (size_t)b * BSZ + e) : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int e = tid + TPB_E * q, r = e >> 6, c = e & 63;
-                if (NH == 1 || roleA) L.X[r * XW + c] = fl[q];
-                if (NH == 1 || roleB) L.X[c * XW + BB + r] = fr[q];
-            }
-        }
-        const double ra = a >= 0 ? ld_pub(Bw.rR + (size_t)a * RSZ + tid) : 0.0;
-        const double rb = b < nblk ? ld_pub(Bw.rL + (size_t)b * RSZ + tid) : 0.0;
-        const int r = tid >> 3, c = tid & 7;
-        L.X[r * XW + 2 * BB + c] = (L.X[r * XW + 2 * BB + c] - ra) - rb;
     }
     if (root) {
-        // the other blocks' Grams (published with their helper-B contributions, which the root's own
-        // levels already waited on or soon will), summed in block order; overlaps F's first panel
-        if (!wait_all_eq((NH == 2 ? elimB_f : elim_f), nblk, epoch, &L.ok, i)) {
+        // the other blocks' Grams (published by their helpers B after their forward substitution), summed in
+        // block order; overlaps F's first panel
+        if (!wait_all_eq(gram_f, nblk, epoch, &L.ok, i)) {
             if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
@@ -1738,15 +1847,14 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     TLS(1);
     double* X = root ? L.X + 2 * BB : L.X;
     const int ncol = root ? RC : XC;
-    // Column-tile ownership (helper_map): each wave keeps its column tiles of X in registers
+    // Column-tile ownership (helper_cb): each wave keeps its column tiles of X in registers
     // (MFMA accumulator layout x[g] = X[16 ii + kk + 4 g][16 cb + rr], which is also the B-operand
     // layout of a 16x16x4 step), so the forward substitution of its columns (X_kb <- W_kb X_kb,
-    // X_ii -= L(ii,kb) X_kb) needs no barrier and no LDS round trip; only the finished row block kb
-    // is stored to LDS, for the Schur contributions of all waves.
-    const HelperMap hm = helper_map<NH>(role, wu, root);
+    // X_ii -= L(ii,kb) X_kb) needs no barrier and no LDS round trip; the finished row block kb is stored
+    // to LDS (the back-substitution's copy, the Gram) and published for the next level (pull hand-off).
     constexpr int MAXOWN = NH == 1 ? 2 : 1;
     int own_cb[MAXOWN];
-    own_cb[0] = hm.cb;
+    own_cb[0] = helper_cb<NH>(roleB, wu, root);
     if constexpr (MAXOWN > 1) own_cb[1] = (!root && wu == 0) ? 8 : -1;
     d4b xt[MAXOWN][4];
     __syncthreads();
@@ -1759,59 +1867,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
             for (int g = 0; g < 4; ++g) xt[j][ii][g] = colok ? X[(16 * ii + kk + 4 * g) * XW + 16 * cb + rr] : 0.0;
     }
-    d4b cacc[NCT8];
-#pragma unroll
-    for (int q = 0; q < NCT8; ++q) cacc[q] = d4b{0.0, 0.0, 0.0, 0.0};
-    // Schur contributions of the finished X row block kbk: operands of every tile first (in-bounds addresses,
-    // selects after: no branch around an LDS load), then interleaved chains. NH = 2: two slots per wave.
-    constexpr int NQA = NH == 2 ? 2 : NCT8;
-    auto contrib_rows = [&](int kbk) {
-        double av[NQA][4], bv[NQA][4];
-#pragma unroll
-        for (int q = 0; q < NQA; ++q) {
-            const int t = hm.tiles[q];
-            const ContribTile ct = contrib_tile(t < 0 ? 0 : t, has_r);
-            const bool on = t >= 0 && ct.valid;
-            const bool bok = on && (!ct.rhs || rr < RC);
-            const bool aok = on && (!ct.gram || rr < RC);
-            const int ia = ct.aoff + 16 * ct.ib + (aok ? rr : 0), ib = ct.boff + 16 * ct.cb + (bok ? rr : 0);
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const double* row = L.X + (16 * kbk + 4 * s4 + kk) * XW;
-                const double a_ = row[ia], b_ = row[ib];
-                av[q][s4] = aok ? a_ : 0.0;
-                bv[q][s4] = bok ? b_ : 0.0;
-            }
-        }
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-            for (int q = 0; q < NQA; ++q)
-                if (hm.tiles[q] >= 0)
-                    cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][s4], bv[q][s4], cacc[q], 0, 0, 0);
-    };
-    // NH = 2: helper A stores its finished XL row block kb (sc1) during its X update of panel kb and
-    // raises xl_f = 4 epoch + 3 with its contributions; helper B, after publishing its own
-    // contributions, loads all of XL (its back-substitution needs it) and, when the block has a right
-    // neighbour, forms the fill F = -XR^T XL (off B's panel loop, which then keeps A's pace).
-    const bool xl_on = NH == 2 && !root;
-    const bool fill_on = xl_on && has_r;
-    // XL of this block, 64 x 64 (stride BB), in the Dacc slot (used only by the per-level launches;
-    // the published panels, 5184 doubles per block, run past Cf into the X slots)
-    double* xlg = Bw.Dacc + (size_t)i * BSZ;
-    d4b facc[2] = {d4b{0.0, 0.0, 0.0, 0.0}, d4b{0.0, 0.0, 0.0, 0.0}};
-    auto fill_rows = [&](int kbk) {  // facc += XR_kbk^T XL_kbk for F tiles 20 + wave + 8 q
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const ContribTile ct = contrib_tile(20 + wu + NWE * q, true);
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const double* row = L.X + (16 * kbk + 4 * s4 + kk) * XW;
-                facc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(row[ct.aoff + 16 * ct.ib + rr], row[ct.boff + 16 * ct.cb + rr],
-                                                               facc[q], 0, 0, 0);
-            }
-        }
-    };
+    // the Gram x^T x (5 x 5 of the 8 x columns, row block by row block) on one wave of helper B / H
+    const bool gram_on = !root && roleB && wu == (NH == 2 ? 6 : 3);
+    d4b gacc = {0.0, 0.0, 0.0, 0.0};
     // Panel data of panel kb -> registers, then LDS. The loads of panel kb + 1 are issued right after
     // the X update of panel kb, so their latency hides under the contributions; values that were still
     // empty (the factor workgroup had not stored them yet) are polled again at the panel's commit.
@@ -1877,6 +1935,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             if (rr < RC)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) L.X[(16 * kb + kk + 4 * g) * XW + 2 * BB + rr] = w[g];
+            if (pubX && rr < RC)  // helper A: x row block kb for the next level
+#pragma unroll
+                for (int g = 0; g < 4; ++g) st_pub(x_pub + (16 * kb + kk + 4 * g) * RC + rr, w[g]);
         }
 #pragma unroll
         for (int j = 0; j < MAXOWN; ++j) {
@@ -1902,13 +1963,17 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             if (16 * cb + rr < ncol)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) X[(16 * kb + kk + 4 * g) * XW + 16 * cb + rr] = w[g];
-            if (xl_on && roleA && cb < 4)
+            // the finished row block for the next level's pulls (no drain: the consumers poll the values)
+            if (cb < 4 ? pubL : (cb < 8 ? pubR : (pubX && rr < RC))) {
+                double* dst = cb < 4 ? xl_pub + 16 * cb : (cb < 8 ? xr_pub + 16 * (cb - 4) : x_pub);
+                const int ldd = cb < 8 ? BB : RC;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) st_pub(xlg + (16 * kb + kk + 4 * g) * BB + 16 * cb + rr, w[g]);
+                for (int g = 0; g < 4; ++g) st_pub(dst + (16 * kb + kk + 4 * g) * ldd + rr, w[g]);
+            }
         }
         __syncthreads();
         TLS(17 + 4 * kb);
-        // next panel's loads in flight under the contributions (values still empty are polled at its commit)
+        // next panel's loads in flight (values still empty are polled at its commit)
         if (kb < 3) issue(kb + 1);
         if (NH == 2 && wu > 4 + kb) {  // x_ii -= L(ii,kb) x_kb, ii = wave - 4
             const int ii = wu - 4;
@@ -1927,7 +1992,16 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                 for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + 2 * BB + rr] = acc[g];
         }
-        if (!root) contrib_rows(kb);
+        if (gram_on) {
+            double xv[4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const double v = L.X[(16 * kb + 4 * s4 + kk) * XW + 2 * BB + (rr & 7)];
+                xv[s4] = rr < RC ? v : 0.0;
+            }
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s4], xv[s4], gacc, 0, 0, 0);
+        }
         if constexpr (STAMP) __syncthreads();
         TLS(3 + 2 * kb);
     }
@@ -1969,62 +2043,45 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
         block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, true, Yl, L.byk, L.bybl);
         return;
     }
-#pragma unroll
-    for (int q = 0; q < NCT8; ++q) {
-        const int t = hm.tiles[q];
-        if (t < 0) continue;
-        const ContribTile ct = contrib_tile(t, has_r);
-        if (!ct.valid || (ct.rhs && rr >= RC)) continue;
-        if (ct.gram) {  // x^T x (5 x 5) -> Bp[i], published with this helper's flag
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                if (kk + 4 * g < 5 && rr < 5) st_pub(Bw.Bp + (size_t)i * 32 + (kk + 4 * g) * 5 + rr, cacc[q][g]);
-            continue;
-        }
-        double* dst = (t < 10 ? Bw.UL : t < 20 ? Bw.UR : t < 36 ? Bw.F : t < 40 ? Bw.rL : Bw.rR) +
-                      (size_t)i * (ct.rhs ? RSZ : BSZ);
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            st_pub(dst + (size_t)(16 * ct.ib + kk + 4 * g) * ct.ldd + 16 * ct.cb + rr, ct.sign * cacc[q][g]);
-    }
-    publish_flag((roleA || NH == 1) ? elim_f + i : elimB_f + i, epoch);
-    // helper A: its final XL (stored during the X updates) is drained by the same publication
-    if (xl_on && roleA && tid == 0) __hip_atomic_store((gu32*)(xl_f + i), 4 * epoch + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    TLS(10);
-    if (roleA) {
+    if (roleA) {  // helper A's rows are all published
+        TLS(10);
         TLS(11);
         return;
     }
+    // the Gram x^T x (5 x 5) -> Bp[i], published with its flag (the root sums every block's)
+    if (gram_on)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            if (kk + 4 * g < 5 && rr < 5) st_pub(Bw.Bp + (size_t)i * 32 + (kk + 4 * g) * 5 + rr, gacc[g]);
+    publish_flag(gram_f + i, epoch);
+    TLS(10);
     if (NH == 2) {
-        // the fill F = -XR^T XL after B's contributions are out (it is needed only by the next level's
-        // helpers, before their first panel); the back-substitution needs all of XL
-        if (!wait_ge(xl_f + i, 4 * epoch + 3, &L.ok)) {
+        // the back-substitution needs XL: helper A's published rows (out long ago; polled value by value)
+        const double* xs = pub_xl(Bw, epoch) + (size_t)i * BSZ;
+        unsigned long long xv[BSZ / TPB_E];
+#pragma unroll
+        for (int u = 0; u < BSZ / TPB_E; ++u) xv[u] = has_l ? ld_u64(xs + tid + TPB_E * u) : 0ull;
+        int okp = 1;
+        for (unsigned n = 0;; ++n) {
+            bool pend = false;
+#pragma unroll
+            for (int u = 0; u < BSZ / TPB_E; ++u) pend = pend || xv[u] == BCR_Y_EMPTY;
+            if (!pend) break;
+            if (n > SPIN_LIMIT) { okp = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int u = 0; u < BSZ / TPB_E; ++u)
+                if (xv[u] == BCR_Y_EMPTY) xv[u] = ld_u64(xs + tid + TPB_E * u);
+        }
+#pragma unroll
+        for (int u = 0; u < BSZ / TPB_E; ++u) {
+            const int e = tid + TPB_E * u;
+            L.X[(e >> 6) * XW + (e & 63)] = __longlong_as_double((long long)xv[u]);
+        }
+        if (!__syncthreads_and(okp)) {
             if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
             return;
         }
-        {
-            double xv[BSZ / TPB_E];
-#pragma unroll
-            for (int u = 0; u < BSZ / TPB_E; ++u) xv[u] = ld_pub(xlg + tid + TPB_E * u);
-#pragma unroll
-            for (int u = 0; u < BSZ / TPB_E; ++u) {
-                const int e = tid + TPB_E * u;
-                L.X[(e >> 6) * XW + (e & 63)] = xv[u];
-            }
-        }
-        __syncthreads();
-        if (fill_on) {
-#pragma unroll
-            for (int kbk = 0; kbk < 4; ++kbk) fill_rows(kbk);
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const ContribTile ct = contrib_tile(20 + wu + NWE * q, true);
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    st_pub(fbuf(Bw, epoch) + (size_t)i * BSZ + (size_t)(16 * ct.ib + kk + 4 * g) * BB + 16 * ct.cb + rr, -facc[q][g]);
-            }
-        }
-        publish_flag(fill_f + i, epoch);
         TLS(11);
     }
     // ---- off the critical path: [P | Q | u] = Cf^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
@@ -2178,6 +2235,7 @@ static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& 
         // the grid cannot be co-resident on this device: this context uses the per-level launches
         // (the k_final of this iteration sees persist == 0 and advances no epoch)
         Bw.persist = 0;
+        CKB(bcr_reset_pull_slots(Bw, false, s));
         return launch_per_level<STAMP>(P, c, W, Bw, s, stamps, pf);
     }
     if (Bw.persist) {
@@ -2224,6 +2282,18 @@ static hipError_t bcr_persist_attr() {
         for (const void* f : fns) CKB(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(HLds)));
         done = true;
     }
+    return hipSuccess;
+}
+
+// k_bcr_split's pull slots (published XL / XR / x rows, two epochs: UL | UR | F, rL | rR, F2) start empty;
+// the per-level and persistent paths use the same buffers for their contributions and need zeros there
+// (the upper tiles of UL / UR are read, never written)
+hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s) {
+    const size_t b64 = (size_t)BSZ * Bw.nblk, b8 = (size_t)RSZ * Bw.nblk;
+    const unsigned pat = split ? BCR_Y_EMPTY_D32 : 0u;
+    CKB(hipMemsetD32Async((hipDeviceptr_t)Bw.UL, pat, 2 * 3 * b64, s));  // UL | UR | F
+    CKB(hipMemsetD32Async((hipDeviceptr_t)Bw.rL, pat, 2 * 2 * b8, s));   // rL | rR
+    CKB(hipMemsetD32Async((hipDeviceptr_t)Bw.F2, pat, 2 * b64, s));
     return hipSuccess;
 }
 

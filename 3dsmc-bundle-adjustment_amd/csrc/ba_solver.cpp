@@ -459,7 +459,8 @@ static size_t bcr_bytes(int nblk) {
 }
 
 // k_bcr_split's hand-off state: the flags (epoch 0) and the flag-free buffers, which start empty (BCR_Y_EMPTY):
-// y (Racc | Y, epoch parity), the published panels (Cf | X slots, two epochs) and the odd epochs' fill
+// y (Racc | Y, epoch parity), the published panels (Cf | X slots, two epochs) and the published X rows of the
+// pull hand-off (bcr_reset_pull_slots: zeros instead when another BCR path runs)
 static int bcr_init_handoffs(ba_context* ctx) {
     const BcrWork& Bw = ctx->W.bcr;
     const size_t b64 = (size_t)64 * 64 * Bw.nblk, b8 = (size_t)64 * 8 * Bw.nblk;
@@ -467,7 +468,7 @@ static int bcr_init_handoffs(ba_context* ctx) {
     HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
     HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Racc, BCR_Y_EMPTY_D32, 4 * b8, s));
     HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.Cf, BCR_Y_EMPTY_D32, 2 * (b64 + (size_t)64 * BCR_XW * Bw.nblk), s));
-    HIPCHECK(ctx, hipMemsetD32Async((hipDeviceptr_t)Bw.F2, BCR_Y_EMPTY_D32, 2 * b64, s));
+    HIPCHECK(ctx, bcr_reset_pull_slots(Bw, Bw.persist >= 2, s));
     ctx->bcr_launches = 0;
     return BA_OK;
 }
@@ -792,13 +793,13 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         Bw.F2 = Bw.rd + (size_t)64 * bcr_nblk;
         Bw.bk = Bw.F2 + b64;
         Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
-        if (int rc = bcr_init_handoffs(ctx)) return rc;
         Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
         if (const char* e = std::getenv("MIBA_BCR")) {
             if (!std::strcmp(e, "launch")) Bw.persist = 0;
             else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
             else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;  // "split3" or unset: default
         }
+        if (int rc = bcr_init_handoffs(ctx)) return rc;
     }
     DevWork& W = ctx->W;
     W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
@@ -990,6 +991,7 @@ static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     Bw.persist = 0;
     ctx->bcr_fallback = true;
     if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
+    HIPCHECK(ctx, bcr_reset_pull_slots(Bw, false, s));
     S.done = 0;
     S.termination = -1;
     S.msg = MSG_NONE;
