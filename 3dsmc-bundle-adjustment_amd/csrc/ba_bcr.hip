@@ -1224,7 +1224,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_persist(const LmState* __restrict
 // block kb; it publishes the contributions, then runs the back-substitution from its copy of L.
 // F's pivot chain thus no longer shares its CU's f64 pipes with the 136-column MFMA work.
 // Hand-offs as in k_bcr_persist; panel flags hold 4 * epoch + kb (monotone, polled with >=).
-static constexpr int SG_LD = 66;         // LDS row stride of pulled 64-column row blocks (pull_rows)
+static constexpr int SG_LD = 66;         // LDS row stride of pulled 64-column row blocks (Pull)
 static constexpr int SG_W = 16 * SG_LD;  // one staged 16 x 64 row block
 struct FLds {
     double T[BB * BLD];
@@ -1327,42 +1327,19 @@ struct PullSrc {
     const double* x[NX > 0 ? NX : 1];  // 8-column sources (64 x 8)
 };
 // Row block kb of every source -> LDS sg (64-column sources at sg + k SG_W, row stride SG_LD, then the
-// 8-column ones, 128 each). ONE lane first waits for each live source's last entry of the row block (so the
-// workgroup does not load the memory path the producers store through while it waits), then every thread
-// loads its entries and re-polls those still empty. Also the barrier that ends the previous row block's
-// reads of sg. Uniform result; false on timeout.
+// 8-column ones, 128 each). issue(kb) puts this thread's loads in flight (the caller issues row block kb + 1
+// right after committing kb, so the loads overlap its MFMAs); commit(kb) re-polls the values still empty and
+// stores the row block to LDS. With `probe`, while some value is still empty ONE lane first waits for each
+// live source's last entry of the row block (all in flight per round trip), so a long wait does not load the
+// memory path the producers store through. commit's first barrier also ends the previous row block's reads of
+// sg. Uniform result; false on timeout.
 template <int NW, int NX>
-__device__ bool pull_rows(const PullSrc<NW, NX>& ps, int kb, double* sg, int* lds_ok, unsigned spin_lim) {
-    const int tid = threadIdx.x;
-    if (tid == 0) {  // every live source's probe in flight per round trip
-        const double* pp[NW + NX];
-        unsigned long long pv[NW + NX];
-#pragma unroll
-        for (int k = 0; k < NW + NX; ++k) {
-            const double* p = k < NW ? ps.w[k] : ps.x[k - NW];
-            pp[k] = p ? p + (k < NW ? (16 * kb + 15) * BB + BB - 1 : (16 * kb + 15) * RC + RC - 1) : nullptr;
-            pv[k] = pp[k] ? ld_u64(pp[k]) : 0ull;
-        }
-        int ok = 1;
-        for (unsigned n = 0;; ++n) {
-            bool pend = false;
-#pragma unroll
-            for (int k = 0; k < NW + NX; ++k) pend = pend || pv[k] == BCR_Y_EMPTY;
-            if (!pend) break;
-            if (n > SPIN_LIMIT) { ok = 0; break; }
-            __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-            for (int k = 0; k < NW + NX; ++k)
-                if (pv[k] == BCR_Y_EMPTY) pv[k] = ld_u64(pp[k]);
-        }
-        *lds_ok = ok;
-    }
-    __syncthreads();
-    if (!*lds_ok) return false;
-    constexpr int NE = NW * 1024 + NX * 128, NU = (NE + TPB_E - 1) / TPB_E;
+struct Pull {
+    static constexpr int NE = NW * 1024 + NX * 128, NU = (NE + TPB_E - 1) / TPB_E;
+    unsigned long long v[NU];
     // the source of entry u is uniform over the workgroup (64-column part) or a wave (8-column part)
-    auto gaddr = [&](int u) -> const double* {
-        const int e = tid + TPB_E * u;
+    __device__ __forceinline__ const double* gaddr(const PullSrc<NW, NX>& ps, int kb, int u) const {
+        const int e = threadIdx.x + TPB_E * u;
         if (e < NW * 1024) {
             const double* p = ps.w[e >> 10];
             return p ? p + (16 * kb + ((e >> 6) & 15)) * BB + (e & 63) : nullptr;
@@ -1375,34 +1352,68 @@ __device__ bool pull_rows(const PullSrc<NW, NX>& ps, int kb, double* sg, int* ld
             }
         }
         return nullptr;
-    };
-    unsigned long long v[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        const double* a = gaddr(u);
-        v[u] = a ? ld_u64(a) : 0ull;
     }
-    int ok = 1;
-    for (unsigned n = 0;; ++n) {
+    __device__ __forceinline__ void issue(const PullSrc<NW, NX>& ps, int kb) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const double* a = gaddr(ps, kb, u);
+            v[u] = a ? ld_u64(a) : 0ull;
+        }
+    }
+    __device__ bool commit(const PullSrc<NW, NX>& ps, int kb, double* sg, int* lds_ok, unsigned spin_lim, bool probe) {
+        const int tid = threadIdx.x;
         bool pend = false;
 #pragma unroll
         for (int u = 0; u < NU; ++u) pend = pend || v[u] == BCR_Y_EMPTY;
-        if (!pend) break;
-        if (n > SPIN_LIMIT) { ok = 0; break; }
-        __builtin_amdgcn_s_sleep(1);
+        if (__syncthreads_or(pend) && probe) {
+            if (tid == 0) {
+                const double* pp[NW + NX];
+                unsigned long long pv[NW + NX];
 #pragma unroll
-        for (int u = 0; u < NU; ++u)
-            if (v[u] == BCR_Y_EMPTY) v[u] = ld_u64(gaddr(u));
-    }
+                for (int k = 0; k < NW + NX; ++k) {
+                    const double* p = k < NW ? ps.w[k] : ps.x[k - NW];
+                    pp[k] = p ? p + (k < NW ? (16 * kb + 15) * BB + BB - 1 : (16 * kb + 15) * RC + RC - 1) : nullptr;
+                    pv[k] = pp[k] ? ld_u64(pp[k]) : 0ull;
+                }
+                int ok = 1;
+                for (unsigned n = 0;; ++n) {
+                    bool pw = false;
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        const int e = tid + TPB_E * u;
-        const double d = __longlong_as_double((long long)v[u]);
-        if (e < NW * 1024) sg[(e >> 10) * SG_W + ((e >> 6) & 15) * SG_LD + (e & 63)] = d;
-        else if (e < NE) sg[NW * SG_W + (e - NW * 1024)] = d;
+                    for (int k = 0; k < NW + NX; ++k) pw = pw || pv[k] == BCR_Y_EMPTY;
+                    if (!pw) break;
+                    if (n > SPIN_LIMIT) { ok = 0; break; }
+                    __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+                    for (int k = 0; k < NW + NX; ++k)
+                        if (pv[k] == BCR_Y_EMPTY) pv[k] = ld_u64(pp[k]);
+                }
+                *lds_ok = ok;
+            }
+            __syncthreads();
+            if (!*lds_ok) return false;
+        }
+        int ok = 1;
+        for (unsigned n = 0;; ++n) {
+            bool pe = false;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) pe = pe || v[u] == BCR_Y_EMPTY;
+            if (!pe) break;
+            if (n > SPIN_LIMIT) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int u = 0; u < NU; ++u)
+                if (v[u] == BCR_Y_EMPTY) v[u] = ld_u64(gaddr(ps, kb, u));
+        }
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int e = tid + TPB_E * u;
+            const double d = __longlong_as_double((long long)v[u]);
+            if (e < NW * 1024) sg[(e >> 10) * SG_W + ((e >> 6) & 15) * SG_LD + (e & 63)] = d;
+            else if (e < NE) sg[NW * SG_W + (e - NW * 1024)] = d;
+        }
+        return __syncthreads_and(ok);
     }
-    return __syncthreads_and(ok);
-}
+};
 
 #define TLS(k)                                                                                     \
     do {                                                                                           \
@@ -1488,7 +1499,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             if (tid < BB) nx[BB * BB + 4 * 256 + tid] = BCR_Y_EMPTY;
         }
         // survived levels: D_i -= XR_a^T XR_a + XL_b^T XL_b, pulled row block by row block from the rows the
-        // eliminated neighbours' helpers publish (pull_rows); lower tiles wq and wq + 8 on wave wq
+        // eliminated neighbours' helpers publish (Pull); lower tiles wq and wq + 8 on wave wq
         for (int m = 0; m < mi; ++m) {
             const int s = 1 << m, a = i - s, b = i + s;
             PullSrc<2, 0> ps;
@@ -1505,11 +1516,16 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 tjb[q] = t;
             }
             d4b acc[2] = {d4b{0.0, 0.0, 0.0, 0.0}, d4b{0.0, 0.0, 0.0, 0.0}};
+            Pull<2, 0> pl;
+            pl.issue(ps, 0);
             for (int kb = 0; kb < 4; ++kb) {
-                if (!pull_rows(ps, kb, L.sg, &L.ok, spin_lim)) {
+                // the probe only for the first row block (the level's long wait): the later ones arrive at the
+                // producers' panel pace, and 4 values per thread are polled directly
+                if (!pl.commit(ps, kb, L.sg, &L.ok, spin_lim, kb == 0)) {
                     if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                     return;
                 }
+                if (kb < 3) pl.issue(ps, kb + 1);
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     if (wq + NWE * q >= 10) continue;
@@ -1744,7 +1760,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     }
     if (root && tid < 14) L.bk[tid] = bkv;
     // Survived levels: the Schur terms of the level's eliminated neighbours a = i - s, b = i + s, pulled row
-    // block by row block (pull_rows; staging in L / rdiag / W, which hold nothing before the first panel):
+    // block by row block (Pull; staging in L / rdiag / W, which hold nothing before the first panel):
     //   x -= XR_a^T x_a + XL_b^T x_b              (x waves: row block wu - xw0; one chain over the row blocks)
     //   last level: XL = -XR_a^T XL_a (helper A / H waves 0-3: column tile wu)
     //               XR = -XL_b^T XR_b (helper B waves 0-3 / H waves 4-7: column tile wu & 3)
@@ -1775,11 +1791,14 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             d4b facc[4];
 #pragma unroll
             for (int ii = 0; ii < 4; ++ii) facc[ii] = d4b{0.0, 0.0, 0.0, 0.0};
+            Pull<4, 2> pl;
+            pl.issue(ps, 0);
             for (int kb = 0; kb < 4; ++kb) {
-                if (!pull_rows(ps, kb, sg, &L.ok, spin_lim)) {
+                if (!pl.commit(ps, kb, sg, &L.ok, spin_lim, true)) {
                     if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
                     return;
                 }
+                if (kb < 3) pl.issue(ps, kb + 1);
                 if (xwave) {
 #pragma unroll
                     for (int src = 0; src < 2; ++src) {

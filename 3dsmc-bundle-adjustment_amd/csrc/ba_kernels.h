@@ -73,6 +73,14 @@ struct DevProblem {
     const int* co_pt;
     const double2* co_uv;
     const double* co_depth;
+    // obs32 windows — every admissible pixel coordinate and depth exactly representable in f32, as the reference's
+    // are (cv::KeyPoint::pt is float, the depth comes from a float image: OptimizationUtils.cpp:261-262,
+    // Map3D.cpp:85-88): one 16-byte record per observation, {u, v, depth, camera index} point-major and
+    // {u, v, depth, point index} camera-major (the index as the float's bits), read in one load instead of the
+    // f64 arrays po_cam / po_uv / po_depth and co_pt / co_uv / co_depth (28 -> 16 bytes per observation and sweep)
+    const float4* po_rec;
+    const float4* co_rec;
+    int obs32;
     const int* seg_ptr;  // [n_seg+1]
     const int* seg_cam;  // [n_seg]
     const int* seg_ac;   // [n_seg]
@@ -118,7 +126,7 @@ static constexpr int BCR_CAMS = 10;
 // plus one global slot: bk = [b_k (4) | S_kk lower (10)].
 struct BcrWork {
     double *Cf, *X, *UL, *UR, *F, *rL, *rR, *Dacc, *Racc, *Y, *Bp, *rd, *bk;
-    double* F2;  // k_bcr_split (two helpers): the fill F of odd epochs (flag-free hand-off)
+    double* F2;  // k_bcr_split: the published XR rows of odd epochs (flag-free pull hand-off)
     // persistent path: flags[0] = call epoch, flags[16 + i] = block i eliminated (helper A's part
     // when split 3-way), flags[16 + nblk + i] = block i back-substituted, [16 + 2 nblk + i] panels
     // published, [16 + 3 nblk + i] helper B's part, [16 + 4 nblk + i] fill F, [16 + 5 nblk + i] XL

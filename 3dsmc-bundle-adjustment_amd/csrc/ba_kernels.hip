@@ -35,6 +35,46 @@ namespace miba {
 
 static constexpr int TPB = 256;
 
+// Observation record as loaded (ObsRaw<O32>): O32 = the window's obs32 records (one 16-byte load), else the f64
+// arrays; u / v / depth widen to f64 exactly, so both paths run the same arithmetic.
+template <bool O32>
+struct ObsRaw;
+template <>
+struct ObsRaw<true> {
+    float4 r;
+    __device__ __forceinline__ double u() const { return (double)r.x; }
+    __device__ __forceinline__ double v() const { return (double)r.y; }
+    __device__ __forceinline__ double d() const { return (double)r.z; }
+    __device__ __forceinline__ int idx() const { return __float_as_int(r.w); }
+};
+template <>
+struct ObsRaw<false> {
+    double2 uv;
+    double dep;
+    int i;
+    __device__ __forceinline__ double u() const { return uv.x; }
+    __device__ __forceinline__ double v() const { return uv.y; }
+    __device__ __forceinline__ double d() const { return dep; }
+    __device__ __forceinline__ int idx() const { return i; }
+};
+// point-major observation o: pixel, depth, camera index
+template <bool O32>
+__device__ __forceinline__ ObsRaw<O32> po_obs(const DevProblem& P, int o) {
+    if constexpr (O32) return ObsRaw<true>{P.po_rec[o]};
+    else return ObsRaw<false>{P.po_uv[o], P.po_depth[o], P.po_cam[o]};
+}
+// camera-major observation o: pixel, depth, point index
+template <bool O32>
+__device__ __forceinline__ ObsRaw<O32> co_obs(const DevProblem& P, int o) {
+    if constexpr (O32) return ObsRaw<true>{P.co_rec[o]};
+    else return ObsRaw<false>{P.co_uv[o], P.co_depth[o], P.co_pt[o]};
+}
+template <bool O32>
+__device__ __forceinline__ ObsRaw<O32> obs_zero() {
+    if constexpr (O32) return ObsRaw<true>{float4{0.f, 0.f, 0.f, 0.f}};
+    else return ObsRaw<false>{double2{0.0, 0.0}, 0.0, 0};
+}
+
 
 // Block (256 threads) sum of NV values; result valid in out[0..NV) after return (LDS).
 template <int NV>
@@ -102,6 +142,7 @@ __device__ __forceinline__ int xcd_seg(int b, int first, int n) {
 // camera-major observation list; k_cam_finalize sums a camera's sub-segments in order.
 // camdata (per sub-segment partial here): U upper-packed (21), C (6x4 = 24), g (6)
 // seg_intr[s*SEGINTR + ..]: Ukk upper-packed (10), gk (4), cost (1)
+template <bool O32>
 __device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                                int gated, double* __restrict__ camdata, double* __restrict__ seg_intr,
                                                double* __restrict__ gmax_word, const int s) {
@@ -122,34 +163,28 @@ __device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaCons
 #pragma unroll
     for (int i = 0; i < CAM_NZ; ++i) acc[i] = 0.0;
     const int o0 = P.seg_ptr[s], o1 = P.seg_ptr[s + 1];
-    // software pipeline: point index two observations ahead, point / pixel / depth one ahead
+    // software pipeline: observation record (point index, pixel, depth) two observations ahead, point one ahead
     const int oa = o0 + threadIdx.x;
-    int pt_n = oa < o1 ? P.co_pt[oa] : 0;
-    const int pt_nn = oa + TPB < o1 ? P.co_pt[oa + TPB] : 0;
-    double X_n[3] = {0.0, 0.0, 0.0}, dep_n = 0.0;
-    double2 uv_n = double2{0.0, 0.0};
+    ObsRaw<O32> r_n = oa < o1 ? co_obs<O32>(P, oa) : obs_zero<O32>();
+    ObsRaw<O32> r_nn = oa + TPB < o1 ? co_obs<O32>(P, oa + TPB) : obs_zero<O32>();
+    double X_n[3] = {0.0, 0.0, 0.0};
     if (oa < o1) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) X_n[k] = pts[3 * pt_n + k];
-        uv_n = P.co_uv[oa];
-        dep_n = P.co_depth[oa];
+        for (int k = 0; k < 3; ++k) X_n[k] = pts[3 * r_n.idx() + k];
     }
-    pt_n = pt_nn;
     for (int o = oa; o < o1; o += TPB) {
         const double X[3] = {X_n[0], X_n[1], X_n[2]};
-        const double2 uv = uv_n;
-        const double dep = dep_n;
+        const ObsRaw<O32> r = r_n;
         const int on = o + TPB;
         if (on < o1) {
+            r_n = r_nn;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) X_n[k] = pts[3 * pt_n + k];
-            uv_n = P.co_uv[on];
-            dep_n = P.co_depth[on];
-            pt_n = on + TPB < o1 ? P.co_pt[on + TPB] : 0;
+            for (int k = 0; k < 3; ++k) X_n[k] = pts[3 * r_n.idx() + k];
+            r_nn = on + TPB < o1 ? co_obs<O32>(P, on + TPB) : obs_zero<O32>();
         }
         ObsEval e;
         double jc[18], jp[9], jk[8];
-        lin_obs(c, pose, X, K, uv.x, uv.y, dep, e, jc, jp, jk);
+        lin_obs(c, pose, X, K, r.u(), r.v(), r.d(), e, jc, jp, jk);
         (void)jp;
         cam_accum(acc, jc, jk, e.f, e.ok ? e.cost : __builtin_nan(""), ac >= 0);
     }
@@ -158,10 +193,11 @@ __device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaCons
         for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)s * CAMDATA + i] = cam_unpack(out, i);
     for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = cam_unpack(out, CAMDATA + i);
 }
+template <bool O32>
 __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
                                                   double* __restrict__ camdata, double* __restrict__ seg_intr,
                                                   double* __restrict__ gmax_word) {
-    cam_side_block(P, c, st, gated, camdata, seg_intr, gmax_word, P.xcd_map ? xcd_seg(blockIdx.x, 0, P.n_seg) : (int)blockIdx.x);
+    cam_side_block<O32>(P, c, st, gated, camdata, seg_intr, gmax_word, P.xcd_map ? xcd_seg(blockIdx.x, 0, P.n_seg) : (int)blockIdx.x);
 }
 
 // One launch for what follows the camera-side pass (was k_cam_reduce + k_lin_finalize):
@@ -488,13 +524,13 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
              lin_w);
 }
 
-template <int PP_LANES>
+template <int PP_LANES, bool O32>
 __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                                  int mode, const double* __restrict__ scale, double* __restrict__ cnp,
                                                  double* __restrict__ pdata, double* __restrict__ part, const int b);
 // Workgroups >= nb_pp assemble the envelope tiles of S (env_tile; independent of the point records),
 // so the assembly needs no launch of its own.
-template <int PP_LANES>
+template <int PP_LANES, bool O32>
 __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c, const LmState* __restrict__ st, int mode,
                                                        const double* __restrict__ scale, double* __restrict__ cnp,
                                                        double* __restrict__ pdata, double* __restrict__ S,
@@ -511,10 +547,10 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
                      camdata_w, lin_w);
         return;
     }
-    point_prep_block<PP_LANES>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
+    point_prep_block<PP_LANES, O32>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
 }
 // Point-side body of k_point_prep for point workgroup b (see k_point_prep).
-template <int PP_LANES>
+template <int PP_LANES, bool O32>
 __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                                  int mode, const double* __restrict__ scale, double* __restrict__ cnp,
                                                  double* __restrict__ pdata, double* __restrict__ part, const int b) {
@@ -539,37 +575,31 @@ __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaCo
 #pragma unroll
         for (int i = 0; i < 21; ++i) acc[i] = 0.0;
         const int o1 = P.pt_ptr[ap + 1];
-        // software pipeline: camera index two observations ahead, pose / pixel / depth one ahead
+        // software pipeline: observation record (camera index, pixel, depth) two observations ahead, pose one ahead
         const double* cams = P.cams[cur];
         const int o0 = P.pt_ptr[ap] + q;
-        int cam_n = o0 < o1 ? P.po_cam[o0] : 0;
-        const int cam_nn = o0 + PP_LANES < o1 ? P.po_cam[o0 + PP_LANES] : 0;
-        double pose_n[7], dep_n = 0.0;
-        double2 uv_n = double2{0.0, 0.0};
+        ObsRaw<O32> r_n = o0 < o1 ? po_obs<O32>(P, o0) : obs_zero<O32>();
+        ObsRaw<O32> r_nn = o0 + PP_LANES < o1 ? po_obs<O32>(P, o0 + PP_LANES) : obs_zero<O32>();
+        double pose_n[7];
         if (o0 < o1) {
 #pragma unroll
-            for (int k = 0; k < 7; ++k) pose_n[k] = cams[7 * cam_n + k];
-            uv_n = P.po_uv[o0];
-            dep_n = P.po_depth[o0];
+            for (int k = 0; k < 7; ++k) pose_n[k] = cams[7 * r_n.idx() + k];
         }
-        cam_n = cam_nn;
         for (int o = o0; o < o1; o += PP_LANES) {
             double pose[7];
 #pragma unroll
             for (int k = 0; k < 7; ++k) pose[k] = pose_n[k];
-            const double2 uv = uv_n;
-            const double dep = dep_n;
+            const ObsRaw<O32> r = r_n;
             const int on = o + PP_LANES;
             if (on < o1) {
+                r_n = r_nn;
 #pragma unroll
-                for (int k = 0; k < 7; ++k) pose_n[k] = cams[7 * cam_n + k];
-                uv_n = P.po_uv[on];
-                dep_n = P.po_depth[on];
-                cam_n = on + PP_LANES < o1 ? P.po_cam[on + PP_LANES] : 0;
+                for (int k = 0; k < 7; ++k) pose_n[k] = cams[7 * r_n.idx() + k];
+                r_nn = on + PP_LANES < o1 ? po_obs<O32>(P, on + PP_LANES) : obs_zero<O32>();
             }
             ObsEval ev;
             double jc[18], jp[9], jk[8];
-            lin_obs(c, pose, X, K, uv.x, uv.y, dep, ev, jc, jp, jk);
+            lin_obs(c, pose, X, K, r.u(), r.v(), r.d(), ev, jc, jp, jk);
             (void)jc;
             acc[0] += jp[0] * jp[0] + jp[3] * jp[3] + jp[6] * jp[6];
             acc[1] += jp[0] * jp[1] + jp[3] * jp[4] + jp[6] * jp[7];
@@ -621,14 +651,14 @@ __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaCo
 // (IterationZero): the points' column norms and the ungated camera side. The point
 // side alone is one long dependent chain per thread at ~1.5 waves per SIMD; the camera sub-segments fill
 // the CUs it leaves idle. The envelope tiles, which need the camera sums, ride in k_schur_tile.
-template <int PP_LANES>
+template <int PP_LANES, bool O32>
 __global__ __launch_bounds__(TPB) void k_lin_point(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                    const double* __restrict__ scale, double* __restrict__ cnp,
                                                    double* __restrict__ pdata, double* __restrict__ part, int nb_pp,
                                                    double* __restrict__ cpart, double* __restrict__ seg_intr,
                                                    double* __restrict__ gmax_word, int mode) {
-    if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
-    else cam_side_block(P, c, st, mode, cpart, seg_intr, gmax_word,
+    if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES, O32>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
+    else cam_side_block<O32>(P, c, st, mode, cpart, seg_intr, gmax_word,
                         P.xcd_map ? xcd_seg(blockIdx.x, nb_pp, P.n_seg) : (int)blockIdx.x - nb_pp);
 }
 
@@ -819,7 +849,7 @@ struct EnvArgs {
     int fin;  // 1: unsharded (finish the camera sums, lin); 2: landmark shard (local terms for the exchange)
 };
 
-template <bool STAMP>
+template <bool STAMP, bool O32>
 __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
@@ -913,13 +943,12 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
     const int n_last = P.n_adm - 1;
     // level 1: observation record of this thread
-    int r_ac, r_ap, r_cam, r_pt;
-    double2 r_uv;
-    double r_dep;
+    int r_ac, r_ap, r_pt;
+    ObsRaw<O32> r_o;  // camera index, pixel, depth
     auto load_rec = [&](int qq) {
         const int qc = qq < n_last ? qq : n_last;
-        r_ac = P.po_ac[qc]; r_ap = P.po_ap[qc]; r_cam = P.po_cam[qc]; r_pt = P.po_pt[qc];
-        r_uv = P.po_uv[qc]; r_dep = P.po_depth[qc];
+        r_ac = P.po_ac[qc]; r_ap = P.po_ap[qc]; r_pt = P.po_pt[qc];
+        r_o = po_obs<O32>(P, qc);
     };
     // level 2: operands of the observation
     double o_pose[7], o_X[3], o_sc[6], o_sp[3], o_G[6];
@@ -927,7 +956,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     auto load_ops = [&](bool ok) {
         o_ok = ok;
         const int ac = ok ? r_ac : 0, ap = ok ? r_ap : 0;
-        const double* pose = P.cams[cur] + 7 * (ok ? r_cam : 0);
+        const double* pose = P.cams[cur] + 7 * (ok ? r_o.idx() : 0);
         const double* X = P.pts[cur] + 3 * (ok ? r_pt : 0);
 #pragma unroll
         for (int k = 0; k < 7; ++k) o_pose[k] = pose[k];
@@ -973,7 +1002,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             const int pl = r_ap - apb;
             ObsEval ev;
             double jc[18], jp[9], jk[8];
-            lin_obs(c, o_pose, o_X, K, r_uv.x, r_uv.y, r_dep, ev, jc, jp, jk);
+            lin_obs(c, o_pose, o_X, K, r_o.u(), r_o.v(), r_o.d(), ev, jc, jp, jk);
             double W[18];
             w_tilde(jc, jp, o_sc, o_sp, W);
             const double g00 = o_G[0], g10 = o_G[1], g11 = o_G[2], g20 = o_G[3], g21 = o_G[4], g22 = o_G[5];
@@ -1765,6 +1794,7 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
 // The points' share of the model cost change, 0.5 (e~^T y_p + y_p^T D~_p y_p), is summed in phase 2
 // (k_update_cams states the identity).
 // A chunk holding a single point with more than BS_OBS observations sums c_o by block reduction.
+template <bool O32>
 __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                        const double* __restrict__ scale,
                                                        const double* __restrict__ pdata, const double* __restrict__ y,
@@ -1794,25 +1824,24 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
     // each thread's observation records (<= BS_OBS / TPB of them) are read once, in phase 1, and kept in
     // registers for phase 3 (a single point with more observations re-reads its records in phase 3)
     constexpr int NR = BS_OBS / TPB;
-    int r_cam[NR], r_ap[NR];
-    double2 r_uv[NR];
-    double r_dep[NR];
+    int r_ap[NR];
+    ObsRaw<O32> r_o[NR];  // camera index, pixel, depth
     // ---- phase 1
     double bsum[3] = {0.0, 0.0, 0.0};
     int it = 0;
     for (int o = ob + tid; o < oe; o += TPB, ++it) {
         const int ac = P.po_ac[o];
-        const int cam = P.po_cam[o], ap = P.po_ap[o];
-        const double2 uv = P.po_uv[o];
-        const double dep = P.po_depth[o];
+        const int ap = P.po_ap[o];
+        const ObsRaw<O32> ro = po_obs<O32>(P, o);
+        const int cam = ro.idx();
 #pragma unroll
         for (int k = 0; k < NR; ++k)  // register arrays: constant indices only
-            if (k == it) { r_cam[k] = cam; r_ap[k] = ap; r_uv[k] = uv; r_dep[k] = dep; }
+            if (k == it) { r_ap[k] = ap; r_o[k] = ro; }
         double v[3] = {0.0, 0.0, 0.0};
         if (ac >= 0) {
             ObsEval ev;
             double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * cam, P.pts[cur] + 3 * P.pt_idx[ap], K, uv.x, uv.y, dep, ev, jc, jp, jk);
+            lin_obs(c, P.cams[cur] + 7 * cam, P.pts[cur] + 3 * P.pt_idx[ap], K, ro.u(), ro.v(), ro.d(), ev, jc, jp, jk);
             const double* sc = scale + 6 * ac;
             const double* yc = y + 6 * ac;
             const double* sp = scale + P.off_pt + 3 * ap;
@@ -1875,21 +1904,22 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
     (void)delta;
     it = 0;
     for (int o = ob + tid; o < oe; o += TPB, ++it) {
-        int cam, ap;
-        double2 uv;
-        double dep;
+        int ap;
+        ObsRaw<O32> ro;
         if (it < NR) {
 #pragma unroll
             for (int k = 0; k < NR; ++k)  // register arrays: constant indices only
-                if (k == it) { cam = r_cam[k]; ap = r_ap[k]; uv = r_uv[k]; dep = r_dep[k]; }
+                if (k == it) { ap = r_ap[k]; ro = r_o[k]; }
         } else {
-            cam = P.po_cam[o]; ap = P.po_ap[o]; uv = P.po_uv[o]; dep = P.po_depth[o];
+            ap = P.po_ap[o];
+            ro = po_obs<O32>(P, o);
         }
+        const int cam = ro.idx();
         const int pl = ap - apb;
         const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
         const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
         ObsEval en;
-        eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, uv.x, uv.y, dep, en);
+        eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, ro.u(), ro.v(), ro.d(), en);
         if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
     }
     if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
@@ -2281,6 +2311,13 @@ static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
         CK(hipGetLastError());              \
     } while (0)
 
+// the observation kernels' obs32 (record) instantiation on obs32 windows, the f64 one otherwise
+#define OPL(kid, KT, KF, ...)                          \
+    do {                                               \
+        if (P.obs32) PL(kid, KT, __VA_ARGS__);         \
+        else PL(kid, KF, __VA_ARGS__);                 \
+    } while (0)
+
 // all-reduce on the solver stream, timed as K_COMM
 #define COMM(send, recv, n, t, op)                                             \
     do {                                                                        \
@@ -2311,11 +2348,11 @@ static hipError_t launch_point_prep(const DevProblem& P, const BaConsts& c, int 
     const int fin = W.comm.on() ? 0 : 1;         // unsharded: they also finish the camera-side sums
     const dim3 g(nb + n_env), b(PP_TPB);
     switch (pp_lanes()) {
-        case 1: PL(kid, k_point_prep<1>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
+        case 1: OPL(kid, (k_point_prep<1, true>), (k_point_prep<1, false>), g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
                    W.env_tile, W.camdata, W.lin, W.chol_flag, fin, W.camdata_part, W.seg_intr, W.camdata, W.lin); break;
-        case 2: PL(kid, k_point_prep<2>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
+        case 2: OPL(kid, (k_point_prep<2, true>), (k_point_prep<2, false>), g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
                    W.env_tile, W.camdata, W.lin, W.chol_flag, fin, W.camdata_part, W.seg_intr, W.camdata, W.lin); break;
-        default: PL(kid, k_point_prep<4>, g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
+        default: OPL(kid, (k_point_prep<4, true>), (k_point_prep<4, false>), g, b, 0, s, P, c, W.st, mode, W.scale, W.cnp, W.pdata, W.S, W.rhs, W.part, nb,
                     W.env_tile, W.camdata, W.lin, W.chol_flag, fin, W.camdata_part, W.seg_intr, W.camdata, W.lin); break;
     }
     return hipSuccess;
@@ -2329,7 +2366,7 @@ int schur_tile_slots() {
     int dev = 0, ncu = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_schur_tile<false>, TPB, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_schur_tile<false, true>, TPB, 0) != hipSuccess) return 0;
     return per_cu * ncu;
 }
 
@@ -2339,11 +2376,11 @@ static hipError_t launch_lin_point(const DevProblem& P, const BaConsts& c, int m
     const int nb = pp_blocks(P.n_ap);
     const int kid = mode ? K_LIN_POINT : K_CAM_SIDE;
     if (nb + P.n_seg > 0) switch (pp_lanes()) {
-        case 1: PL(kid, k_lin_point<1>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
+        case 1: OPL(kid, (k_lin_point<1, true>), (k_lin_point<1, false>), dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
                    W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
-        case 2: PL(kid, k_lin_point<2>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
+        case 2: OPL(kid, (k_lin_point<2, true>), (k_lin_point<2, false>), dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
                    W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
-        default: PL(kid, k_lin_point<4>, dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
+        default: OPL(kid, (k_lin_point<4, true>), (k_lin_point<4, false>), dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
                     W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
     }
     return hipSuccess;
@@ -2359,7 +2396,7 @@ hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, D
         CK(launch_lin_point(P, c, 0, W, s, pf));
         if (P.n_seg == 0) CK(hipMemsetAsync(W.lin + 1, 0, sizeof(double), s));
     } else if (P.n_seg > 0)
-        PL(K_CAM_SIDE, k_cam_side, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr,
+        OPL(K_CAM_SIDE, k_cam_side<true>, k_cam_side<false>, dim3(P.n_seg), dim3(TPB), 0, s, P, c, W.st, gated, W.camdata_part, W.seg_intr,
            W.lin + 1);
     else
         CK(hipMemsetAsync(W.lin + 1, 0, sizeof(double), s));
@@ -2420,15 +2457,24 @@ __global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, in
         const int cam = R.cam[k];
         const_cast<int*>(P.po_cam)[q] = cam;
         const_cast<int*>(P.po_ac)[q] = R.cam_ac[cam];
-        const_cast<double2*>(P.po_uv)[q] = R.uv[k];
-        const_cast<double*>(P.po_depth)[q] = R.depth[k];
+        const double2 uv = R.uv[k];
+        const double dep = R.depth[k];
+        const_cast<double2*>(P.po_uv)[q] = uv;
+        const_cast<double*>(P.po_depth)[q] = dep;
+        if (P.obs32)  // exact: the host checked that every admissible value is an f32
+            const_cast<float4*>(P.po_rec)[q] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(cam)};
     } else if (b < nbq + nbc) {
         const int q = (b - nbq) * TPB + tid;
         if (q >= P.n_adm) return;
         const int k = R.co_orig[q];
-        const_cast<int*>(P.co_pt)[q] = R.pt[k];
-        const_cast<double2*>(P.co_uv)[q] = R.uv[k];
-        const_cast<double*>(P.co_depth)[q] = R.depth[k];
+        const int pt = R.pt[k];
+        const double2 uv = R.uv[k];
+        const double dep = R.depth[k];
+        const_cast<int*>(P.co_pt)[q] = pt;
+        const_cast<double2*>(P.co_uv)[q] = uv;
+        const_cast<double*>(P.co_depth)[q] = dep;
+        if (P.obs32)
+            const_cast<float4*>(P.co_rec)[q] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(pt)};
     } else {
         const int a = (b - nbq - nbc) * TPB + tid;
         if (a >= P.n_ap) return;
@@ -2501,7 +2547,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                 CK(hipMalloc(&sst, sizeof(unsigned long long) * 4 * P.n_tiles));
                 scap = P.n_tiles;
             }
-            PL(K_SCHUR_TILE, k_schur_tile<true>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
+            OPL(K_SCHUR_TILE, (k_schur_tile<true, true>), (k_schur_tile<true, false>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
                sst, pp_parts(P), W.part, W.det_tbuf, E);
             std::vector<unsigned long long> h((size_t)4 * P.n_tiles);
             CK(hipMemcpyAsync(h.data(), sst, sizeof(h[0]) * h.size(), hipMemcpyDeviceToHost, s));
@@ -2534,7 +2580,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             fprintf(stderr, "  median tile %d: %.0f cycles span %d chunks %d points %d\n", t50, tot[P.n_tiles / 2].first,
                     tspan[t50], tch[t50 + 1] - tch[t50], cap[tch[t50 + 1]] - cap[tch[t50]]);
         } else {
-            PL(K_SCHUR_TILE, k_schur_tile<false>, dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
+            OPL(K_SCHUR_TILE, (k_schur_tile<false, true>), (k_schur_tile<false, false>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
                W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf, E);
         }
         if (W.det_tbuf && P.n_tiles > 0)
@@ -2633,7 +2679,7 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
     if (W.fused && P.n_ap == 0)  // an empty landmark shard: no back-substitution chunk zeroes S for the next assembly
         PL(K_MEMSET_S, k_env_zero, dim3(W.n_env), dim3(TPB), 0, s, W.st, W.env_tile, P.npad, W.S);
     if (P.n_ap > 0)
-        PL(K_BACKSUB_EVAL, k_backsub_chunk, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
+        OPL(K_BACKSUB_EVAL, k_backsub_chunk<true>, k_backsub_chunk<false>, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     const int nb_pt = pp_parts(P);
     // the split BCR kernel's call epoch (the persistent kernel's is advanced by k_bcr_border)

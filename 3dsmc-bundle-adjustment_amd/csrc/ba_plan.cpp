@@ -138,11 +138,15 @@ void plan_count(const PlanInput& in, Plan& pl) {
     std::vector<std::vector<int>> cc(T);
     std::vector<int> nadm(T, 0);
     std::vector<long long> bad(T, -1);  // first out-of-range observation of each range
+    std::vector<unsigned char> f32ok(T, 1);
     int* ptc = pl.pt_cnt.data();
+    // an f64 value that survives the round trip through f32 unchanged (NaN does not)
+    auto f32_exact = [](double v) { return (double)(float)v == v; };
     host_parallel(T, [&](int t) {
         std::vector<int>& c = cc[t];
         c.assign(nc, 0);
         int na = 0;
+        bool f32 = in.obs_uv != nullptr;
         for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k) {
             const int ci = in.obs_cam[k], pi = in.obs_pt[k];
             if (ci < 0 || ci >= nc || pi < 0 || pi >= np) { bad[t] = k; break; }
@@ -151,13 +155,17 @@ void plan_count(const PlanInput& in, Plan& pl) {
             ++na;
             ++c[ci];
             __atomic_fetch_add(ptc + pi, 1, __ATOMIC_RELAXED);
+            if (f32) f32 = f32_exact(in.obs_uv[2 * k]) && f32_exact(in.obs_uv[2 * k + 1]) && f32_exact(in.obs_depth[k]);
         }
         nadm[t] = na;
+        f32ok[t] = f32;
     });
     for (int t = 0; t < T; ++t)
         if (bad[t] >= 0) { pl.err = "observation index out of range"; return; }
+    pl.obs32 = in.obs_uv != nullptr;
     for (int t = 0; t < T; ++t) {
         pl.n_adm += nadm[t];
+        pl.obs32 = pl.obs32 && f32ok[t];
         for (int i = 0; i < nc; ++i) pl.cam_cnt[i] += cc[t][i];
     }
 }

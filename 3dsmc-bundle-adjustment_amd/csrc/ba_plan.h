@@ -28,6 +28,7 @@ struct PlanInput {
     const int32_t* obs_cam = nullptr;
     const int32_t* obs_pt = nullptr;
     const double* obs_depth = nullptr;
+    const double* obs_uv = nullptr;  // nullptr: no obs32 check (Plan::obs32 stays false)
 };
 
 struct PlanParams {
@@ -46,6 +47,7 @@ struct Plan {
     std::vector<int> cam_cnt, pt_cnt;
     std::vector<unsigned char> adm;  // observation k admissible (depth > 1e-15)
     int n_adm = 0;
+    bool obs32 = false;              // every admissible pixel and depth is exactly an f32 (DevProblem::obs32)
     // ---- stage 2 (plan_order): given the active cameras (cam_seen, all shards)
     std::vector<int> cam_ac;         // camera -> active index or -1 (fixed / unobserved)
     std::vector<int> ac_cam;         // active camera -> camera

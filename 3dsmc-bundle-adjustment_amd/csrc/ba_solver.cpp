@@ -62,7 +62,7 @@ enum BufId {
     B_CO_PT, B_CO_UV, B_CO_DEP, B_RAW_CAM, B_RAW_PT, B_RAW_UV, B_RAW_DEP, B_PLAN,
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
     B_BCR, B_CAMDATA_LOC, B_ENV_LOC, B_RED, B_PREP, B_CAMPART, B_STATE, B_LOG, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
-    B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF,
+    B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_PO_REC, B_CO_REC,
     B_COUNT
 };
 
@@ -542,6 +542,11 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     in.nc = nc; in.np = np; in.no = no;
     in.fixed_cam = verdict[0] ? -1 : p->fixed_cam;
     if (!verdict[0]) { in.obs_cam = p->obs_cam; in.obs_pt = p->obs_pt; in.obs_depth = p->obs_depth; }
+    // obs32 records when every admissible pixel / depth is an f32 (the reference's are); MIBA_OBS32=0: f64 arrays
+    if (!verdict[0]) {
+        const char* e = std::getenv("MIBA_OBS32");
+        if (!(e && e[0] == '0')) in.obs_uv = p->obs_uv;
+    }
     plan_count(in, pl);
     if (!verdict[0] && !pl.err.empty()) { local_err = pl.err; verdict[0] = 1; }
     if (shard) {
@@ -674,6 +679,10 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     HIPCHECK(ctx, ctx->buf[B_CO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
     HIPCHECK(ctx, ctx->buf[B_CO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
     HIPCHECK(ctx, ctx->buf[B_CO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
+    if (pl.obs32) {
+        HIPCHECK(ctx, ctx->buf[B_PO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_CO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
+    }
     ctx->ac_cam = pl.ac_cam;
     ctx->pt_idx = pl.pt_idx;
     const std::vector<int>& tile_base = pl.tile_base;
@@ -722,6 +731,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     P.pt_idx = dptr(PT_IDX);
     P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
     P.co_depth = ctx->buf[B_CO_DEP].as<double>();
+    P.obs32 = pl.obs32 ? 1 : 0;
+    P.po_rec = pl.obs32 ? ctx->buf[B_PO_REC].as<float4>() : nullptr;
+    P.co_rec = pl.obs32 ? ctx->buf[B_CO_REC].as<float4>() : nullptr;
     P.seg_ptr = dptr(SEG_PTR); P.seg_cam = dptr(SEG_CAM);
     P.seg_ac = dptr(SEG_AC); P.ac_cam = dptr(AC_CAM);
     P.ac_seg = reinterpret_cast<const int2*>(dptr(AC_SEG));
@@ -862,19 +874,21 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         const double env_bytes = env * 16 * 16 * 8;
         double* kb = ctx->k_bytes;
         double* kf = ctx->k_flops;
-        kb[K_CAM_SIDE] = A * 28 + Pn * 24 + (Cn + 1) * 56 + 32 + Sg * (CAMDATA + SEGINTR) * 8;
+        // observation record per sweep: obs32 {u, v, depth, index} 16 B; f64 arrays: index 4 + pixel 16 + depth 8
+        const double rec = P.obs32 ? 16.0 : 28.0;
+        kb[K_CAM_SIDE] = A * rec + Pn * 24 + (Cn + 1) * 56 + 32 + Sg * (CAMDATA + SEGINTR) * 8;
         kb[K_CAM_REDUCE] = Sg * CAMDATA * 8 + Cn * CAMDATA * 8;
         kf[K_CAM_SIDE] = A * 420;
         kb[K_LIN_FINALIZE] = Sg * SEGINTR * 8 + Cn * (56 + 48) + LIN_N * 8;
-        kb[K_POINT_COLNORM] = A * 28 + Pn * (8 + 24 + 24);
+        kb[K_POINT_COLNORM] = A * rec + Pn * (8 + 24 + 24);
         kb[K_SCALE] = (6 * Cn + 3 * Pn + 4) * 16;
         kb[K_MEMSET_S] = (double)n_env * 256 * 8;
         kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
-        kb[K_POINT_PREP] = A * 28 + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
+        kb[K_POINT_PREP] = A * rec + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
         kf[K_POINT_PREP] = A * 300 + Pn * 200;
-        kb[K_SCHUR_TILE] = A * 36 + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
+        kb[K_SCHUR_TILE] = A * (rec + 12) + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
         kf[K_SCHUR_TILE] = A * 350 + Pn * 13300;
-        kb[K_OBS_PAIRS] = ctx->n_ovf_obs * 36.0;
+        kb[K_OBS_PAIRS] = ctx->n_ovf_obs * 40.0;
         kb[K_CHOL] = 2 * env_bytes + 3 * npad * 8.0;
         kf[K_CHOL] = 0;
         for (int k = 0; k < nb; ++k) {
@@ -904,18 +918,21 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             // persistent kernel = the whole elimination + contributions + back-substitution in one
             // launch; bytes: S blocks read once (D, level-0 couplings, border rows, rhs), the
             // contributions written once and read by the two neighbours, y written / read twice.
+            // (k_bcr_split hands the eliminated blocks' X rows over instead — XL, XR, x written once and
+            // read once by the survivors — which the per-launch model below counts.)
             double p_by = nblk * (blk + 4 * 64 * 8.0 + 64 * 8 * 8.0), n_el = 0;
             for (int m = 0; m < L; ++m) {
                 const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
                 n_el += nel;
                 if (m == 0) p_by += nel * 2 * blk;
             }
-            p_by += n_el * 3 * (3 * blk + 2 * 64 * 8 * 8.0) + nblk * 3 * 64 * 8 * 8.0;
+            p_by += (ctx->W.bcr.persist >= 2 ? n_el * 2 * (2 * blk + 64 * 8 * 8.0) : n_el * 3 * (3 * blk + 2 * 64 * 8 * 8.0)) +
+                    nblk * 3 * 64 * 8 * 8.0;
             kf[K_BCR_PERSIST] = e_fl + c_fl + kf[K_BCR_BACK] * std::max(L, 1);
             kb[K_BCR_PERSIST] = p_by;
         }
         kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
-        kb[K_BACKSUB_EVAL] = A * 36 + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read once
+        kb[K_BACKSUB_EVAL] = A * (rec + 8) + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read once
         kf[K_BACKSUB_EVAL] = A * 450;
         kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
         kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step

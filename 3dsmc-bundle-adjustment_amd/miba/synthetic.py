@@ -15,7 +15,12 @@ image, so every measured configuration uses synthetic windows of the stated
   OptimizationUtils.cpp:223-226); depth = z (1 + N(0, 0.01))
   (points3d_local z, OptimizationUtils.cpp:261);
 * initial poses perturbed by 0.01 rad / 1 cm, points by 2 cm, intrinsics at the
-  prior; camera 0 is the gauge (SetParameterBlockConstant, :299).
+  prior; camera 0 is the gauge (SetParameterBlockConstant, :299);
+* ``sensor_f32`` (the BASELINE configs, make_config): pixel coordinates and depths are
+  float32 values, as the reference's are — cv::KeyPoint::pt is a Point2f and the depth
+  comes from a float depth image (OptimizationUtils.cpp:261-262, Map3D.cpp:85-88); the
+  solver widens them to f64 exactly (make_problem's default keeps full f64 values, the
+  general input the C-ABI accepts).
 """
 from __future__ import annotations
 
@@ -125,7 +130,8 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
                  outlier_frac: float = 0.02, outlier_px: float = 20.0, depth_noise: float = 0.01,
                  rot_noise: float = 0.01, trans_noise: float = 0.01, point_noise: float = 0.02,
                  intr_offset=(2.0, -1.5, 1.0, -0.8), fixed_cam: int = 0, shuffle_obs: bool = False,
-                 bad_depth_frac: float = 0.0, dup_frac: float = 0.0, cam_seed: int | None = None) -> ProblemArrays:
+                 bad_depth_frac: float = 0.0, dup_frac: float = 0.0, cam_seed: int | None = None,
+                 sensor_f32: bool = False) -> ProblemArrays:
     """Build one synthetic window. ``obs_per_point`` is an int or an inclusive (lo, hi) range.
     ``cam_seed`` draws the initial camera perturbation from its own stream, so landmark
     shards generated with different ``seed`` share identical window cameras."""
@@ -188,13 +194,16 @@ def make_problem(n_cams: int, n_points: int, obs_per_point=10, seed: int = 0, pi
     if shuffle_obs:
         perm = rng.permutation(n_obs)
         obs_cam, obs_pt, uv, depth = obs_cam[perm], obs_pt[perm], uv[perm], depth[perm]
+    if sensor_f32:  # keypoints and depth as the reference's sensor types hold them (float32)
+        uv = uv.astype(np.float32).astype(np.float64)
+        depth = depth.astype(np.float32).astype(np.float64)
     truth = dict(cams=np.concatenate([quat_from_rotmat(R_wc), t_wc], axis=1), points=X, intr=K_true)
     return ProblemArrays(cams, pts0, ROS_DEFAULT_INTRINSICS.copy(), ROS_DEFAULT_INTRINSICS.copy(), obs_cam, obs_pt,
                          uv, depth, fixed_cam, meta=dict(truth=truth, seed=seed))
 
 
 def make_config(name: str, **overrides) -> ProblemArrays:
-    cfg = dict(CONFIGS[name])
+    cfg = dict(CONFIGS[name], sensor_f32=True)
     cfg.update(overrides)
     return make_problem(**cfg)
 
@@ -203,7 +212,7 @@ def make_landmark_shard(name: str, shard: int, **overrides) -> ProblemArrays:
     """Landmark shard ``shard`` of a window with the cameras of config ``name``: the same
     (seeded) initial cameras and intrinsics on every shard, an independent block of the
     config's size of landmarks per shard (weak scaling of ba_comm_init sharding)."""
-    cfg = dict(CONFIGS[name])
+    cfg = dict(CONFIGS[name], sensor_f32=True)
     cfg.update(overrides)
     base = cfg["seed"]
     cfg["seed"] = base + 1009 * shard

@@ -95,6 +95,17 @@ def load_pmc_traffic(kernel: str, config: str):
     return None
 
 
+def obs_record(p) -> str:
+    """How libmiba streams this window's observations (ba_plan.cpp obs32 check, DevProblem::obs32)."""
+    import numpy as np
+    adm = p.obs_depth > 1e-15
+    f32 = all(np.array_equal(a.astype(np.float32).astype(np.float64), a) for a in (p.obs_uv[adm], p.obs_depth[adm]))
+    if f32 and os.environ.get("MIBA_OBS32", "1") != "0":
+        return ("obs32: 16-byte record {u, v, depth, index} per observation and sweep (pixels and depths are float32 "
+                "values, as the reference's cv::KeyPoint and float depth image hold them; widened to f64 exactly)")
+    return "f64 arrays: index 4 B + pixel 16 B + depth 8 B per observation and sweep"
+
+
 def roofline_entry(k: dict, config: str) -> dict:
     """Roofline of one kernel from libmiba's per-launch HIP-event timing and its
     algorithmic bytes / flops per launch."""
@@ -406,7 +417,8 @@ def main():
             "dtype": "f64",
             "data": "file" if args.problem else "synthetic",
             "config": {"workload": workload, "cams": n_cams, "points": n_pts, "obs": n_obs,
-                       "parallelism": f"landmark-shard{world}" if sharded else "single"},
+                       "parallelism": f"landmark-shard{world}" if sharded else "single",
+                       "obs_record": obs_record(prob0)},
             "setup_ms": round(statistics.median(setups), 3),
             "end_to_end_ms": round(statistics.median(e2e), 3),
             "end_to_end": {"what": "ba_solve = ba_prepare + LM to termination with the reference settings "

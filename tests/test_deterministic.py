@@ -52,3 +52,21 @@ def test_deterministic_solves_are_bitwise_identical(case):
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=8, **no_tol))
     assert abs(s1["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (s1, so)
+
+
+@pytest.mark.parametrize("case", ["c2", "wide_overflow_dup_f32"])
+def test_obs32_records_match_f64_arrays_bitwise(case, monkeypatch):
+    """A window whose pixels / depths are all f32 values (the reference's sensor types) is streamed as 16-byte
+    obs32 records; the f64 arrays (MIBA_OBS32=0) widen the same values, so the two deterministic solves agree
+    bit for bit."""
+    p = synthetic.make_config("C2") if case == "c2" else synthetic.make_problem(
+        **CASES["wide_overflow_dup"], sensor_f32=True)
+    assert np.array_equal(p.obs_uv.astype(np.float32).astype(np.float64), p.obs_uv)
+    q1, s1, l1 = _solve(p, 1)
+    monkeypatch.setenv("MIBA_OBS32", "0")
+    q2, s2, l2 = _solve(p, 1)
+    assert s1["final_cost"] == s2["final_cost"] and s1["num_iterations"] == s2["num_iterations"]
+    np.testing.assert_array_equal(l1, l2)
+    np.testing.assert_array_equal(q1.cams, q2.cams)
+    np.testing.assert_array_equal(q1.points, q2.points)
+    np.testing.assert_array_equal(q1.intr, q2.intr)
