@@ -83,7 +83,8 @@ PMC_ALIASES = {"bcr_split": ("bcr_split", "bcr_persist")}  # profiler id -> kern
 
 def load_pmc_traffic(kernel: str, config: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary, if present."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):  # newest first
+    # newest first: rNN_pmc_<config>[_sK].json (the r03_pmcfx_* diagnostic passes, e.g. the XCD map off, do not count)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except Exception:
