@@ -468,11 +468,16 @@ __device__ void trsm_t_lanes(const double* L, const double* rd, double* Y) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (wave < 4) {
         double x0 = Y[lane * RC + wave], x1 = Y[lane * RC + wave + 4];
-        double lr = L[63 * BLD + lane] * rd[63];
+        // rows of L prefetched PF steps ahead: one step of the chain (FMA -> v_readlane -> FMA) is shorter than an
+        // LDS round trip, so a one-step prefetch left every step waiting on its row
+        constexpr int PF = 4;
+        double lq[PF];
+#pragma unroll
+        for (int p = 0; p < PF; ++p) lq[p] = L[(63 - p) * BLD + lane] * rd[63 - p];
 #pragma unroll
         for (int R = 63; R >= 0; --R) {
-            const double lt = lane < R ? lr : 0.0;
-            if (R > 0) lr = L[(R - 1) * BLD + lane] * rd[R - 1];  // prefetch the next row
+            const double lt = lane < R ? lq[(63 - R) % PF] : 0.0;
+            if (R - PF >= 0) lq[(63 - R) % PF] = L[(R - PF) * BLD + lane] * rd[R - PF];
             const double xr0 = readlane_d(x0, R), xr1 = readlane_d(x1, R);
             x0 = __builtin_fma(-lt, xr0, x0);
             x1 = __builtin_fma(-lt, xr1, x1);
