@@ -1342,18 +1342,24 @@ template <int NW, int NX>
 struct Pull {
     static constexpr int NE = NW * 1024 + NX * 128, NU = (NE + TPB_E - 1) / TPB_E;
     unsigned long long v[NU];
-    // the source of entry u is uniform over the workgroup (64-column part) or a wave (8-column part)
+    // the source of entry u is uniform over the workgroup (64-column part: source u / 2, rows 8 (u & 1) + wave)
+    // or a wave (8-column part, u == 2 NW: source wave / 2). Written with the source index a compile-time
+    // constant (u is one in the unrolled loops) or a select, so the sources stay in registers: indexed by
+    // (threadIdx.x + TPB_E u) >> 10 they went to scratch, one extra memory round trip in front of every pull.
     __device__ __forceinline__ const double* gaddr(const PullSrc<NW, NX>& ps, int kb, int u) const {
-        const int e = threadIdx.x + TPB_E * u;
-        if (e < NW * 1024) {
-            const double* p = ps.w[e >> 10];
-            return p ? p + (16 * kb + ((e >> 6) & 15)) * BB + (e & 63) : nullptr;
+        static_assert(TPB_E == 512 && NX <= 4, "row-block split assumes 512 threads");
+        const int tid = threadIdx.x;
+        if (u < 2 * NW) {
+            const double* p = ps.w[u >> 1];
+            return p ? p + (16 * kb + 8 * (u & 1) + (tid >> 6)) * BB + (tid & 63) : nullptr;
         }
         if constexpr (NX > 0) {
-            const int f = e - NW * 1024;
-            if (f < NX * 128) {
-                const double* p = ps.x[f >> 7];
-                return p ? p + (16 * kb + ((f >> 3) & 15)) * RC + (f & 7) : nullptr;
+            if (u == 2 * NW && tid < NX * 128) {
+                const int k = tid >> 7;
+                const double* p = ps.x[0];
+#pragma unroll
+                for (int q = 1; q < NX; ++q) p = k == q ? ps.x[q] : p;
+                return p ? p + (16 * kb + ((tid >> 3) & 15)) * RC + (tid & 7) : nullptr;
             }
         }
         return nullptr;
