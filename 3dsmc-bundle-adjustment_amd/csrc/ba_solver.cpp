@@ -83,8 +83,24 @@ struct ba_context {
     // original obs index)
     Plan plan;
     std::vector<int> pt_idx, ac_cam;
-    char* stage = nullptr;  // pinned staging of ba_prepare's uploads
+    char* stage = nullptr;  // pinned staging of ba_prepare's uploads: [raw observations | plan index arrays]
     size_t stage_cap = 0;
+    char* pstage = nullptr;  // pinned staging of the parameter uploads (cameras | points | intrinsics | prior)
+    size_t pstage_cap = 0;
+    // plan cache (ba_options.rebuild_plan = 0): the structure key of the last full prepare; while plan_ok the
+    // staging buffer's raw region holds that window's observations (the reuse check compares against it) and
+    // `raw` the device gather inputs (B_RAW_* + the plan's orderings in B_PLAN)
+    struct PlanKey {
+        int nc = -1, np = -1, no = -1, fixed_cam = 0, det = 0, obs32 = 0;
+        unsigned long long env = 0;
+        bool operator==(const PlanKey& o) const {
+            return nc == o.nc && np == o.np && no == o.no && fixed_cam == o.fixed_cam && det == o.det &&
+                   env == o.env;
+        }
+    } key;
+    bool plan_ok = false;
+    PrepRaw raw{};
+    ba_prepare_info pinfo{};
     DevProblem P{};
     DevWork W{};
     BaConsts C{};
@@ -258,6 +274,7 @@ void ba_destroy(ba_context* ctx) {
     if (ctx->hprog) hipHostFree(ctx->hprog);
     if (ctx->hres) hipHostFree(ctx->hres);
     if (ctx->stage) hipHostFree(ctx->stage);
+    if (ctx->pstage) hipHostFree(ctx->pstage);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -474,14 +491,18 @@ static int bcr_init_handoffs(ba_context* ctx) {
 }
 
 // Pinned host staging of ba_prepare's uploads (grown on demand, kept by the context): the raw window is copied
-// in by the host threads and DMA'd while the plan is built; the plan's index arrays follow in one DMA.
-static int stage_ensure(ba_context* ctx, size_t bytes) {
+// in by the host threads and DMA'd while the plan is built; the plan's index arrays follow in one DMA. Growing
+// keeps the first `keep` bytes (the raw region, which the plan cache compares the next window against).
+static int stage_ensure(ba_context* ctx, size_t bytes, size_t keep) {
     if (ctx->stage_cap >= bytes) return BA_OK;
-    if (ctx->stage) HIPCHECK(ctx, hipHostFree(ctx->stage));
-    ctx->stage = nullptr;
-    ctx->stage_cap = 0;
     const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
-    HIPCHECK(ctx, hipHostMalloc((void**)&ctx->stage, want, hipHostMallocDefault));
+    char* nb = nullptr;
+    HIPCHECK(ctx, hipHostMalloc((void**)&nb, want, hipHostMallocDefault));
+    if (ctx->stage) {
+        if (keep) std::memcpy(nb, ctx->stage, std::min(keep, ctx->stage_cap));
+        HIPCHECK(ctx, hipHostFree(ctx->stage));
+    }
+    ctx->stage = nb;
     ctx->stage_cap = want;
     return BA_OK;
 }
@@ -500,12 +521,158 @@ static void stage_copy(const std::vector<StageCopy>& v) {
     });
 }
 
+// The staging layout of the raw observations: obs_uv | obs_depth | obs_cam | obs_pt.
+struct RawStage {
+    double* uv; double* dep; int* cam; int* pt;
+    RawStage(char* sg, size_t no)
+        : uv(reinterpret_cast<double*>(sg)), dep(uv + 2 * no), cam(reinterpret_cast<int*>(dep + no)), pt(cam + no) {}
+};
+static size_t raw_stage_bytes(size_t no) { return no * (16 + 8 + 4 + 4); }
+
+// The window's parameters (cameras, points, intrinsics, prior) -> pinned staging -> HBM slot 0, then copied on the
+// device into the candidate and initial slots (k_reset starts every solve from the initial ones).
+static int upload_params(ba_context* ctx, const ba_problem* p) {
+    hipStream_t s = ctx->stream;
+    const size_t nc = p->n_cams, np = p->n_points;
+    const size_t bytes = 56 * nc + 24 * np + 64;
+    if (ctx->pstage_cap < bytes) {
+        if (ctx->pstage) HIPCHECK(ctx, hipHostFree(ctx->pstage));
+        ctx->pstage = nullptr;
+        ctx->pstage_cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
+        HIPCHECK(ctx, hipHostMalloc((void**)&ctx->pstage, want, hipHostMallocDefault));
+        ctx->pstage_cap = want;
+    }
+    double* hc = reinterpret_cast<double*>(ctx->pstage);
+    double* hp = hc + 7 * nc;
+    double* hk = hp + 3 * np;
+    std::vector<StageCopy> cp = {{hk, p->intr, 32}, {hk + 4, p->intr_prior, 32}};
+    if (nc) cp.push_back({hc, p->cams, 56 * nc});
+    if (np) cp.push_back({hp, p->points, 24 * np});
+    stage_copy(cp);
+    const int slots[3][3] = {{B_CAMS0, B_CAMS1, B_CAMS_INIT}, {B_PTS0, B_PTS1, B_PTS_INIT}, {B_K0, B_K1, B_K_INIT}};
+    const size_t len[3] = {56 * nc, 24 * np, 32};
+    const double* src[3] = {hc, hp, hk};
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) HIPCHECK(ctx, ctx->buf[slots[a][b]].ensure(std::max<size_t>(len[a], 8)));
+        if (!len[a]) continue;
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[slots[a][0]].p, src[a], len[a], hipMemcpyHostToDevice, s));
+        for (int b = 1; b < 3; ++b)
+            HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[slots[a][b]].p, ctx->buf[slots[a][0]].p, len[a], hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHECK(ctx, ctx->buf[B_PRIOR].ensure(32));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PRIOR].p, hk + 4, 32, hipMemcpyHostToDevice, s));
+    return BA_OK;
+}
+
+// The MIBA_* settings ba_prepare reads (layout / solver choices): part of the plan cache key.
+static unsigned long long env_key() {
+    static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
+                                        "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED"};
+    unsigned long long h = 1469598103934665603ull;
+    for (const char* n : names) {
+        const char* v = std::getenv(n);
+        const std::string t = std::string(n) + (v ? std::string("=") + v : std::string("\x01"));
+        for (unsigned char c : t) h = (h ^ c) * 1099511628211ull;
+    }
+    return h;
+}
+
+// The block cyclic reduction's workspace: zeroed (the upper tiles of UL / UR are never written and must read as
+// zero), the resident path probed (bcr_persist_ok; MIBA_BCR overrides), the hand-off state initialised. Every
+// full prepare probes again, also after a hand-off timeout moved the last window to the per-level launches
+// (ba_prepare_info.bcr_path reports the path).
+static int bcr_setup(ba_context* ctx) {
+    BcrWork& Bw = ctx->W.bcr;
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, ctx->buf[B_BCR].cap, ctx->stream));
+    Bw.persist = bcr_persist_ok(Bw.nblk);
+    if (const char* e = std::getenv("MIBA_BCR")) {
+        if (!std::strcmp(e, "launch")) Bw.persist = 0;
+        else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
+        else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;  // "split3" or unset: default
+    }
+    ctx->bcr_fallback = false;
+    return bcr_init_handoffs(ctx);
+}
+
+// Plan cache: the window has the structure of the last full prepare (sizes, gauge, deterministic option and layout
+// settings in the key; obs_cam, obs_pt and the admissibility mask compared here, on the host threads, against the
+// staged copy of that window) -> only the parameters, and the observation values that changed, are uploaded.
+// An admissible value that is no longer an exact f32 on an obs32 plan also forces a rebuild.
+// Returns 1 when the plan was reused, 0 when the window needs a full prepare, < 0 on error.
+static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
+    const int no = p->n_obs;
+    RawStage rs(ctx->stage, (size_t)no);
+    const bool o32 = ctx->key.obs32 != 0;
+    const int T = (int)std::max<long long>(1, std::min<long long>(4LL * host_threads(), (long long)no >> 15));
+    std::vector<unsigned char> changed(T, 0), vals(T, 0);
+    auto f32_exact = [](double v) { return (double)(float)v == v; };
+    host_parallel(T, [&](int t) {
+        const size_t lo = (size_t)no * t / T, hi = (size_t)no * (t + 1) / T, n = hi - lo;
+        if (!n) return;
+        if (std::memcmp(rs.cam + lo, p->obs_cam + lo, 4 * n) || std::memcmp(rs.pt + lo, p->obs_pt + lo, 4 * n)) {
+            changed[t] = 1;
+            return;
+        }
+        if (std::memcmp(rs.dep + lo, p->obs_depth + lo, 8 * n)) {
+            for (size_t k = lo; k < hi; ++k) {
+                const double nd = p->obs_depth[k];
+                const bool adm = nd > 1e-15;
+                if (adm != (rs.dep[k] > 1e-15) || (adm && o32 && !f32_exact(nd))) { changed[t] = 1; return; }
+            }
+            std::memcpy(rs.dep + lo, p->obs_depth + lo, 8 * n);
+            vals[t] = 1;
+        }
+        if (std::memcmp(rs.uv + 2 * lo, p->obs_uv + 2 * lo, 16 * n)) {
+            if (o32)
+                for (size_t k = lo; k < hi; ++k)
+                    if (p->obs_depth[k] > 1e-15 && !(f32_exact(p->obs_uv[2 * k]) && f32_exact(p->obs_uv[2 * k + 1]))) {
+                        changed[t] = 1;
+                        return;
+                    }
+            std::memcpy(rs.uv + 2 * lo, p->obs_uv + 2 * lo, 16 * n);
+            vals[t] = 1;
+        }
+    });
+    ctx->pinfo.compare_ms = now_ms() - tp0;
+    for (int t = 0; t < T; ++t)
+        if (changed[t]) return 0;
+    const double tu = now_ms();
+    hipStream_t s = ctx->stream;
+    bool any_vals = false;
+    for (int t = 0; t < T; ++t) any_vals = any_vals || vals[t];
+    if (any_vals) {  // new pixel / depth values on the same structure: re-gather the observation layouts
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, rs.uv, 16 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, launch_prep_gather(ctx->P, ctx->raw, s));
+    }
+    if (int rc = upload_params(ctx, p)) return rc;
+    // the same device state as after a full prepare: S, rhs and the partial slots cleared
+    const DevProblem& P = ctx->P;
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RHS].p, 0, sizeof(double) * P.npad, s));
+    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * P.part_stride, s));
+    if (P.solver == 2 && ctx->bcr_fallback)
+        if (int rc = bcr_setup(ctx)) return rc;
+    ctx->pinfo.plan_reused = 1;
+    ctx->pinfo.obs_uploaded = any_vals ? 1 : 0;
+    ctx->pinfo.upload_ms = now_ms() - tu;
+    ctx->pinfo.bcr_path = P.solver == 2 ? ctx->W.bcr.persist : -1;
+    ctx->prepared = true;
+    ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;
+    return 1;
+}
+
 static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     const ba_options& o = ctx->opts;
     const bool shard = ctx->W.comm.on();
     const double tp0 = now_ms();
-    // validation: with landmark shards every rank must reach the same verdict before any
-    // further collective (a rank that bailed out alone would leave the others waiting)
+    ctx->pinfo = ba_prepare_info{};
+    ctx->pinfo.host_threads = host_threads();
+    ctx->pinfo.bcr_path = -1;
+    // validation: with landmark shards every rank must reach the same verdict before any further collective (a
+    // rank that bailed out alone would leave the others waiting), so until the verdict all-reduce a rank-local
+    // failure (an invalid problem, 1; a staging / allocation error, 2) goes into verdict[0] instead of a return
     int verdict[3] = {0, 0, 0};  // [0] error code (max), [1] n_cams (min), [2] -n_cams (min)
     std::string local_err;
     if (!p || p->n_cams < 0 || p->n_points < 0 || p->n_obs < 0) { local_err = "invalid problem sizes"; verdict[0] = 1; }
@@ -515,27 +682,43 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         verdict[0] = 1;
     }
     const int nc = verdict[0] ? 0 : p->n_cams, np = verdict[0] ? 0 : p->n_points, no = verdict[0] ? 0 : p->n_obs;
+    // plan cache: a window with the last full prepare's structure reuses its plan (unsharded contexts)
+    ba_context::PlanKey key{};
+    key.nc = nc; key.np = np; key.no = no;
+    key.fixed_cam = verdict[0] ? -1 : p->fixed_cam;
+    key.det = (o.deterministic || force_det) ? 1 : 0;
+    key.env = env_key();
+    if (!verdict[0] && !shard && !force_det && !o.rebuild_plan && ctx->plan_ok && key == ctx->key) {
+        const int r = prepare_reuse(ctx, p, tp0);
+        if (r != 0) {
+            ctx->pinfo.total_ms = now_ms() - tp0;
+            return r < 0 ? r : BA_OK;
+        }
+    }
+    ctx->plan_ok = false;
+    ctx->prepared = false;
     hipStream_t s = ctx->stream;
-    // the raw observations -> pinned staging -> HBM, in flight while the host builds the plan
-    const size_t raw_bytes = (size_t)no * (16 + 8 + 4 + 4);
-    if (!verdict[0] && no > 0) {
-        if (int rc = stage_ensure(ctx, raw_bytes)) return rc;
-        char* sg = ctx->stage;
-        double* s_uv = reinterpret_cast<double*>(sg);
-        double* s_dep = s_uv + 2 * (size_t)no;
-        int* s_cam = reinterpret_cast<int*>(s_dep + no);
-        int* s_pt = s_cam + no;
-        stage_copy({{s_uv, p->obs_uv, 16 * (size_t)no}, {s_dep, p->obs_depth, 8 * (size_t)no},
-                    {s_cam, p->obs_cam, 4 * (size_t)no}, {s_pt, p->obs_pt, 4 * (size_t)no}});
+    // the raw observations -> pinned staging -> HBM, in flight while the host builds the plan (landmark shards:
+    // after the local count, its errors into the verdict)
+    const size_t raw_bytes = raw_stage_bytes((size_t)no);
+    auto stage_raw = [&]() -> int {
+        if (no <= 0) return BA_OK;
+        if (int rc = stage_ensure(ctx, raw_bytes, 0)) return rc;
+        RawStage rs(ctx->stage, (size_t)no);
+        stage_copy({{rs.uv, p->obs_uv, 16 * (size_t)no}, {rs.dep, p->obs_depth, 8 * (size_t)no},
+                    {rs.cam, p->obs_cam, 4 * (size_t)no}, {rs.pt, p->obs_pt, 4 * (size_t)no}});
         HIPCHECK(ctx, ctx->buf[B_RAW_UV].ensure(16 * (size_t)no));
         HIPCHECK(ctx, ctx->buf[B_RAW_DEP].ensure(8 * (size_t)no));
         HIPCHECK(ctx, ctx->buf[B_RAW_CAM].ensure(4 * (size_t)no));
         HIPCHECK(ctx, ctx->buf[B_RAW_PT].ensure(4 * (size_t)no));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, s_uv, 16 * (size_t)no, hipMemcpyHostToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, s_dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, s_cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_PT].p, s_pt, 4 * (size_t)no, hipMemcpyHostToDevice, s));
-    }
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, rs.uv, 16 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, rs.cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_PT].p, rs.pt, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+        return BA_OK;
+    };
+    if (!shard && !verdict[0])
+        if (int rc = stage_raw()) return rc;
     const double tp_raw = now_ms();
     Plan& pl = ctx->plan;
     PlanInput in;
@@ -549,7 +732,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     }
     plan_count(in, pl);
     if (!verdict[0] && !pl.err.empty()) { local_err = pl.err; verdict[0] = 1; }
+    int local_rc = BA_OK;
     if (shard) {
+        if (!verdict[0] && (local_rc = stage_raw()) != BA_OK) { local_err = ctx->err; verdict[0] = 2; }
         verdict[1] = nc;
         verdict[2] = -nc;
         int rc = host_allreduce_i32(ctx, verdict, 1, COMM_MAX);
@@ -557,8 +742,10 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         if (rc != BA_OK) return rc;
         if (!verdict[0] && verdict[1] != -verdict[2]) { local_err = "landmark shards disagree on n_cams"; verdict[0] = 1; }
         if (verdict[0]) {
-            ctx->err = local_err.empty() ? "another landmark shard rejected its problem" : local_err;
-            return BA_E_INVALID;
+            ctx->err = local_err.empty() ? (verdict[0] >= 2 ? "another landmark shard failed to stage its observations"
+                                                             : "another landmark shard rejected its problem")
+                                         : local_err;
+            return local_rc != BA_OK ? local_rc : (verdict[0] >= 2 ? BA_E_DEVICE : BA_E_INVALID);
         }
     } else if (verdict[0]) {
         ctx->err = local_err;
@@ -594,353 +781,355 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         if (rc != BA_OK) return rc;
     }
     plan_envelope(pl);
-    const double tp_plan = now_ms();
-    const int n_ap = pl.n_ap(), n_tiled = pl.n_tiled;
-    const int n = pl.n, npad = pl.npad, nb = pl.nb, band_w = pl.band_w, cam_band = pl.cam_band;
-    const int n_bs_chunks = (int)pl.bs_chunk.size() - 1;
-    const int n_seg = (int)pl.seg_cam.size();
-    const int n_env = (int)pl.env_tile.size() / 2;
-    const bool det = (o.deterministic || force_det) && !pl.tile_base.empty();
-    std::vector<int> trange;  // deterministic mode: each active camera's Schur tile range
-    if (det) {
-        trange.assign(2 * (size_t)std::max(nac, 1), 0);
-        const int nt = (int)pl.tile_base.size();
-        for (int a = 0, lo = 0, hi = 0; a < nac; ++a) {
-            while (lo < nt && pl.tile_base[lo] < a - (TILE_WIN - 1)) ++lo;
-            while (hi < nt && pl.tile_base[hi] <= a) ++hi;
-            trange[2 * a] = lo;
-            trange[2 * a + 1] = std::max(lo, hi);
+    // the uploads and the device structure: every collective of the prepare is behind us, so a landmark shard that
+    // fails here (allocation, staging, launch) says so in one more agreement all-reduce instead of leaving the
+    // other ranks to wait in the first LM iteration's collectives
+    auto finish = [&]() -> int {
+        const double tp_plan = now_ms();
+        const int n_ap = pl.n_ap(), n_tiled = pl.n_tiled;
+        const int n = pl.n, npad = pl.npad, nb = pl.nb, band_w = pl.band_w, cam_band = pl.cam_band;
+        const int n_bs_chunks = (int)pl.bs_chunk.size() - 1;
+        const int n_seg = (int)pl.seg_cam.size();
+        const int n_env = (int)pl.env_tile.size() / 2;
+        const bool det = (o.deterministic || force_det) && !pl.tile_base.empty();
+        std::vector<int> trange;  // deterministic mode: each active camera's Schur tile range
+        if (det) {
+            trange.assign(2 * (size_t)std::max(nac, 1), 0);
+            const int nt = (int)pl.tile_base.size();
+            for (int a = 0, lo = 0, hi = 0; a < nac; ++a) {
+                while (lo < nt && pl.tile_base[lo] < a - (TILE_WIN - 1)) ++lo;
+                while (hi < nt && pl.tile_base[hi] <= a) ++hi;
+                trange[2 * a] = lo;
+                trange[2 * a + 1] = std::max(lo, hi);
+            }
         }
-    }
-    // ---- uploads: the plan's index arrays in one staged DMA (each array 256-byte aligned in B_PLAN)
-    struct Part { const int* src; size_t n; size_t off; };
-    std::vector<Part> parts = {
-        {pl.po_orig.data(), (size_t)n_adm, 0}, {pl.co_orig.data(), (size_t)n_adm, 0}, {pl.cam_ac.data(), (size_t)nc, 0},
-        {pl.pt_ptr.data(), (size_t)n_ap + 1, 0}, {pl.pt_idx.data(), (size_t)n_ap, 0},
-        {pl.seg_ptr.data(), pl.seg_ptr.size(), 0}, {pl.seg_cam.data(), pl.seg_cam.size(), 0},
-        {pl.seg_ac.data(), pl.seg_ac.size(), 0}, {pl.ac_seg.data(), pl.ac_seg.size(), 0},
-        {pl.ac_cam.data(), (size_t)nac, 0}, {pl.fcol.data(), (size_t)nb, 0},
-        {pl.tile_chunk.data(), pl.tile_chunk.size(), 0}, {pl.tile_base.data(), pl.tile_base.size(), 0},
-        {pl.tile_span.data(), pl.tile_span.size(), 0}, {pl.chunk_ap.data(), pl.chunk_ap.size(), 0},
-        {pl.bs_chunk.data(), pl.bs_chunk.size(), 0}, {pl.ovf_obs.data(), pl.ovf_obs.size(), 0},
-        {pl.rptr.data(), (size_t)nb + 1, 0}, {pl.rows.data(), pl.rows.size(), 0},
-        {pl.env_tile.data(), pl.env_tile.size(), 0}, {trange.data(), trange.size(), 0}};
-    enum { PO_ORIG, CO_ORIG, CAM_AC, PT_PTR, PT_IDX, SEG_PTR, SEG_CAM, SEG_AC, AC_SEG, AC_CAM, FCOL, TILE_CHUNK,
-           TILE_BASE, TILE_SPAN, CHUNK_AP, BS_CHUNK, OVF_OBS, RPTR, ROWS, ENV_TILE, TRANGE };
-    size_t plan_ints = 0;
-    for (Part& q : parts) {
-        q.off = plan_ints;
-        plan_ints += (q.n + 63) / 64 * 64 + 64;
-    }
-    const size_t raw_off = (raw_bytes + 255) / 256 * 256;  // after the raw region, which may still be in flight
-    if (ctx->stage_cap < raw_off + 4 * plan_ints) {
-        HIPCHECK(ctx, hipStreamSynchronize(s));  // growing frees the buffer the raw DMA reads
-        if (int rc = stage_ensure(ctx, raw_off + 4 * plan_ints)) return rc;
-    }
-    int* sp = reinterpret_cast<int*>(ctx->stage + raw_off);
-    {
-        std::vector<StageCopy> cp;
-        for (const Part& q : parts)
-            if (q.n) cp.push_back({sp + q.off, q.src, 4 * q.n});
-        stage_copy(cp);
-    }
-    HIPCHECK(ctx, ctx->buf[B_PLAN].ensure(4 * plan_ints));
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PLAN].p, sp, 4 * plan_ints, hipMemcpyHostToDevice, s));
-    int* dp = ctx->buf[B_PLAN].as<int>();
-    auto dptr = [&](int k) { return dp + parts[k].off; };
-    // parameters: one upload each, the other slots copied on the device
-    HIPCHECK(ctx, upload(ctx, B_CAMS0, p->cams, 7 * (size_t)nc));
-    HIPCHECK(ctx, upload(ctx, B_PTS0, p->points, 3 * (size_t)np));
-    HIPCHECK(ctx, upload(ctx, B_K0, p->intr, 4));
-    HIPCHECK(ctx, upload(ctx, B_PRIOR, p->intr_prior, 4));
-    HIPCHECK(ctx, ctx->buf[B_CAMS1].ensure(sizeof(double) * std::max<size_t>(7 * (size_t)nc, 1)));
-    HIPCHECK(ctx, ctx->buf[B_CAMS_INIT].ensure(sizeof(double) * std::max<size_t>(7 * (size_t)nc, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PTS1].ensure(sizeof(double) * std::max<size_t>(3 * (size_t)np, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PTS_INIT].ensure(sizeof(double) * std::max<size_t>(3 * (size_t)np, 1)));
-    HIPCHECK(ctx, ctx->buf[B_K1].ensure(sizeof(double) * 4));
-    HIPCHECK(ctx, ctx->buf[B_K_INIT].ensure(sizeof(double) * 4));
-    if (nc) {
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_CAMS1].p, ctx->buf[B_CAMS0].p, 56 * (size_t)nc, hipMemcpyDeviceToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_CAMS_INIT].p, ctx->buf[B_CAMS0].p, 56 * (size_t)nc, hipMemcpyDeviceToDevice, s));
-    }
-    if (np) {
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PTS1].p, ctx->buf[B_PTS0].p, 24 * (size_t)np, hipMemcpyDeviceToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PTS_INIT].p, ctx->buf[B_PTS0].p, 24 * (size_t)np, hipMemcpyDeviceToDevice, s));
-    }
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_K1].p, ctx->buf[B_K0].p, 32, hipMemcpyDeviceToDevice, s));
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_K_INIT].p, ctx->buf[B_K0].p, 32, hipMemcpyDeviceToDevice, s));
-    // the observation layouts, gathered on the device from the raw window and the plan's orderings
-    HIPCHECK(ctx, ctx->buf[B_PO_CAM].ensure(4 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PO_AC].ensure(4 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PO_AP].ensure(4 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_CO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_CO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
-    HIPCHECK(ctx, ctx->buf[B_CO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
-    if (pl.obs32) {
-        HIPCHECK(ctx, ctx->buf[B_PO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
-        HIPCHECK(ctx, ctx->buf[B_CO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
-    }
-    ctx->ac_cam = pl.ac_cam;
-    ctx->pt_idx = pl.pt_idx;
-    const std::vector<int>& tile_base = pl.tile_base;
-    const std::vector<int>& ovf_obs = pl.ovf_obs;
-    const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
-    const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS, 1});
-    HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
-    // landmark sharding: pack buffers of the envelope tiles of S, exchange scalars
-    if (shard) {
-        // envelope tiles + rhs (+ the camera and intrinsics sums of the folded exchange)
-        const size_t ne = (size_t)n_env * 256 + (size_t)npad + (size_t)nac * CAMDATA + SEGINTR + 1;
-        HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
-        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
-        HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
-        const size_t nred = RED_X + 4 + 2 * (size_t)ctx->W.comm.nranks;
-        HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * nred));
-        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * nred, s));
-    }
-    HIPCHECK(ctx, ctx->buf[B_SEGINTR].ensure(sizeof(double) * SEGINTR * std::max(n_seg, 1)));
-    HIPCHECK(ctx, ctx->buf[B_CAMPART].ensure(sizeof(double) * CAMDATA * std::max(n_seg, 1)));
-    HIPCHECK(ctx, ctx->buf[B_LIN].ensure(sizeof(double) * LIN_N));
-    HIPCHECK(ctx, ctx->buf[B_SCALE].ensure(sizeof(double) * (6 * nac + 3 * (size_t)n_ap + 4)));
-    HIPCHECK(ctx, ctx->buf[B_CNP].ensure(sizeof(double) * 3 * std::max(n_ap, 1)));
-    HIPCHECK(ctx, ctx->buf[B_PDATA].ensure(sizeof(double) * PDATA * std::max(n_ap, 1)));
-    HIPCHECK(ctx, ctx->buf[B_S].ensure(sizeof(double) * (size_t)npad * npad));
-    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)npad * npad, s));
-    HIPCHECK(ctx, ctx->buf[B_RHS].ensure(sizeof(double) * npad));
-    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RHS].p, 0, sizeof(double) * npad, s));
-    HIPCHECK(ctx, ctx->buf[B_DELTA].ensure(sizeof(double) * npad));
-    HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
-    HIPCHECK(ctx, ctx->buf[B_SCAL].ensure(sizeof(double) * SC_N));
-    HIPCHECK(ctx, ctx->buf[B_FLAG].ensure(sizeof(int) * 4));
-    HIPCHECK(ctx, ctx->buf[B_STATE].ensure(sizeof(LmState)));
-    HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (std::max(o.max_num_iterations, 0) + 2)));
-    HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * part_stride, s));
+        // ---- uploads: the plan's index arrays in one staged DMA (each array 256-byte aligned in B_PLAN)
+        struct Part { const int* src; size_t n; size_t off; };
+        std::vector<Part> parts = {
+            {pl.po_orig.data(), (size_t)n_adm, 0}, {pl.co_orig.data(), (size_t)n_adm, 0}, {pl.cam_ac.data(), (size_t)nc, 0},
+            {pl.pt_ptr.data(), (size_t)n_ap + 1, 0}, {pl.pt_idx.data(), (size_t)n_ap, 0},
+            {pl.seg_ptr.data(), pl.seg_ptr.size(), 0}, {pl.seg_cam.data(), pl.seg_cam.size(), 0},
+            {pl.seg_ac.data(), pl.seg_ac.size(), 0}, {pl.ac_seg.data(), pl.ac_seg.size(), 0},
+            {pl.ac_cam.data(), (size_t)nac, 0}, {pl.fcol.data(), (size_t)nb, 0},
+            {pl.tile_chunk.data(), pl.tile_chunk.size(), 0}, {pl.tile_base.data(), pl.tile_base.size(), 0},
+            {pl.tile_span.data(), pl.tile_span.size(), 0}, {pl.chunk_ap.data(), pl.chunk_ap.size(), 0},
+            {pl.bs_chunk.data(), pl.bs_chunk.size(), 0}, {pl.ovf_obs.data(), pl.ovf_obs.size(), 0},
+            {pl.rptr.data(), (size_t)nb + 1, 0}, {pl.rows.data(), pl.rows.size(), 0},
+            {pl.env_tile.data(), pl.env_tile.size(), 0}, {trange.data(), trange.size(), 0}};
+        enum { PO_ORIG, CO_ORIG, CAM_AC, PT_PTR, PT_IDX, SEG_PTR, SEG_CAM, SEG_AC, AC_SEG, AC_CAM, FCOL, TILE_CHUNK,
+               TILE_BASE, TILE_SPAN, CHUNK_AP, BS_CHUNK, OVF_OBS, RPTR, ROWS, ENV_TILE, TRANGE };
+        size_t plan_ints = 0;
+        for (Part& q : parts) {
+            q.off = plan_ints;
+            plan_ints += (q.n + 63) / 64 * 64 + 64;
+        }
+        const size_t raw_off = (raw_bytes + 255) / 256 * 256;  // after the raw region, which may still be in flight
+        if (ctx->stage_cap < raw_off + 4 * plan_ints) {
+            HIPCHECK(ctx, hipStreamSynchronize(s));  // growing frees the buffer the raw DMA reads
+            if (int rc = stage_ensure(ctx, raw_off + 4 * plan_ints, raw_bytes)) return rc;
+        }
+        int* sp = reinterpret_cast<int*>(ctx->stage + raw_off);
+        {
+            std::vector<StageCopy> cp;
+            for (const Part& q : parts)
+                if (q.n) cp.push_back({sp + q.off, q.src, 4 * q.n});
+            stage_copy(cp);
+        }
+        HIPCHECK(ctx, ctx->buf[B_PLAN].ensure(4 * plan_ints));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PLAN].p, sp, 4 * plan_ints, hipMemcpyHostToDevice, s));
+        int* dp = ctx->buf[B_PLAN].as<int>();
+        auto dptr = [&](int k) { return dp + parts[k].off; };
+        if (int rc = upload_params(ctx, p)) return rc;
+        // the observation layouts, gathered on the device from the raw window and the plan's orderings
+        HIPCHECK(ctx, ctx->buf[B_PO_CAM].ensure(4 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_PO_AC].ensure(4 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_PO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_PO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_PO_AP].ensure(4 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_PO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_CO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_CO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
+        HIPCHECK(ctx, ctx->buf[B_CO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
+        if (pl.obs32) {
+            HIPCHECK(ctx, ctx->buf[B_PO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_CO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
+        }
+        ctx->ac_cam = pl.ac_cam;
+        ctx->pt_idx = pl.pt_idx;
+        const std::vector<int>& tile_base = pl.tile_base;
+        const std::vector<int>& ovf_obs = pl.ovf_obs;
+        const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
+        const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS, 1});
+        HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
+        // landmark sharding: pack buffers of the envelope tiles of S, exchange scalars
+        if (shard) {
+            // envelope tiles + rhs (+ the camera and intrinsics sums of the folded exchange)
+            const size_t ne = (size_t)n_env * 256 + (size_t)npad + (size_t)nac * CAMDATA + SEGINTR + 1;
+            HIPCHECK(ctx, ctx->buf[B_CAMDATA_LOC].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
+            HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_CAMDATA_LOC].p, 0, sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16), s));
+            HIPCHECK(ctx, ctx->buf[B_ENV_LOC].ensure(sizeof(double) * ne));
+            const size_t nred = RED_X + 4 + 2 * (size_t)ctx->W.comm.nranks;
+            HIPCHECK(ctx, ctx->buf[B_RED].ensure(sizeof(double) * nred));
+            HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RED].p, 0, sizeof(double) * nred, s));
+        }
+        HIPCHECK(ctx, ctx->buf[B_SEGINTR].ensure(sizeof(double) * SEGINTR * std::max(n_seg, 1)));
+        HIPCHECK(ctx, ctx->buf[B_CAMPART].ensure(sizeof(double) * CAMDATA * std::max(n_seg, 1)));
+        HIPCHECK(ctx, ctx->buf[B_LIN].ensure(sizeof(double) * LIN_N));
+        HIPCHECK(ctx, ctx->buf[B_SCALE].ensure(sizeof(double) * (6 * nac + 3 * (size_t)n_ap + 4)));
+        HIPCHECK(ctx, ctx->buf[B_CNP].ensure(sizeof(double) * 3 * std::max(n_ap, 1)));
+        HIPCHECK(ctx, ctx->buf[B_PDATA].ensure(sizeof(double) * PDATA * std::max(n_ap, 1)));
+        HIPCHECK(ctx, ctx->buf[B_S].ensure(sizeof(double) * (size_t)npad * npad));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)npad * npad, s));
+        HIPCHECK(ctx, ctx->buf[B_RHS].ensure(sizeof(double) * npad));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RHS].p, 0, sizeof(double) * npad, s));
+        HIPCHECK(ctx, ctx->buf[B_DELTA].ensure(sizeof(double) * npad));
+        HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
+        HIPCHECK(ctx, ctx->buf[B_SCAL].ensure(sizeof(double) * SC_N));
+        HIPCHECK(ctx, ctx->buf[B_FLAG].ensure(sizeof(int) * 4));
+        HIPCHECK(ctx, ctx->buf[B_STATE].ensure(sizeof(LmState)));
+        HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (std::max(o.max_num_iterations, 0) + 2)));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * part_stride, s));
 
-    DevProblem& P = ctx->P;
-    P.cams[0] = ctx->buf[B_CAMS0].as<double>(); P.cams[1] = ctx->buf[B_CAMS1].as<double>();
-    P.pts[0] = ctx->buf[B_PTS0].as<double>(); P.pts[1] = ctx->buf[B_PTS1].as<double>();
-    P.K[0] = ctx->buf[B_K0].as<double>(); P.K[1] = ctx->buf[B_K1].as<double>();
-    P.prior = ctx->buf[B_PRIOR].as<double>();
-    P.po_cam = ctx->buf[B_PO_CAM].as<int>(); P.po_ac = ctx->buf[B_PO_AC].as<int>();
-    P.po_uv = ctx->buf[B_PO_UV].as<double2>(); P.po_depth = ctx->buf[B_PO_DEP].as<double>();
-    P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.po_pt = ctx->buf[B_PO_PT].as<int>();
-    P.pt_ptr = dptr(PT_PTR);
-    P.pt_idx = dptr(PT_IDX);
-    P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
-    P.co_depth = ctx->buf[B_CO_DEP].as<double>();
-    P.obs32 = pl.obs32 ? 1 : 0;
-    P.po_rec = pl.obs32 ? ctx->buf[B_PO_REC].as<float4>() : nullptr;
-    P.co_rec = pl.obs32 ? ctx->buf[B_CO_REC].as<float4>() : nullptr;
-    P.seg_ptr = dptr(SEG_PTR); P.seg_cam = dptr(SEG_CAM);
-    P.seg_ac = dptr(SEG_AC); P.ac_cam = dptr(AC_CAM);
-    P.ac_seg = reinterpret_cast<const int2*>(dptr(AC_SEG));
-    P.tile_chunk = dptr(TILE_CHUNK); P.tile_base = dptr(TILE_BASE);
-    P.tile_span = dptr(TILE_SPAN); P.chunk_ap = dptr(CHUNK_AP);
-    P.ovf_obs = dptr(OVF_OBS);
-    P.bs_chunk = dptr(BS_CHUNK);
-    P.n_bs_chunks = n_bs_chunks;
-    P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
-    ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
-    P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
-    P.n = n; P.npad = npad; P.kb = 6 * nac;
-    P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
-    {
-        PrepRaw R;
-        R.cam = ctx->buf[B_RAW_CAM].as<int>();
-        R.pt = ctx->buf[B_RAW_PT].as<int>();
-        R.uv = ctx->buf[B_RAW_UV].as<double2>();
-        R.depth = ctx->buf[B_RAW_DEP].as<double>();
-        R.cam_ac = dptr(CAM_AC);
-        R.po_orig = dptr(PO_ORIG);
-        R.co_orig = dptr(CO_ORIG);
-        HIPCHECK(ctx, launch_prep_gather(P, R, s));
-    }
-    P.part_stride = part_stride;
-    P.band_w = (nb >= 2 && nb <= 2048 && band_w <= 6) ? std::max(band_w, 1) : 0;
-    P.cam_band = cam_band;
-    // reduced-system solver: block cyclic reduction when the camera band fits a 64-dof block (a window of
-    // <= 10 active cameras is one block: the root alone, its factorization on the split kernel's look-ahead
-    // pivot chain — C1 4.9 ms per solve against 5.6 with the band Cholesky); else the banded LDS Cholesky;
-    // else the dense envelope kernel.
-    const int bcr_nblk = (nac + BCR_CAMS - 1) / BCR_CAMS;
-    P.solver = (cam_band < BCR_CAMS && bcr_nblk >= 1) ? 2 : (P.band_w > 0 ? 1 : 0);
-    if (const char* e = std::getenv("MIBA_SOLVER")) {
-        if (!std::strcmp(e, "dense")) P.solver = 0;
-        else if (!std::strcmp(e, "band") && P.band_w > 0) P.solver = 1;
-        else if (!std::strcmp(e, "bcr") && cam_band < BCR_CAMS && bcr_nblk >= 1) P.solver = 2;
-    }
-    if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
-    if (P.solver == 2) {
-        const size_t bytes = bcr_bytes(bcr_nblk);
-        HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
-        // upper tiles of UL/UR are never written and must read as zero
-        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, bytes, ctx->stream));
-        double* base = ctx->buf[B_BCR].as<double>();
-        BcrWork& Bw = ctx->W.bcr;
-        Bw.nblk = bcr_nblk;
-        Bw.levels = 0;
-        while ((1 << Bw.levels) < bcr_nblk) ++Bw.levels;
-        // balanced elimination tree for the split kernels: K = floor(log2 nblk), v = i + 2^K - nblk/2,
-        // so [voff, voff + nblk) holds one multiple of 2^K (the root, block nblk/2) and none of 2^(K+1)
-        Bw.vlevels = 0;
-        while ((2 << Bw.vlevels) <= bcr_nblk) ++Bw.vlevels;
-        Bw.voff = (1 << Bw.vlevels) - bcr_nblk / 2;
-        Bw.vroot = bcr_nblk / 2;
-        const size_t b64 = (size_t)64 * 64 * bcr_nblk, b8 = (size_t)64 * 8 * bcr_nblk;
-        Bw.Cf = base;
-        Bw.X = Bw.Cf + b64;
-        Bw.UL = Bw.X + (size_t)64 * BCR_XW * bcr_nblk;
-        Bw.UR = Bw.UL + b64;
-        Bw.F = Bw.UR + b64;
-        Bw.Dacc = Bw.F + b64;
-        Bw.rL = Bw.Dacc + b64;
-        Bw.rR = Bw.rL + b8;
-        Bw.Racc = Bw.rR + b8;
-        Bw.Y = Bw.Racc + b8;
-        Bw.Bp = Bw.Y + b8;
-        Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
-        Bw.F2 = Bw.rd + (size_t)64 * bcr_nblk;
-        Bw.bk = Bw.F2 + b64;
-        Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
-        Bw.persist = ctx->bcr_fallback ? 0 : bcr_persist_ok(bcr_nblk);
-        if (const char* e = std::getenv("MIBA_BCR")) {
-            if (!std::strcmp(e, "launch")) Bw.persist = 0;
-            else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
-            else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;  // "split3" or unset: default
+        DevProblem& P = ctx->P;
+        P.cams[0] = ctx->buf[B_CAMS0].as<double>(); P.cams[1] = ctx->buf[B_CAMS1].as<double>();
+        P.pts[0] = ctx->buf[B_PTS0].as<double>(); P.pts[1] = ctx->buf[B_PTS1].as<double>();
+        P.K[0] = ctx->buf[B_K0].as<double>(); P.K[1] = ctx->buf[B_K1].as<double>();
+        P.prior = ctx->buf[B_PRIOR].as<double>();
+        P.po_cam = ctx->buf[B_PO_CAM].as<int>(); P.po_ac = ctx->buf[B_PO_AC].as<int>();
+        P.po_uv = ctx->buf[B_PO_UV].as<double2>(); P.po_depth = ctx->buf[B_PO_DEP].as<double>();
+        P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.po_pt = ctx->buf[B_PO_PT].as<int>();
+        P.pt_ptr = dptr(PT_PTR);
+        P.pt_idx = dptr(PT_IDX);
+        P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
+        P.co_depth = ctx->buf[B_CO_DEP].as<double>();
+        P.obs32 = pl.obs32 ? 1 : 0;
+        P.po_rec = pl.obs32 ? ctx->buf[B_PO_REC].as<float4>() : nullptr;
+        P.co_rec = pl.obs32 ? ctx->buf[B_CO_REC].as<float4>() : nullptr;
+        P.seg_ptr = dptr(SEG_PTR); P.seg_cam = dptr(SEG_CAM);
+        P.seg_ac = dptr(SEG_AC); P.ac_cam = dptr(AC_CAM);
+        P.ac_seg = reinterpret_cast<const int2*>(dptr(AC_SEG));
+        P.tile_chunk = dptr(TILE_CHUNK); P.tile_base = dptr(TILE_BASE);
+        P.tile_span = dptr(TILE_SPAN); P.chunk_ap = dptr(CHUNK_AP);
+        P.ovf_obs = dptr(OVF_OBS);
+        P.bs_chunk = dptr(BS_CHUNK);
+        P.n_bs_chunks = n_bs_chunks;
+        P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
+        ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
+        P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
+        P.n = n; P.npad = npad; P.kb = 6 * nac;
+        P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
+        {
+            PrepRaw R;
+            R.cam = ctx->buf[B_RAW_CAM].as<int>();
+            R.pt = ctx->buf[B_RAW_PT].as<int>();
+            R.uv = ctx->buf[B_RAW_UV].as<double2>();
+            R.depth = ctx->buf[B_RAW_DEP].as<double>();
+            R.cam_ac = dptr(CAM_AC);
+            R.po_orig = dptr(PO_ORIG);
+            R.co_orig = dptr(CO_ORIG);
+            ctx->raw = R;
+            HIPCHECK(ctx, launch_prep_gather(P, R, s));
         }
-        if (int rc = bcr_init_handoffs(ctx)) return rc;
-    }
-    DevWork& W = ctx->W;
-    W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
-    W.camdata_loc = shard ? ctx->buf[B_CAMDATA_LOC].as<double>() : W.camdata;
-    W.camdata_part = ctx->buf[B_CAMPART].as<double>();
-    W.env_tile = reinterpret_cast<const int2*>(dptr(ENV_TILE));
-    W.n_env = n_env;
-    W.env_loc = shard ? ctx->buf[B_ENV_LOC].as<double>() : nullptr;
-    W.red = shard ? ctx->buf[B_RED].as<double>() : nullptr;
-    P.rank = W.comm.rank;
-    P.nranks = W.comm.nranks;
-    {
-        const char* e = std::getenv("MIBA_XCD_MAP");
-        P.xcd_map = (e && e[0] == '0') ? 0 : 1;
-    }
-    W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
-    W.cnp = ctx->buf[B_CNP].as<double>(); W.pdata = ctx->buf[B_PDATA].as<double>();
-    W.S = ctx->buf[B_S].as<double>(); W.rhs = ctx->buf[B_RHS].as<double>();
-    W.delta = ctx->buf[B_DELTA].as<double>(); W.part = ctx->buf[B_PART].as<double>();
-    W.scal = ctx->buf[B_SCAL].as<double>(); W.chol_flag = ctx->buf[B_FLAG].as<int>();
-    W.fcol = dptr(FCOL); W.rptr = dptr(RPTR); W.rows = dptr(ROWS);
-    W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
-    // deterministic mode: the Schur tiles write per-tile slabs, summed in tile order per element of S
-    W.det_tbuf = nullptr;
-    W.det_trange = nullptr;
-    if (det) {
-        HIPCHECK(ctx, ctx->buf[B_DET_TBUF].ensure(sizeof(double) * SCH_TBUF * (size_t)P.n_tiles));
-        W.det_tbuf = ctx->buf[B_DET_TBUF].as<double>();
-        W.det_trange = reinterpret_cast<const int2*>(dptr(TRANGE));
-    }
-    // fused LM-loop linearisation (k_lin_point + envelope tiles in k_schur_tile, S / rhs zeroed by the previous
-    // iteration): the unsharded default-mode path with points and camera segments
-    {
-        const char* e = std::getenv("MIBA_FUSED");
-        const bool off = e && e[0] == '0';
-        // landmark shards: the same choice on every rank (it fixes the collective sequence), so only uniform inputs
-        W.fused = (shard ? (!o.deterministic && !off)
-                         : (!W.det_tbuf && n_ap > 0 && n_seg > 0 && !off)) ? 1 : 0;
-    }
-    BaConsts& C = ctx->C;
-    ctx->n_adm_all = n_adm_all;
-    // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
-    // and the window reduces to the IntrinsicsPrior block, :236-241)
-    const double N = (double)std::max(n_adm_all, 1);
-    C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
-    C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
-    C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
-    C.a_r = o.hub_p_repr; C.b_r = o.hub_p_repr * o.hub_p_repr;
-    C.a_d = o.hub_p_unpr; C.b_d = o.hub_p_unpr * o.hub_p_unpr;
-    C.min_diag = o.min_lm_diagonal; C.max_diag = o.max_lm_diagonal;
-    ctx->nblk_pt = nblk_pt;
-    ctx->prepared = true;
-    ctx->prep_nc = nc; ctx->prep_np = np; ctx->prep_no = no;
-    // Algorithmic (compulsory) traffic per launch, DESIGN.md §Roofline:
-    // each input byte read once, each output byte written once.
-    {
-        const double A = n_adm, Pn = n_ap, Cn = nac, Sg = n_seg;
-        double env = 0;  // envelope tiles of the reduced system
-        for (int k = 0; k < nb; ++k) env += (double)(pl.rptr[k + 1] - pl.rptr[k]) + 1.0;
-        const double env_bytes = env * 16 * 16 * 8;
-        double* kb = ctx->k_bytes;
-        double* kf = ctx->k_flops;
-        // observation record per sweep: obs32 {u, v, depth, index} 16 B; f64 arrays: index 4 + pixel 16 + depth 8
-        const double rec = P.obs32 ? 16.0 : 28.0;
-        kb[K_CAM_SIDE] = A * rec + Pn * 24 + (Cn + 1) * 56 + 32 + Sg * (CAMDATA + SEGINTR) * 8;
-        kb[K_CAM_REDUCE] = Sg * CAMDATA * 8 + Cn * CAMDATA * 8;
-        kf[K_CAM_SIDE] = A * 420;
-        kb[K_LIN_FINALIZE] = Sg * SEGINTR * 8 + Cn * (56 + 48) + LIN_N * 8;
-        kb[K_POINT_COLNORM] = A * rec + Pn * (8 + 24 + 24);
-        kb[K_SCALE] = (6 * Cn + 3 * Pn + 4) * 16;
-        kb[K_MEMSET_S] = (double)n_env * 256 * 8;
-        kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
-        kb[K_POINT_PREP] = A * rec + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
-        kf[K_POINT_PREP] = A * 300 + Pn * 200;
-        kb[K_SCHUR_TILE] = A * (rec + 12) + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
-        kf[K_SCHUR_TILE] = A * 350 + Pn * 13300;
-        kb[K_OBS_PAIRS] = ctx->n_ovf_obs * 40.0;
-        kb[K_CHOL] = 2 * env_bytes + 3 * npad * 8.0;
-        kf[K_CHOL] = 0;
-        for (int k = 0; k < nb; ++k) {
-            const double r = pl.rptr[k + 1] - pl.rptr[k];
-            kf[K_CHOL] += (r * (r + 1) / 2) * 2.0 * 16 * 16 * 16 + r * 16 * 16 * 16 + 16 * 16 * 16 / 3.0;
+        P.part_stride = part_stride;
+        P.band_w = (nb >= 2 && nb <= 2048 && band_w <= 6) ? std::max(band_w, 1) : 0;
+        P.cam_band = cam_band;
+        // reduced-system solver: block cyclic reduction when the camera band fits a 64-dof block (a window of
+        // <= 10 active cameras is one block: the root alone, its factorization on the split kernel's look-ahead
+        // pivot chain — C1 4.9 ms per solve against 5.6 with the band Cholesky); else the banded LDS Cholesky;
+        // else the dense envelope kernel.
+        const int bcr_nblk = (nac + BCR_CAMS - 1) / BCR_CAMS;
+        P.solver = (cam_band < BCR_CAMS && bcr_nblk >= 1) ? 2 : (P.band_w > 0 ? 1 : 0);
+        if (const char* e = std::getenv("MIBA_SOLVER")) {
+            if (!std::strcmp(e, "dense")) P.solver = 0;
+            else if (!std::strcmp(e, "band") && P.band_w > 0) P.solver = 1;
+            else if (!std::strcmp(e, "bcr") && cam_band < BCR_CAMS && bcr_nblk >= 1) P.solver = 2;
         }
+        if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
         if (P.solver == 2) {
-            // block cyclic reduction: per eliminated 64-dof block, Cholesky 64^3/3 + forward solve of
-            // 136 columns 64^2*136 (elim); 44 16x16x64 contribution tiles (contrib); per launch =
-            // solve total / launches per solve. Bytes: the blocks each kernel must read / write.
-            const int nblk = ctx->W.bcr.nblk, L = ctx->W.bcr.levels;
-            const double blk = 64.0 * 64 * 8, xblk = 64.0 * 136 * 8;
-            double e_fl = 64.0 * 64 * 64 / 3 + 2.0 * 64 * 64 * 8, e_by = 3 * blk + 2 * 64 * 8 * 8;  // root
-            double c_fl = 0, c_by = 0, b_by = 0;
-            for (int m = 0; m < L; ++m) {
-                const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
-                e_fl += nel * (64.0 * 64 * 64 / 3 + 64.0 * 64 * 136 * 2);
-                e_by += nel * (5 * blk + blk + xblk);
-                c_fl += nel * 44.0 * 16 * 16 * 64 * 2;
-                c_by += nel * (xblk + 3 * blk + 2 * 64 * 8 * 8);
-                b_by += nel * (blk + xblk + 3 * 64 * 8 * 8);
-            }
-            kf[K_BCR_ELIM] = e_fl / (L + 1); kb[K_BCR_ELIM] = e_by / (L + 1);
-            kf[K_BCR_CONTRIB] = c_fl / std::max(L, 1); kb[K_BCR_CONTRIB] = c_by / std::max(L, 1);
-            kf[K_BCR_BACK] = nblk * 2.0 * 64 * 64 * 8 * 2 / std::max(L, 1); kb[K_BCR_BACK] = b_by / std::max(L, 1);
-            kb[K_BCR_BORDER] = nblk * (32.0 + 64 * 8) * 8;
-            // persistent kernel = the whole elimination + contributions + back-substitution in one
-            // launch; bytes: S blocks read once (D, level-0 couplings, border rows, rhs), the
-            // contributions written once and read by the two neighbours, y written / read twice.
-            // (k_bcr_split hands the eliminated blocks' X rows over instead — XL, XR, x written once and
-            // read once by the survivors — which the per-launch model below counts.)
-            double p_by = nblk * (blk + 4 * 64 * 8.0 + 64 * 8 * 8.0), n_el = 0;
-            for (int m = 0; m < L; ++m) {
-                const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
-                n_el += nel;
-                if (m == 0) p_by += nel * 2 * blk;
-            }
-            p_by += (ctx->W.bcr.persist >= 2 ? n_el * 2 * (2 * blk + 64 * 8 * 8.0) : n_el * 3 * (3 * blk + 2 * 64 * 8 * 8.0)) +
-                    nblk * 3 * 64 * 8 * 8.0;
-            kf[K_BCR_PERSIST] = e_fl + c_fl + kf[K_BCR_BACK] * std::max(L, 1);
-            kb[K_BCR_PERSIST] = p_by;
+            const size_t bytes = bcr_bytes(bcr_nblk);
+            HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
+            double* base = ctx->buf[B_BCR].as<double>();
+            BcrWork& Bw = ctx->W.bcr;
+            Bw.nblk = bcr_nblk;
+            Bw.levels = 0;
+            while ((1 << Bw.levels) < bcr_nblk) ++Bw.levels;
+            // balanced elimination tree for the split kernels: K = floor(log2 nblk), v = i + 2^K - nblk/2,
+            // so [voff, voff + nblk) holds one multiple of 2^K (the root, block nblk/2) and none of 2^(K+1)
+            Bw.vlevels = 0;
+            while ((2 << Bw.vlevels) <= bcr_nblk) ++Bw.vlevels;
+            Bw.voff = (1 << Bw.vlevels) - bcr_nblk / 2;
+            Bw.vroot = bcr_nblk / 2;
+            const size_t b64 = (size_t)64 * 64 * bcr_nblk, b8 = (size_t)64 * 8 * bcr_nblk;
+            Bw.Cf = base;
+            Bw.X = Bw.Cf + b64;
+            Bw.UL = Bw.X + (size_t)64 * BCR_XW * bcr_nblk;
+            Bw.UR = Bw.UL + b64;
+            Bw.F = Bw.UR + b64;
+            Bw.Dacc = Bw.F + b64;
+            Bw.rL = Bw.Dacc + b64;
+            Bw.rR = Bw.rL + b8;
+            Bw.Racc = Bw.rR + b8;
+            Bw.Y = Bw.Racc + b8;
+            Bw.Bp = Bw.Y + b8;
+            Bw.rd = Bw.Bp + (size_t)32 * bcr_nblk;
+            Bw.F2 = Bw.rd + (size_t)64 * bcr_nblk;
+            Bw.bk = Bw.F2 + b64;
+            Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
+            if (int rc = bcr_setup(ctx)) return rc;
         }
-        kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
-        kb[K_BACKSUB_EVAL] = A * (rec + 8) + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read once
-        kf[K_BACKSUB_EVAL] = A * 450;
-        kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
-        kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step
-        kf[K_LIN_POINT] = kf[K_CAM_SIDE] + kf[K_POINT_PREP];
+        DevWork& W = ctx->W;
+        W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
+        W.camdata_loc = shard ? ctx->buf[B_CAMDATA_LOC].as<double>() : W.camdata;
+        W.camdata_part = ctx->buf[B_CAMPART].as<double>();
+        W.env_tile = reinterpret_cast<const int2*>(dptr(ENV_TILE));
+        W.n_env = n_env;
+        W.env_loc = shard ? ctx->buf[B_ENV_LOC].as<double>() : nullptr;
+        W.red = shard ? ctx->buf[B_RED].as<double>() : nullptr;
+        P.rank = W.comm.rank;
+        P.nranks = W.comm.nranks;
+        {
+            const char* e = std::getenv("MIBA_XCD_MAP");
+            P.xcd_map = (e && e[0] == '0') ? 0 : 1;
+        }
+        W.lin = ctx->buf[B_LIN].as<double>(); W.scale = ctx->buf[B_SCALE].as<double>();
+        W.cnp = ctx->buf[B_CNP].as<double>(); W.pdata = ctx->buf[B_PDATA].as<double>();
+        W.S = ctx->buf[B_S].as<double>(); W.rhs = ctx->buf[B_RHS].as<double>();
+        W.delta = ctx->buf[B_DELTA].as<double>(); W.part = ctx->buf[B_PART].as<double>();
+        W.scal = ctx->buf[B_SCAL].as<double>(); W.chol_flag = ctx->buf[B_FLAG].as<int>();
+        W.fcol = dptr(FCOL); W.rptr = dptr(RPTR); W.rows = dptr(ROWS);
+        W.st = ctx->buf[B_STATE].as<LmState>(); W.log = ctx->buf[B_LOG].as<double>();
+        // deterministic mode: the Schur tiles write per-tile slabs, summed in tile order per element of S
+        W.det_tbuf = nullptr;
+        W.det_trange = nullptr;
+        if (det) {
+            HIPCHECK(ctx, ctx->buf[B_DET_TBUF].ensure(sizeof(double) * SCH_TBUF * (size_t)P.n_tiles));
+            W.det_tbuf = ctx->buf[B_DET_TBUF].as<double>();
+            W.det_trange = reinterpret_cast<const int2*>(dptr(TRANGE));
+        }
+        // fused LM-loop linearisation (k_lin_point + envelope tiles in k_schur_tile, S / rhs zeroed by the previous
+        // iteration): the unsharded default-mode path with points and camera segments
+        {
+            const char* e = std::getenv("MIBA_FUSED");
+            const bool off = e && e[0] == '0';
+            // landmark shards: the same choice on every rank (it fixes the collective sequence), so only uniform inputs
+            W.fused = (shard ? (!o.deterministic && !off)
+                             : (!W.det_tbuf && n_ap > 0 && n_seg > 0 && !off)) ? 1 : 0;
+        }
+        BaConsts& C = ctx->C;
+        ctx->n_adm_all = n_adm_all;
+        // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
+        // and the window reduces to the IntrinsicsPrior block, :236-241)
+        const double N = (double)std::max(n_adm_all, 1);
+        C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
+        C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
+        C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
+        C.a_r = o.hub_p_repr; C.b_r = o.hub_p_repr * o.hub_p_repr;
+        C.a_d = o.hub_p_unpr; C.b_d = o.hub_p_unpr * o.hub_p_unpr;
+        C.min_diag = o.min_lm_diagonal; C.max_diag = o.max_lm_diagonal;
+        ctx->nblk_pt = nblk_pt;
+        ctx->prepared = true;
+        ctx->prep_nc = nc; ctx->prep_np = np; ctx->prep_no = no;
+        // Algorithmic (compulsory) traffic per launch, DESIGN.md §Roofline:
+        // each input byte read once, each output byte written once.
+        {
+            const double A = n_adm, Pn = n_ap, Cn = nac, Sg = n_seg;
+            double env = 0;  // envelope tiles of the reduced system
+            for (int k = 0; k < nb; ++k) env += (double)(pl.rptr[k + 1] - pl.rptr[k]) + 1.0;
+            const double env_bytes = env * 16 * 16 * 8;
+            double* kb = ctx->k_bytes;
+            double* kf = ctx->k_flops;
+            // observation record per sweep: obs32 {u, v, depth, index} 16 B; f64 arrays: index 4 + pixel 16 + depth 8
+            const double rec = P.obs32 ? 16.0 : 28.0;
+            kb[K_CAM_SIDE] = A * rec + Pn * 24 + (Cn + 1) * 56 + 32 + Sg * (CAMDATA + SEGINTR) * 8;
+            kb[K_CAM_REDUCE] = Sg * CAMDATA * 8 + Cn * CAMDATA * 8;
+            kf[K_CAM_SIDE] = A * 420;
+            kb[K_LIN_FINALIZE] = Sg * SEGINTR * 8 + Cn * (56 + 48) + LIN_N * 8;
+            kb[K_POINT_COLNORM] = A * rec + Pn * (8 + 24 + 24);
+            kb[K_SCALE] = (6 * Cn + 3 * Pn + 4) * 16;
+            kb[K_MEMSET_S] = (double)n_env * 256 * 8;
+            kb[K_ASSEMBLE] = Cn * CAMDATA * 8 + Cn * 36 * 8 + Cn * 24 * 8;
+            kb[K_POINT_PREP] = A * rec + Pn * (8 + 24 + 24) + Pn * PDATA * 8;
+            kf[K_POINT_PREP] = A * 300 + Pn * 200;
+            kb[K_SCHUR_TILE] = A * (rec + 12) + Pn * (PDATA * 8 + 24 + 24 + 8) + env_bytes + npad * 8.0;
+            kf[K_SCHUR_TILE] = A * 350 + Pn * 13300;
+            kb[K_OBS_PAIRS] = ctx->n_ovf_obs * 40.0;
+            kb[K_CHOL] = 2 * env_bytes + 3 * npad * 8.0;
+            kf[K_CHOL] = 0;
+            for (int k = 0; k < nb; ++k) {
+                const double r = pl.rptr[k + 1] - pl.rptr[k];
+                kf[K_CHOL] += (r * (r + 1) / 2) * 2.0 * 16 * 16 * 16 + r * 16 * 16 * 16 + 16 * 16 * 16 / 3.0;
+            }
+            if (P.solver == 2) {
+                // block cyclic reduction: per eliminated 64-dof block, Cholesky 64^3/3 + forward solve of
+                // 136 columns 64^2*136 (elim); 44 16x16x64 contribution tiles (contrib); per launch =
+                // solve total / launches per solve. Bytes: the blocks each kernel must read / write.
+                const int nblk = ctx->W.bcr.nblk, L = ctx->W.bcr.levels;
+                const double blk = 64.0 * 64 * 8, xblk = 64.0 * 136 * 8;
+                double e_fl = 64.0 * 64 * 64 / 3 + 2.0 * 64 * 64 * 8, e_by = 3 * blk + 2 * 64 * 8 * 8;  // root
+                double c_fl = 0, c_by = 0, b_by = 0;
+                for (int m = 0; m < L; ++m) {
+                    const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
+                    e_fl += nel * (64.0 * 64 * 64 / 3 + 64.0 * 64 * 136 * 2);
+                    e_by += nel * (5 * blk + blk + xblk);
+                    c_fl += nel * 44.0 * 16 * 16 * 64 * 2;
+                    c_by += nel * (xblk + 3 * blk + 2 * 64 * 8 * 8);
+                    b_by += nel * (blk + xblk + 3 * 64 * 8 * 8);
+                }
+                kf[K_BCR_ELIM] = e_fl / (L + 1); kb[K_BCR_ELIM] = e_by / (L + 1);
+                kf[K_BCR_CONTRIB] = c_fl / std::max(L, 1); kb[K_BCR_CONTRIB] = c_by / std::max(L, 1);
+                kf[K_BCR_BACK] = nblk * 2.0 * 64 * 64 * 8 * 2 / std::max(L, 1); kb[K_BCR_BACK] = b_by / std::max(L, 1);
+                kb[K_BCR_BORDER] = nblk * (32.0 + 64 * 8) * 8;
+                // persistent kernel = the whole elimination + contributions + back-substitution in one
+                // launch; bytes: S blocks read once (D, level-0 couplings, border rows, rhs), the
+                // contributions written once and read by the two neighbours, y written / read twice.
+                // (k_bcr_split hands the eliminated blocks' X rows over instead — XL, XR, x written once and
+                // read once by the survivors — which the per-launch model below counts.)
+                double p_by = nblk * (blk + 4 * 64 * 8.0 + 64 * 8 * 8.0), n_el = 0;
+                for (int m = 0; m < L; ++m) {
+                    const int s_ = 1 << m, nel = (nblk - s_ + 2 * s_ - 1) / (2 * s_);
+                    n_el += nel;
+                    if (m == 0) p_by += nel * 2 * blk;
+                }
+                p_by += (ctx->W.bcr.persist >= 2 ? n_el * 2 * (2 * blk + 64 * 8 * 8.0) : n_el * 3 * (3 * blk + 2 * 64 * 8 * 8.0)) +
+                        nblk * 3 * 64 * 8 * 8.0;
+                kf[K_BCR_PERSIST] = e_fl + c_fl + kf[K_BCR_BACK] * std::max(L, 1);
+                kb[K_BCR_PERSIST] = p_by;
+            }
+            kb[K_UPDATE_CAMS] = Cn * (56 * 2 + 48 * 3) + 4 * 8 * 4;
+            kb[K_BACKSUB_EVAL] = A * (rec + 8) + Pn * (8 + 24 * 2 + 24 + PDATA * 8) + npad * 16.0;  // obs records read once
+            kf[K_BACKSUB_EVAL] = A * 450;
+            kb[K_FINAL] = (double)PART_NSLOTS * part_stride * 8;
+            kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step
+            kf[K_LIN_POINT] = kf[K_CAM_SIDE] + kf[K_POINT_PREP];
+        }
+        if (std::getenv("MIBA_PREP_TIMES"))  // diagnostic: host phases of ba_prepare (the device work is still in flight)
+            std::fprintf(stderr, "prepare: raw staging %.3f ms, plan %.3f ms, plan staging + enqueue %.3f ms (%d host threads)\n",
+                         tp_raw - tp0, tp_plan - tp_raw, now_ms() - tp_plan, host_threads());
+        ctx->pinfo.plan_ms = tp_plan - tp_raw;
+        ctx->pinfo.upload_ms = (tp_raw - tp0) + (now_ms() - tp_plan);
+        ctx->pinfo.obs_uploaded = 1;
+        ctx->pinfo.bcr_path = P.solver == 2 ? ctx->W.bcr.persist : -1;
+        return BA_OK;
+    };
+    int rc = finish();
+    if (shard) {
+        int bad = rc != BA_OK ? 1 : 0;
+        const std::string my_err = ctx->err;
+        const int rc2 = host_allreduce_i32(ctx, &bad, 1, COMM_MAX);
+        if (rc == BA_OK && rc2 != BA_OK) rc = rc2;
+        else if (rc == BA_OK && bad) {
+            ctx->err = "another landmark shard failed its prepare (device allocation / upload)";
+            rc = BA_E_DEVICE;
+        } else if (rc != BA_OK) ctx->err = my_err;
+        if (rc != BA_OK) ctx->prepared = false;
+        return rc;
     }
-    if (std::getenv("MIBA_PREP_TIMES"))  // diagnostic: host phases of ba_prepare (the device work is still in flight)
-        std::fprintf(stderr, "prepare: raw staging %.3f ms, plan %.3f ms, plan staging + enqueue %.3f ms (%d host threads)\n",
-                     tp_raw - tp0, tp_plan - tp_raw, now_ms() - tp_plan, host_threads());
+    if (rc != BA_OK) return rc;
+    // plan cache (unsharded, not gathered): this window's structure is the context's from now on
+    ctx->key = key;
+    ctx->key.obs32 = pl.obs32 ? 1 : 0;
+    ctx->plan_ok = !force_det;
+    ctx->pinfo.total_ms = now_ms() - tp0;
     return BA_OK;
 }
 
@@ -1026,9 +1215,17 @@ extern "C" int32_t ba_prepare(ba_context* ctx, const ba_problem* p) {
     miba_maybe_dump_window(p, &ctx->opts);
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     if (int rc = apply_spin_limit(ctx)) return rc;
+    const double t0 = now_ms();
     int rc = prepare(ctx, p);
     if (rc) return rc;
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->pinfo.total_ms = now_ms() - t0;  // device work included
+    return BA_OK;
+}
+
+extern "C" int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info) {
+    if (!ctx || !info) return BA_E_INVALID;
+    *info = ctx->pinfo;
     return BA_OK;
 }
 

@@ -7,7 +7,7 @@ import ctypes as C
 import os
 import subprocess
 
-from .capi import BaKernelStat, BaOptions, BaProblem, BaSummary
+from .capi import BaKernelStat, BaOptions, BaPrepareInfo, BaProblem, BaSummary
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MIBA_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libmiba.so")  # override: A/B builds
@@ -17,7 +17,7 @@ EXPORTS = (
     "ba_api_version", "ba_build_info", "ba_default_options", "ba_create", "ba_destroy", "ba_last_error", "ba_set_options",
     "ba_solve", "ba_prepare", "ba_solve_prepared", "ba_kernel_stats", "ba_reset_kernel_stats",
     "ba_debug_linearize", "ba_debug_reduced_system", "ba_debug_camera_sums", "ba_comm_unique_id", "ba_comm_init", "ba_comm_init_host",
-    "ba_iteration_log",
+    "ba_iteration_log", "ba_last_prepare",
     "ba_problem_write", "ba_problem_read_dims", "ba_problem_read", "ba_bal_read_dims", "ba_bal_read", "ba_bal_write",
 )
 COMM_ID_BYTES = 128  # BA_COMM_ID_BYTES
@@ -78,6 +78,8 @@ def lib():
     L.ba_comm_init_host.argtypes = [C.c_void_p, C.c_int32, C.c_int32, ALLREDUCE_FN, C.c_void_p]
     L.ba_comm_init_host.restype = C.c_int32
     L.ba_iteration_log.argtypes = [C.c_void_p, dp, C.c_int32]
+    L.ba_last_prepare.argtypes = [C.c_void_p, C.POINTER(BaPrepareInfo)]
+    L.ba_last_prepare.restype = C.c_int32
     L.ba_iteration_log.restype = C.c_int32
     ip = C.POINTER(C.c_int32)
     L.ba_problem_write.argtypes = [C.c_char_p, C.POINTER(BaProblem), C.POINTER(BaOptions)]

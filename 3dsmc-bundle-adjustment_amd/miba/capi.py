@@ -56,7 +56,8 @@ class BaOptions(C.Structure):
         ("profile_mask", C.c_int32),
         ("shard_min_obs", C.c_int32),
         ("small_window", C.c_int32),
-        ("reserved", C.c_int32 * 2),
+        ("rebuild_plan", C.c_int32),
+        ("reserved", C.c_int32 * 1),
     ]
 
 
@@ -125,6 +126,24 @@ class BaKernelStat(C.Structure):
     ]
 
 
+class BaPrepareInfo(C.Structure):
+    """Mirror of ``ba_prepare_info`` (what the last prepare did; ba_last_prepare)."""
+
+    _fields_ = [
+        ("plan_reused", C.c_int32),
+        ("obs_uploaded", C.c_int32),
+        ("host_threads", C.c_int32),
+        ("bcr_path", C.c_int32),
+        ("compare_ms", C.c_double),
+        ("plan_ms", C.c_double),
+        ("upload_ms", C.c_double),
+        ("total_ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 def default_options_py() -> BaOptions:
     """Pure-Python defaults (used only where no compiled library is loaded)."""
     o = BaOptions()
@@ -150,6 +169,7 @@ def default_options_py() -> BaOptions:
     o.deterministic = 0  # = ba_default_options
     o.shard_min_obs = 262144
     o.small_window = 0
+    o.rebuild_plan = 0  # reuse the host plan of an unchanged window structure
     return o
 
 

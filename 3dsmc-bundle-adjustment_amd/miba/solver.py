@@ -13,7 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .capi import BaKernelStat, BaOptions, BaSummary, ProblemArrays
+from .capi import BaKernelStat, BaOptions, BaPrepareInfo, BaSummary, ProblemArrays
 
 
 def default_options(**overrides) -> BaOptions:
@@ -136,6 +136,13 @@ class Solver:
         ps = prob.struct()
         self._check(self._L.ba_solve_prepared(self._h, C.byref(ps), C.byref(s)), "ba_solve_prepared")
         return s.as_dict()
+
+    def last_prepare(self) -> dict:
+        """ba_last_prepare(): whether the last prepare reused the plan, uploaded observations, its phase times and
+        the reduced-solve path (bcr_path)."""
+        info = BaPrepareInfo()
+        self._check(self._L.ba_last_prepare(self._h, C.byref(info)), "ba_last_prepare")
+        return info.as_dict()
 
     def kernel_stats(self) -> list:
         arr = (BaKernelStat * 32)()

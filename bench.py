@@ -192,7 +192,8 @@ def time_runs(solver, prob0, steps, runs):
     import torch.distributed as dist
     world = dist.get_world_size() if dist.is_initialized() else 1
     el, setup, summ = [], [], None
-    solver.set_options(max_num_iterations=steps, profile_kernels=0)
+    # setup_ms is the cost of a NEW window: the plan is rebuilt on every prepare (rebuild_plan = 1)
+    solver.set_options(max_num_iterations=steps, profile_kernels=0, rebuild_plan=1)
     for _ in range(runs):
         prob = prob0.copy()
         ts = time.perf_counter()
@@ -228,14 +229,16 @@ def latency_bench(args):
     with Solver(device=0, **opts) as s:
         for _ in range(max(args.warmup, 1)):
             s.solve(prob0.copy())
-        full, resolve, its = [], [], []
-        for _ in range(max(args.steps, 5)):
-            q = prob0.copy()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            sm = s.solve(q)
-            full.append((time.perf_counter() - t0) * 1e3)
-            its.append(sm["num_iterations"])
+        full, repeat, resolve, its = [], [], [], []
+        for rebuild, out in ((1, full), (0, repeat)):  # a new window per call / the same window again (plan cache)
+            s.set_options(rebuild_plan=rebuild)
+            for _ in range(max(args.steps, 5)):
+                q = prob0.copy()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sm = s.solve(q)
+                out.append((time.perf_counter() - t0) * 1e3)
+                its.append(sm["num_iterations"])
         q = prob0.copy()
         s.prepare(q)
         for _ in range(max(args.steps, 5)):
@@ -259,6 +262,10 @@ def latency_bench(args):
                       "points": prob0.n_points, "obs": prob0.n_obs, "parallelism": "single"},
            "lm_iterations": its[0], "ms_per_resolve_prepared": round(med(resolve), 4),
            "ms_per_lm_iteration": round(med(full) / max(its[0], 1), 4),
+           "ms_per_repeat_solve": round(med(repeat), 4),
+           "what": "value: ba_solve of a new window (host plan rebuilt, rebuild_plan = 1); ms_per_repeat_solve: "
+                   "ba_solve of the same window again, the reference's per-frame call (main.cpp:163-168), plan cache "
+                   "on; ms_per_resolve_prepared: ba_solve_prepared of the resident window",
            "cpu_baseline": {"value": round(med(cpu), 3), "unit": "ms", "cores": 1, "kind": "port",
                             "sample": f"oracle full solve of the same window ({so['num_iterations']} LM iterations), "
                                       f"median of 3", "host": host_info()}}
@@ -342,19 +349,32 @@ def main():
         stats = solver.kernel_stats()
     # end-to-end windowOptimize cost of this window: ba_solve = ba_prepare (host plan + upload) + the LM loop to
     # termination with the reference's own settings (tolerances on, max_num_iterations 75), median of 3 warm calls
-    e2e, e2e_it = [], 0
-    solver.set_options(max_num_iterations=75, profile_kernels=0, function_tolerance=1e-6, gradient_tolerance=1e-10,
-                       parameter_tolerance=1e-8)
-    for _ in range(4):
-        q = prob0.copy()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        se = solver.solve(q)
-        e2e.append((time.perf_counter() - t0) * 1e3)
-        e2e_it = se["num_iterations"]
-    e2e = e2e[1:]  # the first call may grow buffers
+    # new window every call (rebuild_plan = 1) and the reference's per-frame re-solve of the same window
+    # (main.cpp:163-168: the plan cache reuses the structure, rebuild_plan = 0; unsharded windows only)
+    def e2e_leg(rebuild):
+        out, its, prep = [], 0, []
+        solver.set_options(max_num_iterations=75, profile_kernels=0, function_tolerance=1e-6, gradient_tolerance=1e-10,
+                           parameter_tolerance=1e-8, rebuild_plan=rebuild)
+        for _ in range(4):
+            q = prob0.copy()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            se = solver.solve(q)
+            out.append((time.perf_counter() - t0) * 1e3)
+            its = se["num_iterations"]
+            prep.append(solver.last_prepare())
+        return out[1:], its, prep[1:]  # the first call may grow buffers / build the plan
+    e2e, e2e_it, _ = e2e_leg(1)
+    e2e_rep, e2e_rep_it, rep_prep = e2e_leg(0)
+    setups_rep = []
+    solver.set_options(max_num_iterations=args.steps, rebuild_plan=0, **NO_TOL)
+    for _ in range(TIMED_RUNS):
+        ts = time.perf_counter()
+        solver.prepare(prob0.copy())
+        setups_rep.append((time.perf_counter() - ts) * 1e3)
+    rep_info = solver.last_prepare()
     iters = summ["num_iterations"]
     elapsed = statistics.median(els)
     t = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device="cuda")
@@ -423,8 +443,18 @@ def main():
             "setup_ms": round(statistics.median(setups), 3),
             "end_to_end_ms": round(statistics.median(e2e), 3),
             "end_to_end": {"what": "ba_solve = ba_prepare + LM to termination with the reference settings "
-                                   "(tolerances 1e-6 / 1e-10 / 1e-8, max 75 iterations), warm context, median of 3",
+                                   "(tolerances 1e-6 / 1e-10 / 1e-8, max 75 iterations), warm context, median of 3; "
+                                   "a new window every call (the host plan rebuilt: rebuild_plan = 1)",
                            "lm_iterations": e2e_it, "runs_ms": [round(v, 3) for v in e2e]},
+            "setup_ms_repeat": round(statistics.median(setups_rep), 3),
+            "end_to_end_repeat_ms": round(statistics.median(e2e_rep), 3),
+            "end_to_end_repeat": {"what": "the reference's per-frame re-solve of the same window (main.cpp:163-168): "
+                                          "ba_solve of an unchanged window structure, the plan cache reuses the host "
+                                          "plan and the device structure (rebuild_plan = 0) and uploads the parameters",
+                                  "lm_iterations": e2e_rep_it, "runs_ms": [round(v, 3) for v in e2e_rep],
+                                  "plan_reused": [int(i["plan_reused"]) for i in rep_prep],
+                                  "prepare": {k: (round(v, 4) if isinstance(v, float) else v)
+                                              for k, v in rep_info.items()}},
             "timed_runs": {"n": len(els), "ms_per_step": [round(e * 1e3 / max(iters, 1), 4) for e in els],
                            "statistic": "median"},
             "roofline": roofs.get(dom),

@@ -92,7 +92,13 @@ typedef struct ba_options {
                                 its own points; 0 = always run the sharded exchange. Default 262144 */
     int32_t small_window;    /* ignored: kept for layout compatibility (the round-2 single-workgroup small-window
                                 kernel measured slower than the multi-launch path and was removed) */
-    int32_t reserved[2];
+    int32_t rebuild_plan;    /* 0 (default): ba_prepare / ba_solve reuse the context's host plan and device
+                                structure when the window's structure is unchanged since the last prepare
+                                (same sizes, fixed_cam, obs_cam, obs_pt, admissibility mask; the reference
+                                re-optimises the same window every frame, main.cpp:163-168) and upload only the
+                                parameters and the observation values that changed; 1 = rebuild every call.
+                                Unsharded contexts only (landmark shards always rebuild) */
+    int32_t reserved[1];
 } ba_options;
 
 /* One window, flattened. Mirrors what windowOptimize feeds to Ceres
@@ -173,6 +179,22 @@ int32_t ba_solve(ba_context* ctx, ba_problem* prob, ba_summary* summary);
  * (which must be the same window, same sizes). */
 int32_t ba_prepare(ba_context* ctx, const ba_problem* prob);
 int32_t ba_solve_prepared(ba_context* ctx, ba_problem* prob, ba_summary* summary);
+
+/* What the last ba_prepare (or the prepare inside ba_solve / the debug hooks) did. */
+typedef struct ba_prepare_info {
+    int32_t plan_reused;     /* 1: the window's structure matched the context's last plan (no plan rebuild) */
+    int32_t obs_uploaded;    /* 1: observation values were uploaded (always on a rebuild; on a reuse only when
+                                some pixel / depth value changed) */
+    int32_t host_threads;    /* host plan threads (MIBA_HOST_THREADS, else min(16, OMP_NUM_THREADS, affinity)) */
+    int32_t bcr_path;        /* reduced-solve path of the prepared window: 3 / 2 = resident split kernel with
+                                two / one helper workgroups per block, 1 = resident one-workgroup kernel,
+                                0 = per-level launches, -1 = not the block cyclic reduction (band / dense) */
+    double compare_ms;       /* structure / value comparison against the last prepare (reuse check) */
+    double plan_ms;          /* host plan build (0 on a reuse) */
+    double upload_ms;        /* staging + enqueue of the uploads and the device gather */
+    double total_ms;         /* the whole prepare, device work included */
+} ba_prepare_info;
+int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info);
 
 /* Landmark sharding (one process per GPU). Every rank passes the SAME window
  * cameras, intrinsics, prior and fixed_cam to ba_solve / ba_prepare, and its OWN block of

@@ -71,7 +71,8 @@ def _c_layout(struct_name, fields):
 
 
 @pytest.mark.parametrize("cls,cname", [(BaOptions, "ba_options"), (BaProblem, "ba_problem"),
-                                       (BaSummary, "ba_summary"), ("BaKernelStat", "ba_kernel_stat")])
+                                       (BaSummary, "ba_summary"), ("BaKernelStat", "ba_kernel_stat"),
+                                       ("BaPrepareInfo", "ba_prepare_info")])
 def test_struct_layout_matches_header(cls, cname):
     if isinstance(cls, str):
         from miba import capi
