@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstddef>
 
 #include "ba_device.h"
 #include "ba_kernels.h"
@@ -309,15 +310,22 @@ __device__ __forceinline__ void lm_decide_local(LmState& S, const LmParams& prm,
     }
     const double gmax = fmax(S.gmax_ci, scal[SC_GMAX_PT]);
     log[S.iter * LOG_W + 2] = gmax;
-    // FinalizeIterationAndCheckIfMinimizerCanContinue
-    if (S.iter >= prm.max_iter) {
-        S.done = 1; S.termination = 1; S.msg = MSG_MAX_ITER; S.msg_a = S.iter;
-    } else if (S.step_ok && gmax <= prm.gradient_tolerance) {
-        S.done = 1; S.termination = 0; S.msg = MSG_GRAD_TOL; S.msg_a = gmax; S.msg_b = prm.gradient_tolerance;
-    } else if (S.radius <= prm.min_radius) {
-        S.done = 1; S.termination = 0; S.msg = MSG_MIN_RADIUS; S.msg_a = S.radius; S.msg_b = prm.min_radius;
+    // FinalizeIterationAndCheckIfMinimizerCanContinue. The message operands are chosen by selects and stored
+    // once: per-branch stores of msg_a / msg_b were merged into one store at a selected field offset, which
+    // kept the state in scratch (24 B per lane in k_final / k_combine / k_lm_decide).
+    {
+        const bool t_iter = S.iter >= prm.max_iter;
+        const bool t_grad = !t_iter && S.step_ok && gmax <= prm.gradient_tolerance;
+        const bool t_rad = !t_iter && !t_grad && S.radius <= prm.min_radius;
+        if (t_iter || t_grad || t_rad) {
+            S.done = 1;
+            S.termination = t_iter ? 1 : 0;
+            S.msg = t_iter ? MSG_MAX_ITER : (t_grad ? MSG_GRAD_TOL : MSG_MIN_RADIUS);
+            S.msg_a = t_iter ? (double)S.iter : (t_grad ? gmax : S.radius);
+            S.msg_b = t_iter ? S.msg_b : (t_grad ? prm.gradient_tolerance : prm.min_radius);
+            return;
+        }
     }
-    if (S.done) return;
     if (scal[SC_BAD] >= SC_BAD_TIMEOUT) {
         // a BCR hand-off timed out (the resident workgroups were not co-resident): this iteration computed no
         // step. Stop the device loop WITHOUT a termination (termination -1, the iteration not counted, x /
@@ -348,14 +356,12 @@ __device__ __forceinline__ void lm_decide_local(LmState& S, const LmParams& prm,
     const double step_norm = sqrt(scal[SC_SN2]);
     const double xnorm = sqrt(S.xnorm2);
     const double cost_change = S.x_cost - cand;
-    if (step_norm <= prm.parameter_tolerance * (xnorm + prm.parameter_tolerance)) {
-        S.done = 1; S.termination = 0; S.msg = MSG_PARAM_TOL;
-        S.msg_a = step_norm / (xnorm + prm.parameter_tolerance); S.msg_b = prm.parameter_tolerance;
-    } else if (fabs(cost_change) <= prm.function_tolerance * S.x_cost) {
-        S.done = 1; S.termination = 0; S.msg = MSG_FUNC_TOL;
-        S.msg_a = fabs(cost_change) / S.x_cost; S.msg_b = prm.function_tolerance;
-    }
-    if (S.done) {
+    const bool t_par = step_norm <= prm.parameter_tolerance * (xnorm + prm.parameter_tolerance);
+    const bool t_fun = !t_par && fabs(cost_change) <= prm.function_tolerance * S.x_cost;
+    if (t_par || t_fun) {
+        S.done = 1; S.termination = 0; S.msg = t_par ? MSG_PARAM_TOL : MSG_FUNC_TOL;
+        S.msg_a = t_par ? step_norm / (xnorm + prm.parameter_tolerance) : fabs(cost_change) / S.x_cost;
+        S.msg_b = t_par ? prm.parameter_tolerance : prm.function_tolerance;
         lg[0] = cand; lg[1] = cost_change; lg[3] = step_norm; lg[4] = 0.0; lg[5] = S.radius; lg[6] = -1.0;
         return;
     }
@@ -384,13 +390,27 @@ __device__ __forceinline__ void lm_decide_local(LmState& S, const LmParams& prm,
 
 // Publishes the LM progress to the host-mapped block (one thread): the terminal state first (8-byte
 // system-scope stores, drained), then the word n_decide | done << 31.
+// The state's 8-byte words field by field (no reinterpret_cast of the struct: that view kept the state in scratch,
+// 24 B per lane in k_final / k_combine); the host copies the block back as an LmState.
+static_assert(offsetof(LmState, msg_b) == 64 && offsetof(LmState, iter) == 72 && offsetof(LmState, n_decide) == 116 &&
+                  sizeof(LmState) == 120,
+              "publish_progress writes LmState's layout word by word");
+__device__ __forceinline__ unsigned long long pack2(int lo, int hi) {
+    return (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
+}
 __device__ inline void publish_progress(unsigned* progress, const LmState& S) {
     if (S.done) {
-        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
+        const unsigned long long w[15] = {
+            (unsigned long long)__double_as_longlong(S.radius), (unsigned long long)__double_as_longlong(S.decrease_factor),
+            (unsigned long long)__double_as_longlong(S.x_cost), (unsigned long long)__double_as_longlong(S.xnorm2),
+            (unsigned long long)__double_as_longlong(S.final_cost), (unsigned long long)__double_as_longlong(S.gmax_ci),
+            (unsigned long long)__double_as_longlong(S.initial_cost), (unsigned long long)__double_as_longlong(S.msg_a),
+            (unsigned long long)__double_as_longlong(S.msg_b), pack2(S.iter, S.n_succ), pack2(S.n_unsucc, S.n_invalid),
+            pack2(S.step_ok, S.cur), pack2(S.need_lin, S.done), pack2(S.termination, S.msg),
+            pack2(S.stop_next, S.n_decide)};
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(progress) + PROG_STATE_OFF);
 #pragma unroll
-        for (int k = 0; k < (int)(sizeof(LmState) / 8); ++k)
-            __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k < 15; ++k) __hip_atomic_store(dst + k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __hip_atomic_store(progress, (unsigned)S.n_decide | (S.done ? 0x80000000u : 0u), __ATOMIC_RELAXED,

@@ -727,6 +727,7 @@ __global__ void k_assemble(DevProblem P, BaConsts c, const LmState* __restrict__
 
 // Schur scatter for the OVERFLOW points (span > TILE_WIN cameras or repeated
 // cameras): thread per listed observation, global f64 atomics.
+template <bool O32>
 __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                    const double* __restrict__ scale,
                                                    const double* __restrict__ pdata, double* __restrict__ S,
@@ -750,10 +751,10 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, con
     // W~_a = s_c (Jc^T Jp) s_p
     double Y[18];
     {
-        const double2 uv = P.po_uv[a];
+        const ObsRaw<O32> o = po_obs<O32>(P, a);
         ObsEval ev;
         double jc[18], jp[9], jk[8];
-        lin_obs(c, P.cams[cur] + 7 * P.po_cam[a], X, K, uv.x, uv.y, P.po_depth[a], ev, jc, jp, jk);
+        lin_obs(c, P.cams[cur] + 7 * o.idx(), X, K, o.u(), o.v(), o.d(), ev, jc, jp, jk);
         const double* sc = scale + 6 * ca;
         double W[18];
         w_tilde(jc, jp, sc, sp, W);
@@ -776,10 +777,10 @@ __global__ __launch_bounds__(TPB) void k_obs_pairs(DevProblem P, BaConsts c, con
     for (int b = P.pt_ptr[ap]; b < P.pt_ptr[ap + 1]; ++b) {
         const int cb = P.po_ac[b];
         if (cb < ca || (cb == ca && b < a)) continue;
-        const double2 uv = P.po_uv[b];
+        const ObsRaw<O32> o = po_obs<O32>(P, b);
         ObsEval ev;
         double jc[18], jp[9], jk[8];
-        lin_obs(c, P.cams[cur] + 7 * P.po_cam[b], X, K, uv.x, uv.y, P.po_depth[b], ev, jc, jp, jk);
+        lin_obs(c, P.cams[cur] + 7 * o.idx(), X, K, o.u(), o.v(), o.d(), ev, jc, jp, jk);
         const double* sc = scale + 6 * cb;
         double W[18];
         w_tilde(jc, jp, sc, sp, W);
@@ -1210,6 +1211,7 @@ __global__ __launch_bounds__(TPB) void k_schur_gather(DevProblem P, const LmStat
 // by 36 + d, border row m by 42 + 4 d + m), so the sums run in program order without barriers or atomics.
 // Overflow points (spanning > TILE_WIN cameras or linking a camera twice) are rare; this path is for the
 // reproducibility mode, not for speed.
+template <bool O32>
 __global__ __launch_bounds__(128) void k_obs_pairs_det(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                        const double* __restrict__ scale,
                                                        const double* __restrict__ pdata, double* __restrict__ S,
@@ -1221,10 +1223,10 @@ __global__ __launch_bounds__(128) void k_obs_pairs_det(DevProblem P, BaConsts c,
     const int kb = P.kb;
     const double* K = P.K[cur];
     auto wt = [&](int q, int ca, const double* sp, const double* X, double W[18]) {
-        const double2 uv = P.po_uv[q];
+        const ObsRaw<O32> o = po_obs<O32>(P, q);
         ObsEval ev;
         double jc[18], jp[9], jk[8];
-        lin_obs(c, P.cams[cur] + 7 * P.po_cam[q], X, K, uv.x, uv.y, P.po_depth[q], ev, jc, jp, jk);
+        lin_obs(c, P.cams[cur] + 7 * o.idx(), X, K, o.u(), o.v(), o.d(), ev, jc, jp, jk);
         w_tilde(jc, jp, scale + 6 * ca, sp, W);
     };
     for (int i = 0; i < P.n_ovf_obs; ++i) {
@@ -2277,17 +2279,17 @@ __global__ void k_lm_decide(LmState* __restrict__ st, LmParams prm, const double
 
 // ---------------------------------------------------------------- debug hook
 // Per admissible observation (point-major order) residual + Jacobians, for the parity tests.
+template <bool O32>
 __global__ void k_debug_lin(DevProblem P, BaConsts c, const LmState* __restrict__ st, double* __restrict__ res,
                             double* __restrict__ jcam, double* __restrict__ jpt, double* __restrict__ jint) {
     const int cur = st->cur;
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= P.n_adm) return;
     const int ap = P.po_ap[a];
-    const double2 uv = P.po_uv[a];
+    const ObsRaw<O32> o = po_obs<O32>(P, a);
     ObsEval ev;
     double jc[18], jp[9], jk[8];
-    lin_obs(c, P.cams[cur] + 7 * P.po_cam[a], P.pts[cur] + 3 * P.pt_idx[ap], P.K[cur], uv.x, uv.y, P.po_depth[a], ev,
-            jc, jp, jk);
+    lin_obs(c, P.cams[cur] + 7 * o.idx(), P.pts[cur] + 3 * P.pt_idx[ap], P.K[cur], o.u(), o.v(), o.d(), ev, jc, jp, jk);
     for (int i = 0; i < 3; ++i) res[3 * (size_t)a + i] = ev.f[i];
     for (int i = 0; i < 18; ++i) jcam[18 * (size_t)a + i] = jc[i];
     for (int i = 0; i < 9; ++i) jpt[9 * (size_t)a + i] = jp[i];
@@ -2445,9 +2447,11 @@ __global__ __launch_bounds__(TPB) void k_reset(DevProblem P, LmState st0, LmStat
     for (size_t e = t; e < nS2; e += stride) reinterpret_cast<double2*>(S)[e] = double2{0.0, 0.0};
 }
 
-// ba_prepare: the observation layouts from the raw window (uploaded as the caller passed it) and the host plan's
-// orderings (ba_plan.cpp) — workgroups [0, nbq): point-major slot q (obs po_orig[q]); [nbq, nbq + nbc): camera-
-// major slot q (obs co_orig[q]); the rest: one active point per thread, its slots' point indices.
+// ba_prepare: the observation layout the window uses, from the raw window (uploaded as the caller passed it) and
+// the host plan's orderings (ba_plan.cpp) — workgroups [0, nbq): point-major slot q (obs po_orig[q]); [nbq, nbq +
+// nbc): camera-major slot q (obs co_orig[q]); the rest: one active point per thread, its slots' point indices.
+// O32: the 16-byte records only (every observation kernel of an obs32 window reads those); else the f64 arrays.
+template <bool O32>
 __global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, int nbq, int nbc) {
     const int b = blockIdx.x, tid = threadIdx.x;
     if (b < nbq) {
@@ -2455,14 +2459,16 @@ __global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, in
         if (q >= P.n_adm) return;
         const int k = R.po_orig[q];
         const int cam = R.cam[k];
-        const_cast<int*>(P.po_cam)[q] = cam;
-        const_cast<int*>(P.po_ac)[q] = R.cam_ac[cam];
         const double2 uv = R.uv[k];
         const double dep = R.depth[k];
-        const_cast<double2*>(P.po_uv)[q] = uv;
-        const_cast<double*>(P.po_depth)[q] = dep;
-        if (P.obs32)  // exact: the host checked that every admissible value is an f32
+        const_cast<int*>(P.po_ac)[q] = R.cam_ac[cam];
+        if constexpr (O32) {  // exact: the host checked that every admissible value is an f32
             const_cast<float4*>(P.po_rec)[q] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(cam)};
+        } else {
+            const_cast<int*>(P.po_cam)[q] = cam;
+            const_cast<double2*>(P.po_uv)[q] = uv;
+            const_cast<double*>(P.po_depth)[q] = dep;
+        }
     } else if (b < nbq + nbc) {
         const int q = (b - nbq) * TPB + tid;
         if (q >= P.n_adm) return;
@@ -2470,11 +2476,13 @@ __global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, in
         const int pt = R.pt[k];
         const double2 uv = R.uv[k];
         const double dep = R.depth[k];
-        const_cast<int*>(P.co_pt)[q] = pt;
-        const_cast<double2*>(P.co_uv)[q] = uv;
-        const_cast<double*>(P.co_depth)[q] = dep;
-        if (P.obs32)
+        if constexpr (O32) {
             const_cast<float4*>(P.co_rec)[q] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(pt)};
+        } else {
+            const_cast<int*>(P.co_pt)[q] = pt;
+            const_cast<double2*>(P.co_uv)[q] = uv;
+            const_cast<double*>(P.co_depth)[q] = dep;
+        }
     } else {
         const int a = (b - nbq - nbc) * TPB + tid;
         if (a >= P.n_ap) return;
@@ -2488,7 +2496,10 @@ __global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, in
 
 hipError_t launch_prep_gather(const DevProblem& P, const PrepRaw& R, hipStream_t s) {
     const int nbq = nblocks(P.n_adm, TPB), nba = nblocks(P.n_ap, TPB);
-    if (nbq + nbq + nba > 0) hipLaunchKernelGGL(k_prep_gather, dim3(2 * nbq + nba), dim3(TPB), 0, s, P, R, nbq, nbq);
+    if (nbq + nbq + nba > 0) {
+        if (P.obs32) hipLaunchKernelGGL(k_prep_gather<true>, dim3(2 * nbq + nba), dim3(TPB), 0, s, P, R, nbq, nbq);
+        else hipLaunchKernelGGL(k_prep_gather<false>, dim3(2 * nbq + nba), dim3(TPB), 0, s, P, R, nbq, nbq);
+    }
     return hipGetLastError();
 }
 
@@ -2589,9 +2600,10 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     }
     if (P.n_ovf_obs > 0) {
         if (W.det_tbuf)
-            PL(K_OBS_PAIRS, k_obs_pairs_det, dim3(1), dim3(128), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs);
+            OPL(K_OBS_PAIRS, k_obs_pairs_det<true>, k_obs_pairs_det<false>, dim3(1), dim3(128), 0, s, P, c, W.st, W.scale,
+                W.pdata, W.S, W.rhs);
         else
-            PL(K_OBS_PAIRS, k_obs_pairs, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale,
+            OPL(K_OBS_PAIRS, k_obs_pairs<true>, k_obs_pairs<false>, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c, W.st, W.scale,
                W.pdata, W.S, W.rhs);
     }
     if (W.comm.on() && W.fused) {
@@ -2703,8 +2715,10 @@ hipError_t launch_decide(const DevProblem& P, const LmParams& prm, DevWork& W, h
 
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,
                             double* jk, hipStream_t s) {
-    if (P.n_adm > 0)
-        hipLaunchKernelGGL(k_debug_lin, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, W.st, res, jc, jp, jk);
+    if (P.n_adm > 0) {
+        if (P.obs32) hipLaunchKernelGGL(k_debug_lin<true>, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, W.st, res, jc, jp, jk);
+        else hipLaunchKernelGGL(k_debug_lin<false>, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, W.st, res, jc, jp, jk);
+    }
     return hipGetLastError();
 }
 

@@ -841,18 +841,20 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         auto dptr = [&](int k) { return dp + parts[k].off; };
         if (int rc = upload_params(ctx, p)) return rc;
         // the observation layouts, gathered on the device from the raw window and the plan's orderings
-        HIPCHECK(ctx, ctx->buf[B_PO_CAM].ensure(4 * std::max<size_t>(n_adm, 1)));
+        // ... in ONE layout: the 16-byte records on obs32 windows, the f64 arrays otherwise (the index arrays always)
         HIPCHECK(ctx, ctx->buf[B_PO_AC].ensure(4 * std::max<size_t>(n_adm, 1)));
-        HIPCHECK(ctx, ctx->buf[B_PO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
-        HIPCHECK(ctx, ctx->buf[B_PO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
         HIPCHECK(ctx, ctx->buf[B_PO_AP].ensure(4 * std::max<size_t>(n_adm, 1)));
         HIPCHECK(ctx, ctx->buf[B_PO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
-        HIPCHECK(ctx, ctx->buf[B_CO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
-        HIPCHECK(ctx, ctx->buf[B_CO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
-        HIPCHECK(ctx, ctx->buf[B_CO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
         if (pl.obs32) {
             HIPCHECK(ctx, ctx->buf[B_PO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
             HIPCHECK(ctx, ctx->buf[B_CO_REC].ensure(16 * std::max<size_t>(n_adm, 1)));
+        } else {
+            HIPCHECK(ctx, ctx->buf[B_PO_CAM].ensure(4 * std::max<size_t>(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_PO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_PO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_CO_PT].ensure(4 * std::max<size_t>(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_CO_UV].ensure(16 * std::max<size_t>(n_adm, 1)));
+            HIPCHECK(ctx, ctx->buf[B_CO_DEP].ensure(8 * std::max<size_t>(n_adm, 1)));
         }
         ctx->ac_cam = pl.ac_cam;
         ctx->pt_idx = pl.pt_idx;
@@ -895,13 +897,16 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         P.pts[0] = ctx->buf[B_PTS0].as<double>(); P.pts[1] = ctx->buf[B_PTS1].as<double>();
         P.K[0] = ctx->buf[B_K0].as<double>(); P.K[1] = ctx->buf[B_K1].as<double>();
         P.prior = ctx->buf[B_PRIOR].as<double>();
-        P.po_cam = ctx->buf[B_PO_CAM].as<int>(); P.po_ac = ctx->buf[B_PO_AC].as<int>();
-        P.po_uv = ctx->buf[B_PO_UV].as<double2>(); P.po_depth = ctx->buf[B_PO_DEP].as<double>();
+        const bool f64l = !pl.obs32;  // the f64 layout (else nullptr: no kernel of an obs32 window reads it)
+        P.po_cam = f64l ? ctx->buf[B_PO_CAM].as<int>() : nullptr; P.po_ac = ctx->buf[B_PO_AC].as<int>();
+        P.po_uv = f64l ? ctx->buf[B_PO_UV].as<double2>() : nullptr;
+        P.po_depth = f64l ? ctx->buf[B_PO_DEP].as<double>() : nullptr;
         P.po_ap = ctx->buf[B_PO_AP].as<int>(); P.po_pt = ctx->buf[B_PO_PT].as<int>();
         P.pt_ptr = dptr(PT_PTR);
         P.pt_idx = dptr(PT_IDX);
-        P.co_pt = ctx->buf[B_CO_PT].as<int>(); P.co_uv = ctx->buf[B_CO_UV].as<double2>();
-        P.co_depth = ctx->buf[B_CO_DEP].as<double>();
+        P.co_pt = f64l ? ctx->buf[B_CO_PT].as<int>() : nullptr;
+        P.co_uv = f64l ? ctx->buf[B_CO_UV].as<double2>() : nullptr;
+        P.co_depth = f64l ? ctx->buf[B_CO_DEP].as<double>() : nullptr;
         P.obs32 = pl.obs32 ? 1 : 0;
         P.po_rec = pl.obs32 ? ctx->buf[B_PO_REC].as<float4>() : nullptr;
         P.co_rec = pl.obs32 ? ctx->buf[B_CO_REC].as<float4>() : nullptr;

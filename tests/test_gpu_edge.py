@@ -78,8 +78,11 @@ def test_bcr_handoff_timeout_reruns_the_iteration_in_the_same_solve(monkeypatch)
         note = s.last_error()
         monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
         q2 = p.copy()
-        sg2 = s.solve(q2)  # the context keeps the per-level launches
+        sg2 = s.solve(q2)  # the next prepare probes the resident kernel again (no sticky fallback)
+        info2 = s.last_prepare()
+        note2 = s.last_error()
     assert "re-run with the per-level BCR launches" in note, note
+    assert info2["bcr_path"] >= 2 and note2 == "", (info2, note2)
     for g in (sg, sg2):
         assert g["linear_solver"] == 2
         assert g["termination"] == so["termination"]
@@ -115,7 +118,10 @@ def test_two_contexts_solve_concurrently_on_one_gpu():
         t.start()
     for t in th:
         t.join(timeout=300)
+    hung = [k for k, t in enumerate(th) if t.is_alive()]
+    assert not hung, f"solver thread(s) {hung} still running after 300 s (hang or deadlock)"
     assert not errs, errs
+    assert all(o is not None for o in out), out
     for (sg, q), so in zip(out, want):
         assert sg["termination"] == so["termination"], (sg, so)
         assert sg["num_iterations"] == so["num_iterations"]

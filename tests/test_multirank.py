@@ -138,3 +138,50 @@ def test_sharded_exchange_runs_collectives(tmp_path):
                                                                   "max_num_iterations": 4}}
     res = run_ranks(tmp_path, 2, spec)
     assert all(r["comm_launches"] > 0 for r in res)
+
+
+def test_c5_sharded_two_ranks(tmp_path):
+    """C5 (1000 cams / 500k points / 5M obs, BASELINE configs[4], the 8-GPU window; main.cpp:179-183's global
+    BA is where windows this large come from) split over 2 ranks on GPU 0: 3 LM iterations with the tolerances
+    off through the sharded exchange (the ~6 MB envelope + rhs + camera sums all-reduce of 1000 cameras).
+    Cameras bitwise identical across ranks; the unsharded solve to 1e-10; the oracle fixture's first 3 trace
+    rows (tests/golden/c5_oracle.json) to 1e-9."""
+    opts = {"shard_min_obs": 0, "max_num_iterations": 3, "function_tolerance": 0.0, "parameter_tolerance": 0.0,
+            "gradient_tolerance": 0.0}
+    res = run_ranks(tmp_path, 2, {"problem": {"config": "C5"}, "nsplit": 2, "options": opts}, timeout=600)
+    whole = synthetic.make_config("C5")
+    ref_q, ref_s, ref_log = unsharded(whole, **{k: v for k, v in opts.items() if k != "shard_min_obs"})
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "c5_oracle.json")))
+    tr = np.array(gold["trace"])[:4]
+    s0 = res[0]["summary"]
+    for r in res:
+        assert r["summary"]["num_iterations"] == 3 and r["summary"]["final_cost"] == s0["final_cost"]
+        np.testing.assert_array_equal(r["cams"], res[0]["cams"])
+        np.testing.assert_array_equal(r["log"], res[0]["log"])
+        assert r["comm_launches"] == 0  # unprofiled: kernel stats are not collected
+    assert s0["num_obs_admissible"] == ref_s["num_obs_admissible"] == whole.n_obs
+    assert abs(s0["final_cost"] - ref_s["final_cost"]) <= 1e-10 * ref_s["final_cost"], (s0, ref_s)
+    np.testing.assert_array_equal(res[0]["log"][:, 6], ref_log[:, 6])
+    np.testing.assert_allclose(res[0]["log"][:, 0], tr[:, 0], rtol=1e-9)  # cost of iterations 0..3
+    np.testing.assert_allclose(res[0]["log"][:, 5], tr[:, 5], rtol=1e-9)  # trust-region radius
+    np.testing.assert_allclose(res[0]["log"][1:, 3], tr[1:, 3], rtol=1e-6)  # |step|
+    pts = whole.points.copy()
+    for r in res:
+        pts[r["ids"]] = r["points"]
+    np.testing.assert_allclose(res[0]["cams"], ref_q.cams, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(pts, ref_q.points, rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("profiled", [0, 1])
+def test_bcr_timeout_rerun_in_lockstep_on_shards(tmp_path, profiled):
+    """A forced hand-off timeout of the resident BCR kernel (MIBA_BCR_SPIN_LIMIT=1) on landmark shards: every
+    rank sees the same decision (the timeout flag rides the step-scalar exchange), pads its enqueued iterations
+    to the same count, re-runs the iteration with the per-level launches and finishes with BA_OK; the profiled
+    batch loop takes the same re-run path. Same iterations on every rank, oracle parity."""
+    spec = {"problem": {"config": "C2"}, "nsplit": 2, "env": {"MIBA_BCR_SPIN_LIMIT": "1"},
+            "options": {"shard_min_obs": 0, "profile_kernels": profiled}}
+    res = run_ranks(tmp_path, 2, spec)
+    whole = synthetic.make_config("C2")
+    ref_q, ref_s, ref_log = unsharded(whole)
+    so = oracle.solve(whole.copy())
+    check(res, whole, ref_q, ref_s, ref_log, so)
