@@ -245,6 +245,13 @@ def latency_bench(args):
             t0 = time.perf_counter()
             s.solve_prepared(q)
             resolve.append((time.perf_counter() - t0) * 1e3)
+        # per-kernel breakdown of one profiled re-solve (HIP events around every launch; not the timed runs)
+        s.set_options(profile_kernels=1, profile_mask=0)
+        s.reset_kernel_stats()
+        sp = s.solve_prepared(prob0.copy())
+        breakdown = {k["name"]: round(k["total_ms"] * 1e3 / max(sp["num_iterations"], 1), 2)
+                     for k in s.kernel_stats() if k["launches"] > 0}
+        s.set_options(profile_kernels=0)
     oracle.config(1, True)
     cpu = []
     for _ in range(3):
@@ -263,6 +270,7 @@ def latency_bench(args):
            "lm_iterations": its[0], "ms_per_resolve_prepared": round(med(resolve), 4),
            "ms_per_lm_iteration": round(med(full) / max(its[0], 1), 4),
            "ms_per_repeat_solve": round(med(repeat), 4),
+           "kernel_us_per_lm_iteration": breakdown,
            "what": "value: ba_solve of a new window (host plan rebuilt, rebuild_plan = 1); ms_per_repeat_solve: "
                    "ba_solve of the same window again, the reference's per-frame call (main.cpp:163-168), plan cache "
                    "on; ms_per_resolve_prepared: ba_solve_prepared of the resident window",

@@ -1,0 +1,144 @@
+// Pivot-chain micro-benchmark for the BCR's 64x64 block Cholesky (k_bcr_split's wave-0 chain): one wave factors
+// a tall 64 x 16 column panel in registers (lane r holds row r), 16 pivots, repeated. Variants:
+//   0  the kernel's chain: y = rsq(d) + one Newton step folded into l = a y (1 + e/2); next pivot
+//      dn = a_{j+1,j+1} - l^2 on lane j+1, broadcast by v_readlane; trailing updates a[k] -= l bcast(l, k)
+//   1  the next pivot from the reciprocal: dn = a_{j+1,j+1} - a_{j+1,j}^2 / d_j with r = rcp(d) + one Newton
+//      step (rcp + 3 dependent ops + readlane on the chain instead of rsq + 4); l and the trailing updates as 0
+//   2  variant 0 without the trailing updates (the chain alone: a lower bound)
+// Reports ns and shader cycles per pivot and the max |L L^T - A| of the last repetition.
+// build: hipcc --offload-arch=gfx950 -O3 tools/pivot_chain_bench.hip -o /tmp/pcb && /tmp/pcb
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+__device__ __forceinline__ double bcast(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ unsigned long long rt() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+__device__ __forceinline__ unsigned long long clk() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+template <int V>
+__device__ __forceinline__ void chain(double (&a)[16], double& my_inv) {
+    const int r = threadIdx.x & 63;
+    if constexpr (V == 0 || V == 2) {
+        double dn = bcast(a[0], 0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double d = dn;
+            const double y = __builtin_amdgcn_rsq(d);
+            const double e = __builtin_fma(-d * y, y, 1.0);
+            const double l = __builtin_fma(0.5 * a[j] * y, e, a[j] * y);
+            my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+            a[j] = l;
+            if (j < 15) {
+                dn = bcast(__builtin_fma(-l, l, a[j + 1]), j + 1);
+                if constexpr (V == 0) {
+#pragma unroll
+                    for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast(l, k), a[k]);
+                } else {
+                    a[j + 1] = __builtin_fma(-l, bcast(l, j + 1), a[j + 1]);
+                }
+            }
+        }
+    } else {
+        // d_{j+1} = a_{j+1,j+1} - a_{j+1,j}^2 / d_j on lane j + 1: the chain is rcp + e + r' + dn + readlane
+        double dn = bcast(a[0], 0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double d = dn;
+            if (j < 15) {
+                const double q = a[j] * a[j];  // lane j + 1: a_{j+1,j}^2 (current before pivot j)
+                const double rc = __builtin_amdgcn_rcp(d);
+                const double er = __builtin_fma(-d, rc, 1.0);
+                const double rr = __builtin_fma(rc, er, rc);
+                dn = bcast(__builtin_fma(-q, rr, a[j + 1]), j + 1);
+            }
+            const double y = __builtin_amdgcn_rsq(d);
+            const double e = __builtin_fma(-d * y, y, 1.0);
+            const double l = __builtin_fma(0.5 * a[j] * y, e, a[j] * y);
+            my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+            a[j] = l;
+            if (j < 15) {
+#pragma unroll
+                for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast(l, k), a[k]);
+            }
+        }
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(64) void k_bench(const double* __restrict__ A, double* __restrict__ L,
+                                              unsigned long long* __restrict__ t, int reps) {
+    const int r = threadIdx.x;
+    double a0[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) a0[c] = A[r * 16 + c];
+    double a[16], my_inv = 0.0, sink = 0.0;
+    const unsigned long long t0 = rt(), c0 = clk();
+    for (int it = 0; it < reps; ++it) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) a[c] = a0[c] + sink * 1e-300;  // depends on the previous repetition
+        chain<V>(a, my_inv);
+        sink = bcast(a[15], 63);
+    }
+    const unsigned long long c1 = clk(), t1 = rt();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) L[r * 16 + c] = a[c];
+    if (r == 0) { t[0] = t1 - t0; t[1] = c1 - c0; }
+}
+
+int main() {
+    // tall panel: rows 0..63 of column block 0 of an SPD 64 x 64 matrix A = B B^T + 64 I (rows 16..63: below)
+    const int n = 64;
+    std::vector<double> B(n * n), Af(n * n), A(64 * 16);
+    unsigned long long s = 12345;
+    for (auto& v : B) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = ((s >> 11) * (1.0 / 9007199254740992.0)) - 0.5; }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = i == j ? 64.0 : 0.0;
+            for (int k = 0; k < n; ++k) acc += B[i * n + k] * B[j * n + k];
+            Af[i * n + j] = acc;
+        }
+    for (int r = 0; r < 64; ++r)
+        for (int c = 0; c < 16; ++c) A[r * 16 + c] = Af[r * n + c];
+    double *dA, *dL;
+    unsigned long long* dt;
+    (void)hipMalloc(&dA, 8 * A.size()); (void)hipMalloc(&dL, 8 * A.size()); (void)hipMalloc(&dt, 16);
+    (void)hipMemcpy(dA, A.data(), 8 * A.size(), hipMemcpyHostToDevice);
+    const int reps = 2000;
+    const char* names[3] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)"};
+    for (int round = 0; round < 2; ++round)
+        for (int v = 0; v < 3; ++v) {
+            if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 2) hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            unsigned long long t[2];
+            std::vector<double> L(64 * 16);
+            (void)hipMemcpy(t, dt, 16, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(L.data(), dL, 8 * L.size(), hipMemcpyDeviceToHost);
+            // residual of the leading 16 x 16 block and the panel rows: (L L^T)[r][c] vs A[r][c], c <= min(r, 15)
+            double err = 0.0;
+            for (int r = 0; r < 64; ++r)
+                for (int c = 0; c <= (r < 16 ? r : 15); ++c) {
+                    double acc = 0.0;
+                    for (int k = 0; k <= c; ++k) acc += L[r * 16 + k] * L[c * 16 + k];
+                    err = std::fmax(err, std::fabs(acc - A[r * 16 + c]) / std::fabs(A[c * 16 + c]));
+                }
+            const double ns = t[0] * 10.0 / (reps * 16.0);  // s_memrealtime: 100 MHz
+            printf("round %d  %-26s %7.1f ns/pivot  %7.1f clk/pivot  rel.err %.2e\n", round, names[v], ns,
+                   (double)t[1] / (reps * 16.0), v == 2 ? 0.0 : err);
+        }
+    return 0;
+}
