@@ -2195,592 +2195,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
     block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, false, L.yt, L.byk, L.bybl);
 }
 
-// ---- twin path: two resident workgroups per block, each factoring D_i itself ---------------------------------
-// In k_bcr_split the factor workgroup publishes every panel (L tiles, W_kb, 1/diag) to its helpers on other CUs:
-// a cross-CU hop (~1.1 us) between W_kb and the helpers' X update of every panel, which at a level's last panel
-// sits on the critical path (the level's last rows -> the next level). Here each of a block's two workgroups —
-// A: [XL | x]; B: [XR | x], the Gram of x and the back-substitution; the root: one workgroup with the x columns —
-// runs the factorization of D_i in its own LDS. Both see the same inputs (D_i from S, the same pulled rows) and
-// run the same code with the same wave assignment, so they hold bitwise the same L, and each applies every panel
-// from LDS. Wave roles after the pulls (SIMD s = wave & 3):
-//   wave 0        the pivot chain (tall column block kb, as k_bcr_split's factor); nothing else on SIMD 0
-//   waves 1-3     the critical update of column block kb + 1, then this side's column tile wave - 1
-//   wave 5        W_kb = L_kk^-1 into LDS, then column tile 3
-//   wave 6        the trailing tile (3,3) (panels 0, 1), then the x columns (a register tile)
-//   wave 7        the trailing tiles (2,2), (3,2) (panel 0); B: the Gram of x after the last panel
-//   wave 4        idle (SIMD 0)
-// Each tile receives its updates in panel order on one wave or behind an LDS counter, as in k_bcr_split.
-// The survived levels' pulls serve the factorization and the columns at once: D_i -= XR_a^T XR_a + XL_b^T XL_b
-// (lower tiles wave and wave + 8), x -= XR_a^T x_a + XL_b^T x_b (row tile wave - 4 on waves 4-7) and, at the
-// block's last survived level, this side's fill (XL_i = -XR_a^T XL_a, XR_i = -XL_b^T XR_b) on the column-tile
-// waves.
-struct TwLds {
-    double T[BB * BLD];                // D_i -> L (in place)
-    double Lcm[4][256];                // panel kb's diagonal tile, column-major (wave 0 -> wave 5)
-    double W[4][256];                  // W_kb = L_kk^-1 (wave 5 -> the column-tile waves)
-    double rdiag[BB];
-    double X[BB * XW];                 // [XL | XR | x]: this side's columns and x (B: XL joins for the back-substitution)
-    double U[4 * SG_W + 2 * RSZ / 4];  // pull staging; afterwards yl | yr | yt | bpl | red
-    double bk[16], bred[25], byk[4], bybl[G_DOF];
-    int ok;
-    int sync[16];  // [0] panels factored, [1..4] crit[kb], [5..8] trailing done per column block, [9] W_kb published
-};
-static constexpr int TW_YL = 0, TW_YR = RSZ, TW_YT = 2 * RSZ, TW_BPL = 3 * RSZ, TW_RED = 3 * RSZ + 25 * 32;
-static_assert(TW_RED + 100 <= 4 * SG_W + 2 * RSZ / 4, "yl | yr | yt | bpl | red fit the pull staging");
-static_assert(sizeof(TwLds) <= 160 * 1024, "twin workgroup LDS");
-
-template <bool STAMP>
-__global__ __launch_bounds__(TPB_E) void k_bcr_twin(const LmState* __restrict__ st, DevProblem P,
-                                                    const double* __restrict__ S, double* __restrict__ rhs,
-                                                    BcrWork Bw, int* __restrict__ flag,
-                                                    unsigned long long* __restrict__ tl, BaConsts c,
-                                                    const double* __restrict__ scale,
-                                                    const double* __restrict__ camdata,
-                                                    const double* __restrict__ lin, double* __restrict__ delta,
-                                                    double* __restrict__ part) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int nblk = Bw.nblk;
-    const int i = blockIdx.x >> 1;
-    const bool roleB = (blockIdx.x & 1) != 0;  // B: XR side, the Gram, the back-substitution (the root's only one)
-    const bool roleA = !roleB;
-    const bool root = i == Bw.vroot;
-    if (root && roleA) return;
-    const int mi = root ? Bw.vlevels : __builtin_ctz(i + Bw.voff);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
-    const size_t ld = P.npad;
-    const int nd = 6 * P.nac;
-    const int b0 = i * G_DOF;
-    constexpr int NQ = BSZ / TPB_E;
-    // the level-0 inputs from S, issued before the LM state is read (addresses from kernel arguments only)
-    double pd[NQ], px[NQ];
-    double pre_r = 0.0, pre_bk = 0.0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = tid + TPB_E * q, r = e >> 6, cc = e & 63;
-        const bool ok = cc <= r && r < G_DOF && b0 + r < nd;
-        pd[q] = S[ok ? (size_t)(b0 + r) * ld + b0 + cc : 0];
-    }
-    if (mi == 0) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int e = tid + TPB_E * q, r = e >> 6, cc = e & 63;
-            const int b1 = b0 + G_DOF;
-            const bool okl = i >= 1 && r < G_DOF && b0 + r < nd && cc < G_DOF;
-            const bool okr = i + 1 < nblk && r < G_DOF && b1 + r < nd && cc < G_DOF;
-            const size_t al = okl ? (size_t)(b0 + r) * ld + b0 - G_DOF + cc : 0;
-            const size_t ar = okr ? (size_t)(b1 + r) * ld + b0 + cc : 0;
-            px[q] = S[roleA ? al : ar];
-        }
-    }
-    {
-        const int r = tid >> 3, cc = tid & 7, gr = b0 + r;
-        const bool rok = r < G_DOF && gr < nd && cc <= 4;
-        pre_r = rok ? (cc == 0 ? rhs[gr] : S[(size_t)(P.kb + cc - 1) * ld + gr]) : 0.0;
-    }
-    if (root && tid < 14) {  // border inputs [b_k | S_kk packed]
-        int q = tid - 4, mm = 0;
-        while (q > mm) { q -= mm + 1; ++mm; }
-        pre_bk = tid < 4 ? rhs[P.kb + tid] : S[(size_t)(P.kb + mm) * ld + P.kb + q];
-    }
-    if (skip_step(st)) return;
-    TLS(0);
-    const unsigned spin_lim = g_spin_limit;
-    const unsigned epoch = Bw.flags[0] + 1;
-    unsigned* const gram_f = Bw.flags + 16 + 3 * nblk;
-    const int s_i = 1 << mi;
-    const bool has_r = !root && i + s_i < nblk;
-    const bool has_l = !root && i - s_i >= 0;
-    TwLds& L = *reinterpret_cast<TwLds*>(smem);
-    const int wu = __builtin_amdgcn_readfirstlane(wave);
-    // rows this workgroup publishes for the next level (pull hand-off)
-    const bool pubL = !root && roleA && has_l;
-    const bool pubR = !root && roleB && has_r;
-    const bool pubX = !root && roleA && (has_l || has_r);
-    double* const xl_pub = pub_xl(Bw, epoch) + (size_t)i * BSZ;
-    double* const xr_pub = pub_xr(Bw, epoch) + (size_t)i * BSZ;
-    double* const x_pub = pub_x(Bw, epoch) + (size_t)i * RSZ;
-    // this block's slots of the next epoch's buffers start empty (y, published rows)
-    if (roleB) reinterpret_cast<unsigned long long*>(ybuf(Bw, epoch + 1))[(size_t)i * RSZ + tid] = BCR_Y_EMPTY;
-    {
-        unsigned long long* nl = reinterpret_cast<unsigned long long*>(pub_xl(Bw, epoch + 1) + (size_t)i * BSZ);
-        unsigned long long* nr = reinterpret_cast<unsigned long long*>(pub_xr(Bw, epoch + 1) + (size_t)i * BSZ);
-        if (pubL)
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) nl[tid + TPB_E * q] = BCR_Y_EMPTY;
-        if (pubR)
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) nr[tid + TPB_E * q] = BCR_Y_EMPTY;
-        if (pubX) reinterpret_cast<unsigned long long*>(pub_x(Bw, epoch + 1) + (size_t)i * RSZ)[tid] = BCR_Y_EMPTY;
-    }
-    // level-0 inputs -> LDS
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = tid + TPB_E * q, r = e >> 6, cc = e & 63;
-        const bool ok = cc <= r && r < G_DOF && b0 + r < nd;
-        L.T[r * BLD + cc] = ok ? pd[q] : (r == cc ? 1.0 : 0.0);
-    }
-    if (mi == 0) {
-        const int b1 = b0 + G_DOF;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int e = tid + TPB_E * q, rq = e >> 6, cq = e & 63;
-            if (roleA) {
-                const bool okl = i >= 1 && rq < G_DOF && b0 + rq < nd && cq < G_DOF;
-                L.X[rq * XW + cq] = okl ? px[q] : 0.0;
-            } else {
-                const bool okr = i + 1 < nblk && rq < G_DOF && b1 + rq < nd && cq < G_DOF;
-                L.X[cq * XW + BB + rq] = okr ? px[q] : 0.0;
-            }
-        }
-    }
-    L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)] = pre_r;
-    if (root && tid < 14) L.bk[tid] = pre_bk;
-    if (tid < 16) L.sync[tid] = 0;
-    // Column tiles this wave owns (-1: none): this side's tile wave - 1 (waves 1-3) / 3 (wave 5); the x columns
-    // on wave 6 (tile 8). The root has only the x columns.
-    const int cbase = roleA ? 0 : 4;
-    const int own_cb = root ? (wu == 6 ? 8 : -1)
-                            : (wu >= 1 && wu <= 3 ? cbase + wu - 1 : (wu == 5 ? cbase + 3 : (wu == 6 ? 8 : -1)));
-    // ---- survived levels: pulled row blocks of the eliminated neighbours a = i - s, b = i + s
-    {
-        double* const sg = L.U;
-        const double* const sx = sg + 4 * SG_W;
-        int tib[2], tjb[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            int t = wu + NWE * q, ib = 0;
-            while (t > ib) { t -= ib + 1; ++ib; }
-            tib[q] = ib;
-            tjb[q] = t;
-        }
-        const int xr = wu - 4;                        // x row tile of waves 4-7
-        const bool fwave = own_cb >= 0 && own_cb < 8;  // column-tile waves (fills)
-        for (int m = 0; m < mi; ++m) {
-            const int s = 1 << m, a = i - s, b = i + s;
-            const bool ha = a >= 0, hb = b < nblk;
-            const bool last = m == mi - 1 && !root;
-            const bool fa = last && has_l && roleA, fb = last && has_r && roleB;
-            PullSrc<4, 2> ps;
-            ps.w[0] = ha ? pub_xr(Bw, epoch) + (size_t)a * BSZ : nullptr;
-            ps.w[1] = hb ? pub_xl(Bw, epoch) + (size_t)b * BSZ : nullptr;
-            ps.w[2] = fa ? pub_xl(Bw, epoch) + (size_t)a * BSZ : nullptr;
-            ps.w[3] = fb ? pub_xr(Bw, epoch) + (size_t)b * BSZ : nullptr;
-            ps.x[0] = ha ? pub_x(Bw, epoch) + (size_t)a * RSZ : nullptr;
-            ps.x[1] = hb ? pub_x(Bw, epoch) + (size_t)b * RSZ : nullptr;
-            const bool fon = fwave && (roleA ? fa : fb);
-            d4b dacc[2] = {d4b{0.0, 0.0, 0.0, 0.0}, d4b{0.0, 0.0, 0.0, 0.0}};
-            d4b xacc = {0.0, 0.0, 0.0, 0.0};
-            d4b facc[4];
-#pragma unroll
-            for (int ii = 0; ii < 4; ++ii) facc[ii] = d4b{0.0, 0.0, 0.0, 0.0};
-            Pull<4, 2> pl;
-            pl.issue(ps, 0);
-            for (int kb = 0; kb < 4; ++kb) {
-                if (!pl.commit(ps, kb, sg, &L.ok, spin_lim, true)) {
-                    if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-                    return;
-                }
-                if (kb < 3) pl.issue(ps, kb + 1);
-                // D_i: XR_a^T XR_a + XL_b^T XL_b on the lower tiles wave, wave + 8
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    if (wu + NWE * q >= 10) continue;
-#pragma unroll
-                    for (int src = 0; src < 2; ++src) {
-                        if (!(src ? hb : ha)) continue;
-                        const double* sgs = sg + src * SG_W;
-                        double av[4], bv[4];
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) {
-                            av[s4] = sgs[(4 * s4 + kk) * SG_LD + 16 * tib[q] + rr];
-                            bv[s4] = sgs[(4 * s4 + kk) * SG_LD + 16 * tjb[q] + rr];
-                        }
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) dacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], dacc[q], 0, 0, 0);
-                    }
-                }
-                // x: XR_a^T x_a + XL_b^T x_b (row tile xr on waves 4-7)
-                if (wu >= 4) {
-#pragma unroll
-                    for (int src = 0; src < 2; ++src) {
-                        if (!(src ? hb : ha)) continue;
-                        double av[4], bv[4];
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) {
-                            av[s4] = sg[src * SG_W + (4 * s4 + kk) * SG_LD + 16 * xr + rr];
-                            const double xb_ = sx[src * RSZ / 4 + (4 * s4 + kk) * RC + (rr & 7)];
-                            bv[s4] = rr < RC ? xb_ : 0.0;
-                        }
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) xacc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], xacc, 0, 0, 0);
-                    }
-                }
-                // this side's fill on its column tile
-                if (fon) {
-                    const double* sa = sg + (roleA ? 0 : 1) * SG_W;  // XR_a (A) / XL_b (B): row tiles of the fill
-                    const double* sb = sg + (roleA ? 2 : 3) * SG_W;  // XL_a (A) / XR_b (B): its column tile
-                    const int ct = own_cb & 3;
-                    double av[4][4], bv[4];
-#pragma unroll
-                    for (int s4 = 0; s4 < 4; ++s4) {
-                        bv[s4] = sb[(4 * s4 + kk) * SG_LD + 16 * ct + rr];
-#pragma unroll
-                        for (int ii = 0; ii < 4; ++ii) av[ii][s4] = sa[(4 * s4 + kk) * SG_LD + 16 * ii + rr];
-                    }
-#pragma unroll
-                    for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-                        for (int ii = 0; ii < 4; ++ii)
-                            facc[ii] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ii][s4], bv[s4], facc[ii], 0, 0, 0);
-                }
-            }
-            // the level's terms: D_i, x (rows of waves 4-7), this side's coupling of level mi (zero without the
-            // neighbour). Every read of sg / T / X above precedes the next commit's barrier or the one below.
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                if (wu + NWE * q >= 10) continue;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) L.T[(16 * tib[q] + kk + 4 * g) * BLD + 16 * tjb[q] + rr] -= dacc[q][g];
-            }
-            if (wu >= 4 && rr < RC)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) L.X[(16 * xr + kk + 4 * g) * XW + 2 * BB + rr] -= xacc[g];
-            if (last && fwave) {
-                const int col = (roleA ? 0 : BB) + 16 * (own_cb & 3);
-                const bool f = roleA ? fa : fb;
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) L.X[(16 * ii + kk + 4 * g) * XW + col + rr] = f ? -facc[ii][g] : 0.0;
-            }
-        }
-    }
-    __syncthreads();
-    TLS(1);
-    // ---- factorization (k_bcr_split's factor roles) interleaved with this side's forward substitution
-    double* T = L.T;
-    int* const sync = L.sync;
-    auto lds_ld = [&](int k) { return __hip_atomic_load(sync + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    auto spin_ge = [&](int k, int v) {
-        unsigned n = 0;
-        while (lds_ld(k) < v) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++n > SPIN_LIMIT) return false;
-        }
-        return true;
-    };
-    auto tile_sub = [&](int ii, int jj, int p) {  // T(ii,jj) -= L(ii,p) L(jj,p)^T
-        const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * p, BLD, T + (16 * jj) * BLD + 16 * p, BLD, rr, kk);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
-    };
-    auto signal = [&](int k) {  // one add per wave, after the wave's LDS stores
-        if (lane == 0) __hip_atomic_fetch_add(sync + k, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    // this wave's column tile in registers (MFMA accumulator layout, also the B-operand layout of a 16x16x4 step)
-    d4b xt[4];
-    {
-        const int col = own_cb >= 0 ? 16 * own_cb + rr : 0;
-        const bool colok = own_cb >= 0 && (own_cb < 8 || rr < RC);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) xt[ii][g] = colok ? L.X[(16 * ii + kk + 4 * g) * XW + col] : 0.0;
-    }
-    // panel kb applied to this wave's column tile: X_kb <- W_kb X_kb, X_ii -= L(ii,kb) X_kb (ii > kb); the
-    // finished row block to LDS (the Gram, the back-substitution) and, for the next level's pulls, to memory
-    auto apply_panel = [&](int kb) {
-        double aw[4], al[3][4];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) aw[s4] = L.W[kb][rr * 16 + 4 * s4 + kk];
-#pragma unroll
-        for (int ii = kb + 1; ii < 4; ++ii)
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) al[ii - kb - 1][s4] = -T[(16 * ii + rr) * BLD + 16 * kb + 4 * s4 + kk];
-        d4b w = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) w = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[s4], xt[kb][s4], w, 0, 0, 0);
-        xt[kb] = w;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-            for (int ii = kb + 1; ii < 4; ++ii)
-                xt[ii] = __builtin_amdgcn_mfma_f64_16x16x4f64(al[ii - kb - 1][s4], w[s4], xt[ii], 0, 0, 0);
-        const bool colok = own_cb < 8 || rr < RC;
-        if (colok)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) L.X[(16 * kb + kk + 4 * g) * XW + 16 * own_cb + rr] = w[g];
-        const bool pub = own_cb < 4 ? pubL : (own_cb < 8 ? pubR : (pubX && rr < RC));
-        if (pub) {
-            double* dst = own_cb < 4 ? xl_pub + 16 * own_cb : (own_cb < 8 ? xr_pub + 16 * (own_cb - 4) : x_pub);
-            const int ldd = own_cb < 8 ? BB : RC;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) st_pub(dst + (16 * kb + kk + 4 * g) * ldd + rr, w[g]);
-        }
-    };
-    bool ok = true;
-    if (wu == 0) {
-        bool bad = false;
-        for (int kb = 0; kb < 4; ++kb) {
-            if (kb > 0 && !spin_ge(1 + kb - 1, 4 - kb)) { ok = false; break; }  // column block kb updated
-            const int r = lane, row = 16 * kb + r;
-            const bool live = row < BB;
-            double a[16];
-#pragma unroll
-            for (int cc = 0; cc < 16; ++cc) a[cc] = live ? T[row * BLD + 16 * kb + cc] : 0.0;
-            double my_inv = 0.0;
-            double dn = bcast_b(a[0], 0);
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const double d = dn;
-                bad = bad || !(d > 0.0 && d < INFINITY);
-                const double y = __builtin_amdgcn_rsq(d);
-                const double e = __builtin_fma(-d * y, y, 1.0);
-                const double l = __builtin_fma(0.5 * a[j] * y, e, a[j] * y);
-                my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
-                a[j] = l;
-                if (j < 15) {
-                    dn = bcast_b(__builtin_fma(-l, l, a[j + 1]), j + 1);
-#pragma unroll
-                    for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast_b(l, k), a[k]);
-                }
-            }
-            if (live)
-#pragma unroll
-                for (int cc = 0; cc < 16; ++cc) T[row * BLD + 16 * kb + cc] = (r >= 16 || cc <= r) ? a[cc] : 0.0;
-            if (r < 16) {
-                L.rdiag[16 * kb + r] = my_inv;
-#pragma unroll
-                for (int cc = 0; cc < 16; ++cc) L.Lcm[kb][cc * 16 + r] = a[cc];
-            }
-            if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if constexpr (STAMP) if (lane == 0) tl[32 * blockIdx.x + 2 + kb] = realtime_now();
-        }
-        if (bad) raise_flag(flag, FLAG_NOT_PD);
-    } else if (wu != 4) {
-        // unrolled: the column tile's row tiles xt[kb] / xt[ii] are indexed by compile-time constants (a runtime
-        // panel index put them in scratch)
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            if (!ok) continue;
-            if (!spin_ge(0, kb + 1)) { ok = false; continue; }
-            if (wu <= 3 && kb + wu <= 3 && kb < 3) {  // the critical update of column block kb + 1
-                if (kb + 1 >= 2 && !spin_ge(5 + kb + 1, 2)) { ok = false; continue; }
-                tile_sub(kb + wu, kb + 1, kb);
-                signal(1 + kb);
-            } else if (wu == 6 && kb < 2) {  // tile (3,3): panels 0, 1
-                tile_sub(3, 3, kb);
-                signal(5 + 3);
-            } else if (wu == 7 && kb == 0) {  // tiles (2,2), (3,2): panel 0
-                tile_sub(2, 2, 0);
-                tile_sub(3, 2, 0);
-                __hip_atomic_fetch_add(sync + 5 + 2, lane == 0 ? 2 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            if (wu == 5) {
-                // W_kb = L_kk^-1, column `lane` per lane (lanes 0-15): forward substitution of e_lane against the
-                // column-major diagonal tile
-                if (lane < 16) {
-                    const double* Lc = L.Lcm[kb];
-                    const double* rd = L.rdiag + 16 * kb;
-                    double v[16];
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) v[m] = (m == lane) ? 1.0 : 0.0;
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) {
-                        v[m] *= rd[m];
-#pragma unroll
-                        for (int j = m + 1; j < 16; ++j) v[j] = __builtin_fma(-Lc[m * 16 + j], v[m], v[j]);
-                    }
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) L.W[kb][m * 16 + lane] = v[m];
-                }
-                signal(9);
-                if constexpr (STAMP) if (lane == 0) tl[32 * blockIdx.x + 6 + kb] = realtime_now();
-            }
-            if (own_cb >= 0) {
-                if (!spin_ge(9, kb + 1)) { ok = false; continue; }
-                apply_panel(kb);
-                if constexpr (STAMP) if (lane == 0 && wu == 6) tl[32 * blockIdx.x + 10 + kb] = realtime_now();
-            }
-        }
-    }
-    if (!__syncthreads_and(ok)) {
-        if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-        return;
-    }
-    TLS(14);
-    if (root) {
-        // the other blocks' Grams (published by their B workgroups after their forward substitution), summed
-        // in block order; then this block's own
-        if (!wait_all_eq(gram_f, nblk, epoch, &L.ok, i)) {
-            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-            return;
-        }
-        double* const bpl = L.U + TW_BPL;
-        double gsum = 0.0;
-        for (int j0 = 0; j0 < nblk; j0 += BP_CHUNK) {
-            const int nb = nblk - j0 < BP_CHUNK ? nblk - j0 : BP_CHUNK;
-            for (int e = tid; e < 25 * nb; e += TPB_E) bpl[e] = j0 + e / 25 == i ? 0.0 : ld_pub(Bw.Bp + (size_t)(j0 + e / 25) * 32 + e % 25);
-            __syncthreads();
-            if (tid < 25)
-                for (int b = 0; b < nb; ++b) gsum += bpl[25 * b + tid];
-            __syncthreads();
-        }
-        if (tid < 25) L.bred[tid] = gsum;
-        double* const Yl = L.U + TW_YT;
-        double* const red = L.U + TW_RED;
-        {
-            const int r = tid >> 3, cc = tid & 7;
-            Yl[tid] = L.X[r * XW + 2 * BB + cc];
-        }
-        __syncthreads();
-        // the root's Gram z^T z: 25 entries x 4 row quarters (fixed-order sums)
-        if (tid < 100) {
-            const int q = tid >> 2, part4 = tid & 3, gr = q / 5, gc = q % 5;
-            double acc = 0.0;
-#pragma unroll
-            for (int k = 16 * part4; k < 16 * part4 + 16; ++k) acc = __builtin_fma(Yl[k * RC + gr], Yl[k * RC + gc], acc);
-            red[tid] = acc;
-        }
-        __syncthreads();
-        // border system on one lane of wave 4 while waves 0-3 back-solve [u | V] = L^-T z
-        if (tid == 256) {
-            double g20[20];  // (B^T A^-1 [b_a | B])[m][c] = G[1 + m][c]
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int cc = 0; cc < 5; ++cc) {
-                    const int q = (1 + m) * 5 + cc;
-                    g20[m * 5 + cc] = L.bred[q] + (((red[4 * q] + red[4 * q + 1]) + red[4 * q + 2]) + red[4 * q + 3]);
-                }
-            bool bad = false;
-            border_solve4(L.bk, g20, L.byk, bad);
-            if (bad) raise_flag(flag, FLAG_NOT_PD);
-        }
-        trsm_t_lanes(L.T, L.rdiag, Yl);  // ends with a barrier
-        st_pub(ybuf(Bw, epoch) + (size_t)i * RSZ + tid, ((tid & 7) == 5 && tid < 4 * RC) ? L.byk[tid >> 3] : Yl[tid]);
-        TLS(15);
-        block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, true, Yl, L.byk, L.bybl);
-        return;
-    }
-    if (roleA) return;  // A's rows are all published
-    // B: the Gram x^T x (5 x 5) -> Bp[i], published with its flag (the root sums every block's)
-    if (wu == 7) {
-        d4b gacc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            double xv[4];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const double v = L.X[(16 * kb + 4 * s4 + kk) * XW + 2 * BB + (rr & 7)];
-                xv[s4] = rr < RC ? v : 0.0;
-            }
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s4], xv[s4], gacc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            if (kk + 4 * g < 5 && rr < 5) st_pub(Bw.Bp + (size_t)i * 32 + (kk + 4 * g) * 5 + rr, gacc[g]);
-    }
-    publish_flag(gram_f + i, epoch);
-    // the back-substitution needs XL: A's published rows (out long ago; polled value by value)
-    {
-        const double* xs = pub_xl(Bw, epoch) + (size_t)i * BSZ;
-        unsigned long long xv[BSZ / TPB_E];
-#pragma unroll
-        for (int u = 0; u < BSZ / TPB_E; ++u) xv[u] = has_l ? ld_u64(xs + tid + TPB_E * u) : 0ull;
-        int okp = 1;
-        for (unsigned n = 0;; ++n) {
-            bool pend = false;
-#pragma unroll
-            for (int u = 0; u < BSZ / TPB_E; ++u) pend = pend || xv[u] == BCR_Y_EMPTY;
-            if (!pend) break;
-            if (n > SPIN_LIMIT) { okp = 0; break; }
-            __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int u = 0; u < BSZ / TPB_E; ++u)
-                if (xv[u] == BCR_Y_EMPTY) xv[u] = ld_u64(xs + tid + TPB_E * u);
-        }
-#pragma unroll
-        for (int u = 0; u < BSZ / TPB_E; ++u) {
-            const int e = tid + TPB_E * u;
-            L.X[(e >> 6) * XW + (e & 63)] = __longlong_as_double((long long)xv[u]);
-        }
-        if (!__syncthreads_and(okp)) {
-            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-            return;
-        }
-    }
-    // ---- off the critical path: [P | Q | u] = L^-T [XL | XR | x]; then y_i = u - P y_{i-s} - Q y_{i+s}
-    trsm_lower64_t(L.T, L.rdiag, L.X, XW, XC);
-    double* const yl = L.U + TW_YL;
-    double* const yr = L.U + TW_YR;
-    double* const yt = L.U + TW_YT;
-    {
-        const double* Yb = ybuf(Bw, epoch);
-        const double* pl = Yb + (size_t)(i - s_i) * RSZ + tid;
-        const double* pr = Yb + (size_t)(i + s_i) * RSZ + tid;
-        const double* pk = Yb + (size_t)Bw.vroot * RSZ + tid * RC + 5;
-        unsigned long long ul = has_l ? ld_u64(pl) : 0ull, ur = has_r ? ld_u64(pr) : 0ull, uk = tid < 4 ? ld_u64(pk) : 0ull;
-        int okp = 1;
-        unsigned n = 0;
-        while (ul == BCR_Y_EMPTY || ur == BCR_Y_EMPTY || uk == BCR_Y_EMPTY) {
-            __builtin_amdgcn_s_sleep(1);
-            if (ul == BCR_Y_EMPTY) ul = ld_u64(pl);
-            if (ur == BCR_Y_EMPTY) ur = ld_u64(pr);
-            if (uk == BCR_Y_EMPTY) uk = ld_u64(pk);
-            if (++n > SPIN_LIMIT) { okp = 0; break; }
-        }
-        yl[tid] = __longlong_as_double((long long)ul);
-        yr[tid] = __longlong_as_double((long long)ur);
-        if (tid < 4) L.byk[tid] = __longlong_as_double((long long)uk);
-        yt[tid] = L.X[(tid >> 3) * XW + 2 * BB + (tid & 7)];
-        if (!__syncthreads_and(okp)) {
-            if (tid == 0) raise_flag(flag, FLAG_TIMEOUT);
-            return;
-        }
-    }
-    TLS(16);
-    {
-        // y_i = u - P y_l - Q y_r on all 8 waves: wave w owns row block w & 3 and half (w >> 2) of the 64-deep
-        // contraction; the second half's partials meet the first's in LDS
-        const int rb = wave & 3, kh = wave >> 2;
-        double al[8], ar[8], bl[8], br[8];
-#pragma unroll
-        for (int s4 = 0; s4 < 8; ++s4) {
-            const int k = 8 * kh + s4;
-            const double* row = L.X + (16 * rb + rr) * XW + 4 * k + kk;
-            al[s4] = has_l ? row[0] : 0.0;
-            ar[s4] = has_r ? row[BB] : 0.0;
-            bl[s4] = has_l && rr < RC ? yl[(4 * k + kk) * RC + rr] : 0.0;
-            br[s4] = has_r && rr < RC ? yr[(4 * k + kk) * RC + rr] : 0.0;
-        }
-        d4b acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s4 = 0; s4 < 8; ++s4) {
-            if (has_l) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(al[s4], bl[s4], acc0, 0, 0, 0);
-            if (has_r) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s4], br[s4], acc1, 0, 0, 0);
-        }
-        double* part2 = L.U + TW_BPL;  // 64 x RC partials of the second half
-        if (kh == 1 && rr < RC)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) part2[(16 * rb + kk + 4 * g) * RC + rr] = acc0[g] + acc1[g];
-        __syncthreads();
-        if (kh == 0 && rr < RC) {
-            double* yout = ybuf(Bw, epoch) + (size_t)i * RSZ;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int e = (16 * rb + kk + 4 * g) * RC + rr;
-                const double v = yt[e] - ((acc0[g] + acc1[g]) + part2[e]);
-                st_pub(yout + e, v);
-                yt[e] = v;
-            }
-        }
-    }
-    __syncthreads();
-    TLS(15);
-    block_step(st, P, rhs, c, scale, camdata, lin, delta, part, i, false, yt, L.byk, L.bybl);
-}
 #undef TLS
 static_assert(PANEL_DOUBLES <= BCR_BLOCK_DOUBLES, "published panels fit the block's workspace");
 static_assert(2 * PANEL_DOUBLES <= BB * BB + BB * XW, "two epochs' panels fit the Cf | X slots");
@@ -2852,11 +2266,6 @@ template <bool STAMP>
 static hipError_t launch_bcr_t(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
     const int nblk = Bw.nblk;
-    if (Bw.persist == 4) {  // twin workgroups, each factoring its block (the border solve and camera step inside)
-        BPL(K_BCR_PERSIST, k_bcr_twin<STAMP>, dim3(2 * nblk), dim3(TPB_E), sizeof(TwLds), s, W.st, P, W.S, W.rhs, Bw,
-            W.chol_flag, stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
-        return hipSuccess;
-    }
     if (Bw.persist >= 2) {
         // the border solve and the camera step run inside the split kernel (no k_bcr_border launch)
         const hipError_t e = Bw.persist == 3 ? launch_split<STAMP, 2>(P, c, W, Bw, s, stamps, pf)
@@ -2912,10 +2321,7 @@ static hipError_t bcr_persist_attr() {
         const void* fns[] = {(const void*)k_bcr_split<false, 1>, (const void*)k_bcr_split<true, 1>,
                              (const void*)k_bcr_split<false, 2>, (const void*)k_bcr_split<true, 2>};
         for (const void* f : fns) CKB(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(HLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_twin<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(TwLds)));
-        CKB(hipFuncSetAttribute((const void*)k_bcr_twin<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(TwLds)));
+
         done = true;
     }
     return hipSuccess;
@@ -2935,15 +2341,6 @@ hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s) {
 
 hipError_t bcr_set_spin_limit(unsigned limit) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &limit, sizeof(limit));
-}
-
-bool bcr_twin_ok(int nblk) {
-    if (bcr_persist_attr() != hipSuccess) return false;
-    int dev = 0, ncu = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_twin<false>, TPB_E, sizeof(TwLds)) == hipSuccess &&
-           per_cu >= 1 && 2 * nblk <= per_cu * ncu;
 }
 
 int bcr_persist_ok(int nblk) {
@@ -2982,21 +2379,6 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
         static unsigned long long h[NSTAMP];
         CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
-        if (Bw.persist == 4) {
-            unsigned long long t0 = ~0ull;
-            for (int g = 0; g < 2 * Bw.nblk && g < 256; ++g) if (h[32 * g]) t0 = std::min(t0, h[32 * g]);
-            auto us = [&](unsigned long long t) { return t ? (double)(t - t0) * 0.01 : -1.0; };
-            for (int g = 0; g < 2 * Bw.nblk && g < 256; ++g) {
-                const unsigned long long* q = h + 32 * g;
-                if (!q[0]) continue;
-                fprintf(stderr, "bcr T%c%3d start %7.2f loaded %7.2f chain %7.2f %7.2f %7.2f %7.2f W %7.2f %7.2f %7.2f %7.2f "
-                                "x-applied %7.2f %7.2f %7.2f %7.2f factored %7.2f back-wait %7.2f done %7.2f\n",
-                        g & 1 ? 'B' : 'A', g / 2, us(q[0]), us(q[1]), us(q[2]), us(q[3]), us(q[4]), us(q[5]), us(q[6]),
-                        us(q[7]), us(q[8]), us(q[9]), us(q[10]), us(q[11]), us(q[12]), us(q[13]), us(q[14]), us(q[16]),
-                        us(q[15]));
-            }
-            return hipSuccess;
-        }
         if (Bw.persist >= 2) {
             const int nr = Bw.persist;  // workgroups per block
             unsigned long long t0 = ~0ull;

@@ -134,8 +134,7 @@ struct BcrWork {
     unsigned* flags;  // flags[0] (the epoch) is advanced by k_final after every BCR launch that ran
     int nblk, levels;
     int voff, vroot, vlevels;  // k_bcr_split: balanced tree on v = i + voff, root block vroot, depth vlevels + 1
-    int persist;  // 4 = two twin workgroups per block, each factoring it (k_bcr_twin),
-                  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
+    int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level
 };
@@ -345,8 +344,6 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
 // 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);
-// the 2 * nblk workgroups of k_bcr_twin (each factoring its block) can all be resident on the current device
-bool bcr_twin_ok(int nblk);
 // k_bcr_split's pull slots: empty (split = true, Bw.persist >= 2) or zero (the per-level / persistent paths)
 hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s);
 // spin bound of the resident BCR kernels' inter-workgroup waits (default 1 << 22 polls; tests force a

@@ -589,8 +589,7 @@ static int bcr_setup(ba_context* ctx) {
     if (const char* e = std::getenv("MIBA_BCR")) {
         if (!std::strcmp(e, "launch")) Bw.persist = 0;
         else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
-        else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;
-        else if (!std::strcmp(e, "twin") && bcr_twin_ok(Bw.nblk)) Bw.persist = 4;  // "split3" or unset: default
+        else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;  // "split3" or unset: default
     }
     ctx->bcr_fallback = false;
     return bcr_init_handoffs(ctx);
@@ -1558,8 +1557,7 @@ extern "C" int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, i
     for (int k = 0; k < K_COUNT && n < max_n; ++k, ++n) {
         std::memset(&out[n], 0, sizeof(ba_kernel_stat));
         // the resident BCR id times whichever resident kernel the window runs: name it after that kernel
-        const char* nm = (k == K_BCR_PERSIST && ctx->W.bcr.persist >= 2) ? (ctx->W.bcr.persist == 4 ? "bcr_twin" : "bcr_split")
-                                                                         : kKernelNames[k];
+        const char* nm = (k == K_BCR_PERSIST && ctx->W.bcr.persist >= 2) ? "bcr_split" : kKernelNames[k];
         std::snprintf(out[n].name, sizeof(out[n].name), "%s", nm);
         out[n].launches = ctx->k_launches[k];
         out[n].total_ms = ctx->k_ms[k];

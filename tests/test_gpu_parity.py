@@ -196,7 +196,7 @@ def test_comm_init_rejects_bad_rank():
 @pytest.mark.parametrize("n_cams", [23, 64, 200, 333])
 def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
     """The persistent BCR kernels (one resident workgroup per 10-camera block; factor + one helper;
-    factor + two helpers; two twin workgroups each factoring the block) against the per-level
+    factor + two helpers, the default where 3 workgroups per block fit) against the per-level
     launches and the oracle. The GPU paths sum the contributions in different orders and the Schur
     flush into S uses f64 atomics, so they agree to rounding: tolerances off, all run exactly 6
     iterations."""
@@ -205,7 +205,7 @@ def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
     res = {}
-    paths = {"launch": 0, "persist": 1, "split": 2, "split3": 3, "twin": 4}
+    paths = {"launch": 0, "persist": 1, "split": 2, "split3": 3}
     for mode in paths:
         monkeypatch.setenv("MIBA_BCR", mode)
         q = p.copy()
@@ -214,7 +214,7 @@ def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
             assert s.last_prepare()["bcr_path"] == paths[mode], mode
     sa, qa = res["launch"]
     assert sa["linear_solver"] == LS["bcr"]
-    for mode in ("persist", "split", "split3", "twin"):
+    for mode in ("persist", "split", "split3"):
         sb, qb = res[mode]
         assert sb["linear_solver"] == LS["bcr"], mode
         assert sa["num_iterations"] == sb["num_iterations"] == 6, mode

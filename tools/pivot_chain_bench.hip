@@ -5,6 +5,7 @@
 //   1  the next pivot from the reciprocal: dn = a_{j+1,j+1} - a_{j+1,j}^2 / d_j with r = rcp(d) + one Newton
 //      step (rcp + 3 dependent ops + readlane on the chain instead of rsq + 4); l and the trailing updates as 0
 //   2  variant 0 without the trailing updates (the chain alone: a lower bound)
+//   3  variant 0 with the trailing updates of columns j + 2.. fed by an LDS broadcast of the multipliers
 // Reports ns and shader cycles per pivot and the max |L L^T - A| of the last repetition.
 // build: hipcc --offload-arch=gfx950 -O3 tools/pivot_chain_bench.hip -o /tmp/pcb && /tmp/pcb
 #include <hip/hip_runtime.h>
@@ -30,9 +31,43 @@ __device__ __forceinline__ unsigned long long clk() {
 }
 
 template <int V>
-__device__ __forceinline__ void chain(double (&a)[16], double& my_inv) {
+__device__ __forceinline__ void chain(double (&a)[16], double& my_inv, double* lb) {
     const int r = threadIdx.x & 63;
-    if constexpr (V == 0 || V == 2) {
+    if constexpr (V == 3) {
+        // the next column by v_readlane (on the chain); columns j + 2.. by an LDS broadcast of the multipliers
+        // (lanes 0-15 store l, every lane reads l_k two at a time with uniform-address ds_read_b128): the
+        // trailing updates cost one FMA per column instead of two v_readlane_b32 + one FMA
+        double dn = bcast(a[0], 0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double d = dn;
+            const double y = __builtin_amdgcn_rsq(d);
+            const double e = __builtin_fma(-d * y, y, 1.0);
+            const double l = __builtin_fma(0.5 * a[j] * y, e, a[j] * y);
+            my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+            a[j] = l;
+            if (j < 15) {
+                dn = bcast(__builtin_fma(-l, l, a[j + 1]), j + 1);
+                a[j + 1] = __builtin_fma(-l, bcast(l, j + 1), a[j + 1]);
+                if (j < 14) {
+                    if (r < 16) lb[r] = l;
+                    __builtin_amdgcn_wave_barrier();
+                    int k = j + 2;
+                    if (k & 1) {
+                        a[k] = __builtin_fma(-l, lb[k], a[k]);
+                        ++k;
+                    }
+#pragma unroll
+                    for (; k < 16; k += 2) {
+                        const double2 lk = *reinterpret_cast<const double2*>(lb + k);
+                        a[k] = __builtin_fma(-l, lk.x, a[k]);
+                        a[k + 1] = __builtin_fma(-l, lk.y, a[k + 1]);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+        }
+    } else if constexpr (V == 0 || V == 2) {
         double dn = bcast(a[0], 0);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -85,12 +120,13 @@ __global__ __launch_bounds__(64) void k_bench(const double* __restrict__ A, doub
     double a0[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) a0[c] = A[r * 16 + c];
+    __shared__ __attribute__((aligned(16))) double lb[16];
     double a[16], my_inv = 0.0, sink = 0.0;
     const unsigned long long t0 = rt(), c0 = clk();
     for (int it = 0; it < reps; ++it) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) a[c] = a0[c] + sink * 1e-300;  // depends on the previous repetition
-        chain<V>(a, my_inv);
+        chain<V>(a, my_inv, lb);
         sink = bcast(a[15], 63);
     }
     const unsigned long long c1 = clk(), t1 = rt();
@@ -118,12 +154,14 @@ int main() {
     (void)hipMalloc(&dA, 8 * A.size()); (void)hipMalloc(&dL, 8 * A.size()); (void)hipMalloc(&dt, 16);
     (void)hipMemcpy(dA, A.data(), 8 * A.size(), hipMemcpyHostToDevice);
     const int reps = 2000;
-    const char* names[3] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)"};
+    const char* names[4] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)",
+                            "LDS-broadcast trailing"};
     for (int round = 0; round < 2; ++round)
-        for (int v = 0; v < 3; ++v) {
+        for (int v = 0; v < 4; ++v) {
             if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 2) hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 3) hipLaunchKernelGGL(k_bench<3>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             unsigned long long t[2];
             std::vector<double> L(64 * 16);
             (void)hipMemcpy(t, dt, 16, hipMemcpyDeviceToHost);
