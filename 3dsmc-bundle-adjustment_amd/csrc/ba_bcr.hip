@@ -1633,6 +1633,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             for (int kb = 0; kb < 4; ++kb) {
                 if (kb > 0 && !spin_ge(1 + kb - 1, 4 - kb)) { ok = false; break; }  // column block kb updated
                 TLS(17 + 3 * kb);
+                // shader-clock stamps of the first and last chains (slots 28-31): cycles per pivot in the kernel,
+                // beside the micro-benchmark's (tools/pivot_chain_bench.hip)
+                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 28 + (kb ? 2 : 0)] = bcr_stamp();
                 const int r = lane, row = 16 * kb + r;
                 const bool live = row < BB;
                 double a[16];
@@ -1665,6 +1668,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                     for (int c = 0; c < 16; ++c) L.Lcm[kb][c * 16 + r] = a[c];  // strictly-lower part is what W reads
                 }
+                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 29 + (kb ? 2 : 0)] = bcr_stamp();
                 if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 // publish the panel's L tiles straight from the chain's registers (column-major: one
                 // coalesced row of 64 per store); W_kb and 1/diag follow from wave 5
@@ -2392,6 +2396,9 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
                     fprintf(stderr, "        chain start | chain end | published:");
                     for (int kb = 0; kb < 4; ++kb)
                         fprintf(stderr, "  %7.2f %7.2f %7.2f", us(q[17 + 3 * kb]), us(q[16 + 3 * kb]), us(q[2 + kb]));
+                    // shader clocks per pivot (LDS loads .. chain .. LDS stores) and the clock rate they imply
+                    const double c0 = (double)(q[29] - q[28]) / 16.0, c3 = (double)(q[31] - q[30]) / 16.0;
+                    fprintf(stderr, "  | chain clk/pivot %.0f %.0f", c0, c3);
                     fprintf(stderr, "\n");
                 } else
                 {

@@ -72,5 +72,28 @@ int main() {
             (void)hipEventElapsedTime(&ms, e0, e1);
             printf("round %d  %-24s %6.2f us per launch\n", round, names[v], ms * 1000.0 / n);
         }
+    // the same chains captured into one hipGraph (host launch cost out of the picture)
+    for (int v = 0; v < 6; v += 5) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        (void)hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+        for (int i = 0; i < n; ++i) {
+            if (v == 0) hipLaunchKernelGGL(k<0>, dim3(1), dim3(64), 0, s, dev, host);
+            else hipLaunchKernelGGL(k<5>, dim3(1), dim3(256), 0, s, dev, host);
+        }
+        (void)hipStreamEndCapture(s, &g);
+        (void)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphLaunch(ge, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipEventRecord(e0, s);
+        (void)hipGraphLaunch(ge, s);
+        (void)hipEventRecord(e1, s);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        printf("graph    %-24s %6.2f us per launch\n", names[v], ms * 1000.0 / n);
+        (void)hipGraphExecDestroy(ge);
+        (void)hipGraphDestroy(g);
+    }
     return 0;
 }
