@@ -1633,9 +1633,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
             for (int kb = 0; kb < 4; ++kb) {
                 if (kb > 0 && !spin_ge(1 + kb - 1, 4 - kb)) { ok = false; break; }  // column block kb updated
                 TLS(17 + 3 * kb);
-                // shader-clock stamps of the first and last chains (slots 28-31): cycles per pivot in the kernel,
-                // beside the micro-benchmark's (tools/pivot_chain_bench.hip)
-                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 28 + (kb ? 2 : 0)] = bcr_stamp();
                 const int r = lane, row = 16 * kb + r;
                 const bool live = row < BB;
                 double a[16];
@@ -1643,6 +1640,9 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 for (int c = 0; c < 16; ++c) a[c] = live ? T[row * BLD + 16 * kb + c] : 0.0;
                 double my_inv = 0.0;
                 double dn = bcast_b(a[0], 0);
+                // shader-clock stamps around the first and last chains' pivots (slots 28-31): cycles per pivot in
+                // the kernel, beside the micro-benchmark's (tools/pivot_chain_bench.hip)
+                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 28 + (kb ? 2 : 0)] = bcr_stamp();
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     // d = current pivot; y ~ d^-1/2 (v_rsq_f64), one Newton step folded into l = a y (1 + e/2)
@@ -1660,6 +1660,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                         for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast_b(l, k), a[k]);
                     }
                 }
+                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 29 + (kb ? 2 : 0)] = bcr_stamp();
                 if (live)
 #pragma unroll
                     for (int c = 0; c < 16; ++c) T[row * BLD + 16 * kb + c] = (r >= 16 || c <= r) ? a[c] : 0.0;
@@ -1668,7 +1669,6 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 #pragma unroll
                     for (int c = 0; c < 16; ++c) L.Lcm[kb][c * 16 + r] = a[c];  // strictly-lower part is what W reads
                 }
-                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 29 + (kb ? 2 : 0)] = bcr_stamp();
                 if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 // publish the panel's L tiles straight from the chain's registers (column-major: one
                 // coalesced row of 64 per store); W_kb and 1/diag follow from wave 5
