@@ -889,7 +889,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         }
         return;
     }
-    unsigned long long t_prev = 0, st_acc[4] = {0, 0, 0, 0};
+    unsigned long long t_prev = 0, st_acc[5] = {0, 0, 0, 0, 0};
 #define SCH_STAMP(k)                                          \
     do {                                                      \
         if constexpr (STAMP) {                                \
@@ -975,9 +975,14 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     for (;;) {
         const int npts = ape - apb;
         {
-            double2* M2 = reinterpret_cast<double2*>(Mt);
-            for (int e = tid; e < SCH_K * SCH_LDM / 2; e += TPB) M2[e] = double2{0.0, 0.0};
+            // every thread the same number of 16-byte stores, unrolled: straight-line ds_write_b128 with immediate
+            // offsets (the strided loop spent ~120 instructions of issue per thread on 15 stores)
+            static_assert(SCH_K * SCH_LDM / 2 % TPB == 0, "zeroing: whole rounds");
+            double2* M2 = reinterpret_cast<double2*>(Mt) + tid;
+#pragma unroll
+            for (int i = 0; i < SCH_K * SCH_LDM / 2 / TPB; ++i) M2[TPB * i] = double2{0.0, 0.0};
         }
+        SCH_STAMP(4);  // zero stores issued (wave 0); slot 0 is then the barrier
         __syncthreads();
         SCH_STAMP(0);
         // ---- phase A
@@ -1157,7 +1162,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         __syncthreads();
         SCH_STAMP(3);
         if (threadIdx.x == 0)
-            for (int k = 0; k < 4; ++k) stamps[(size_t)blockIdx.x * 4 + k] = st_acc[k];
+            for (int k = 0; k < 5; ++k) stamps[(size_t)blockIdx.x * 5 + k] = st_acc[k];
     }
 #undef SCH_STAMP
 }
@@ -2555,22 +2560,24 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
         if (smode == 1) {
             if (scap < P.n_tiles) {
                 if (sst) CK(hipFree(sst));
-                CK(hipMalloc(&sst, sizeof(unsigned long long) * 4 * P.n_tiles));
+                CK(hipMalloc(&sst, sizeof(unsigned long long) * 5 * P.n_tiles));
                 scap = P.n_tiles;
             }
             OPL(K_SCHUR_TILE, (k_schur_tile<true, true>), (k_schur_tile<true, false>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
                sst, pp_parts(P), W.part, W.det_tbuf, E);
-            std::vector<unsigned long long> h((size_t)4 * P.n_tiles);
-            CK(hipMemcpyAsync(h.data(), sst, sizeof(h[0]) * h.size(), hipMemcpyDeviceToHost, s));
+            std::vector<unsigned long long> h5((size_t)5 * P.n_tiles), h((size_t)4 * P.n_tiles);
+            CK(hipMemcpyAsync(h5.data(), sst, sizeof(h5[0]) * h5.size(), hipMemcpyDeviceToHost, s));
             CK(hipStreamSynchronize(s));
-            double sum[4] = {0, 0, 0, 0}, mx = 0;
+            double sum[5] = {0, 0, 0, 0, 0}, mx = 0;
             for (int t = 0; t < P.n_tiles; ++t) {
                 double tot = 0;
-                for (int k = 0; k < 4; ++k) { sum[k] += (double)h[4 * t + k]; tot += (double)h[4 * t + k]; }
+                for (int k = 0; k < 5; ++k) { sum[k] += (double)h5[5 * t + k]; tot += (double)h5[5 * t + k]; }
+                for (int k = 0; k < 4; ++k) h[4 * t + k] = h5[5 * t + k] + (k == 0 ? h5[5 * t + 4] : 0ull);
                 mx = std::max(mx, tot);
             }
-            fprintf(stderr, "schur_tile %d tiles, mean cycles/tile: zero %.0f phaseA %.0f phaseB %.0f flush %.0f | max total %.0f\n",
-                    P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
+            fprintf(stderr, "schur_tile %d tiles, mean cycles/tile: zero %.0f (stores %.0f, barrier %.0f) phaseA %.0f phaseB %.0f flush %.0f | max total %.0f\n",
+                    P.n_tiles, (sum[0] + sum[4]) / P.n_tiles, sum[4] / P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles,
+                    sum[2] / P.n_tiles, sum[3] / P.n_tiles, mx);
             // the slowest tiles: span, chunks, points (the kernel lasts as long as its slowest tile)
             std::vector<int> tspan(P.n_tiles), tch(P.n_tiles + 1), cap;
             CK(hipMemcpy(tspan.data(), P.tile_span, sizeof(int) * P.n_tiles, hipMemcpyDeviceToHost));
