@@ -2200,6 +2200,196 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 }
 
 #undef TLS
+
+// ---- one-block windows (<= 10 active cameras: the reference's TUM windows) -------------------------------------
+// The whole reduced system — the 6 nac camera dofs and the 4 intrinsics rows that follow them in S, n = 6 nac + 4
+// <= 64 — is one dense SPD block. One workgroup loads it into LDS (identity pad), factors it with the split
+// kernel's pivot chain on wave 0 and the trailing tiles on the other waves' f64 MFMA, solves L z = b and
+// L^T y = z on wave 0 (lane = row, v_readlane broadcasts, the next column prefetched) and applies the camera /
+// intrinsics step (block_step with y in the u column): no border system, no cross-workgroup hand-off — the split
+// kernel's factor / helper pair spends ~5 us of a ~21 us one-block launch on those (C1 stamps).
+static constexpr int TPB_D1 = 256;
+// STAMP: s_memrealtime after each phase into tl[0..8] (loaded, 4 panels, forward, backward, step)
+template <bool STAMP>
+__global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict__ st, DevProblem P,
+                                                      const double* __restrict__ S, double* __restrict__ rhs,
+                                                      int* __restrict__ flag, BaConsts c,
+                                                      const double* __restrict__ scale,
+                                                      const double* __restrict__ camdata,
+                                                      const double* __restrict__ lin, double* __restrict__ delta,
+                                                      double* __restrict__ part, unsigned long long* __restrict__ tl) {
+#define D1S(k)                                                                      \
+    do {                                                                            \
+        if constexpr (STAMP) if (threadIdx.x == 0) tl[(k)] = realtime_now();        \
+    } while (0)
+    D1S(9);
+    __shared__ __attribute__((aligned(16))) double T[BB * BLD];
+    __shared__ double rdg[BB];
+    __shared__ double Wm[4][256];          // W_kb = L_kk^-1, row-major
+    __shared__ double vr[BB], vz[BB];      // wave 0's broadcast rows of the blocked triangular solves
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
+    const int n = P.kb + 4;  // camera dofs, then the intrinsics rows (P.kb = 6 nac)
+    const size_t ld = P.npad;
+    // the lower triangle (every load in flight together: clamped addresses, selects after)
+    {
+        constexpr int NL = BB * BB / TPB_D1;
+        double v[NL];
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
+            const int e = tid + TPB_D1 * q, r = e >> 6, cc = e & 63;
+            const bool ok = cc <= r && r < n;
+            v[q] = S[ok ? (size_t)r * ld + cc : 0];
+        }
+        if (skip_step(st)) return;
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
+            const int e = tid + TPB_D1 * q, r = e >> 6, cc = e & 63;
+            T[r * BLD + cc] = (cc <= r && r < n) ? v[q] : (r == cc ? 1.0 : 0.0);
+        }
+    }
+    // the step's operands (cameras on wave 0's lanes < nac, the intrinsics on lane BCR_CAMS), in flight through
+    // the factorization
+    const int cur = st->cur;
+    const double radius = st->radius;
+    CamStepOps cops;
+    IntrStepOps iops;
+    if (wave == 0 && lane < P.nac) load_cam_step_ops(P, cur, scale, camdata, lane, cops);
+    if (wave == 0 && lane == BCR_CAMS) load_intr_step_ops(P, cur, scale, lin, iops);
+    double b = (wave == 0 && lane < n) ? rhs[lane] : 0.0;
+    __syncthreads();
+    D1S(0);
+    bool bad = false;
+    for (int kb = 0; kb < 4; ++kb) {
+        if (wave == 0) {  // the pivot chain of the tall column block kb (k_bcr_split's wave 0)
+            const int r = lane, row = 16 * kb + r;
+            const bool live = row < BB;
+            double a[16];
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) a[cc] = live ? T[row * BLD + 16 * kb + cc] : 0.0;
+            double my_inv = 0.0;
+            double dn = bcast_b(a[0], 0);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const double d = dn;
+                bad = bad || !(d > 0.0 && d < INFINITY);
+                const double y = __builtin_amdgcn_rsq(d);
+                const double e = __builtin_fma(-d * y, y, 1.0);
+                const double l = __builtin_fma(0.5 * a[j] * y, e, a[j] * y);
+                my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+                a[j] = l;
+                if (j < 15) {
+                    dn = bcast_b(__builtin_fma(-l, l, a[j + 1]), j + 1);
+#pragma unroll
+                    for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast_b(l, k), a[k]);
+                }
+            }
+            if (live)
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) T[row * BLD + 16 * kb + cc] = (r >= 16 || cc <= r) ? a[cc] : 0.0;
+            if (r < 16) rdg[16 * kb + r] = my_inv;
+        }
+        __syncthreads();
+        // trailing tiles (ii, jj), kb < jj <= ii < 4: T(ii,jj) -= L(ii,kb) L(jj,kb)^T, round-robin over the waves
+        const int m = 3 - kb, ntl = m * (m + 1) / 2;
+        for (int t = wave; t < ntl; t += TPB_D1 / 64) {
+            int q = t, ib = 0;
+            while (q > ib) { q -= ib + 1; ++ib; }
+            const int ii = kb + 1 + ib, jj = kb + 1 + q;
+            const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * kb, BLD, T + (16 * jj) * BLD + 16 * kb, BLD, rr, kk);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
+        }
+        __syncthreads();
+        D1S(1 + kb);
+    }
+    // W_kb = L_kk^-1 on wave kb (lanes 0-15, column `lane` by forward substitution; k_bcr_split's wave-5 form)
+    if (lane < 16) {
+        const int kb = wave;
+        double w[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) w[m] = (m == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            w[m] *= rdg[16 * kb + m];
+#pragma unroll
+            for (int j = m + 1; j < 16; ++j) w[j] = __builtin_fma(-T[(16 * kb + j) * BLD + 16 * kb + m], w[m], w[j]);
+        }
+#pragma unroll
+        for (int m = 0; m < 16; ++m) Wm[kb][m * 16 + lane] = w[m];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        auto wsync = [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        // L z = b by 16-row blocks: z_kb = W_kb r_kb, then r -= L(:, kb) z_kb below (lane = row)
+        for (int kb = 0; kb < 4; ++kb) {
+            const bool in = (lane >> 4) == kb;
+            if (in) vr[lane] = b;
+            wsync();
+            if (in) {
+                double z = 0.0;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) z = __builtin_fma(Wm[kb][(lane & 15) * 16 + m], vr[16 * kb + m], z);
+                b = z;
+                vz[lane] = z;
+            }
+            wsync();
+            if ((lane >> 4) > kb)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) b = __builtin_fma(-T[lane * BLD + 16 * kb + j], vz[16 * kb + j], b);
+            wsync();
+        }
+        D1S(5);
+        // L^T y = z by blocks, last first: y_kb = W_kb^T r_kb, then r -= L(kb, :)^T y_kb above
+        for (int kb = 3; kb >= 0; --kb) {
+            const bool in = (lane >> 4) == kb;
+            if (in) vr[lane] = b;
+            wsync();
+            if (in) {
+                double y = 0.0;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) y = __builtin_fma(Wm[kb][m * 16 + (lane & 15)], vr[16 * kb + m], y);
+                b = y;
+                vz[lane] = y;
+            }
+            wsync();
+            if ((lane >> 4) < kb)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) b = __builtin_fma(-T[(16 * kb + j) * BLD + lane], vz[16 * kb + j], b);
+            wsync();
+        }
+        D1S(6);
+        // the step (block_step's arithmetic): y into rhs for the back-substitution, the camera / intrinsics updates
+        // from the prefetched operands, the step scalars reduced over the wave in block_step's order
+        if (lane < n) {
+            rhs[lane] = b;
+            vz[lane] = b;
+        }
+        wsync();
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
+        if (lane < P.nac) cam_step(P, c, cur, radius, cops, lane, vz + 6 * lane, delta, acc);
+        else if (lane == BCR_CAMS) intr_step(P, c, cur, radius, iops, vz + P.kb, delta, acc);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+        if (lane == 0) {
+            part[PART_UPD_SN2 * P.part_stride] = acc[0];
+            part[PART_UPD_MCC * P.part_stride] = acc[1];
+            part[PART_UPD_COST * P.part_stride] = acc[2];
+            part[PART_UPD_XN2 * P.part_stride] = acc[3];
+            if (bad) raise_flag(flag, FLAG_NOT_PD);
+        }
+    }
+    if constexpr (STAMP) {
+        __syncthreads();
+        D1S(7);
+    }
+#undef D1S
+}
+
 static_assert(PANEL_DOUBLES <= BCR_BLOCK_DOUBLES, "published panels fit the block's workspace");
 static_assert(2 * PANEL_DOUBLES <= BB * BB + BB * XW, "two epochs' panels fit the Cf | X slots");
 
@@ -2347,6 +2537,13 @@ hipError_t bcr_set_spin_limit(unsigned limit) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &limit, sizeof(limit));
 }
 
+// One-block windows take k_bcr_dense1 (MIBA_BCR_DENSE1=0, or any MIBA_BCR path override, keeps the split kernel).
+int bcr_dense1_ok(int nblk, int kb) {
+    if (nblk != 1 || kb + 4 > BB || std::getenv("MIBA_BCR")) return 0;
+    const char* e = std::getenv("MIBA_BCR_DENSE1");
+    return (e && e[0] == '0') ? 0 : 1;
+}
+
 int bcr_persist_ok(int nblk) {
     if (bcr_persist_attr() != hipSuccess) return 0;
     int dev = 0, ncu = 0, per_cu = 0, per_cu2 = 0;
@@ -2365,6 +2562,32 @@ int bcr_persist_ok(int nblk) {
 }
 
 hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s, Prof* pf) {
+    if (Bw.dense1) {  // one-block window: the dense single-workgroup solve (bcr_dense1_ok)
+        static unsigned long long* dst = nullptr;
+        static int dmode = -1;
+        if (dmode < 0) {
+            const char* e = getenv("MIBA_BCR_STAMPS");
+            dmode = (e && e[0] == '1') ? 1 : 0;
+            if (dmode) CKB(hipMalloc(&dst, 16 * sizeof(unsigned long long)));
+        }
+        if (dmode) {
+            CKB(hipMemsetAsync(dst, 0, 16 * sizeof(unsigned long long), s));
+            BPL(K_BCR_PERSIST, k_bcr_dense1<true>, dim3(1), dim3(TPB_D1), 0, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
+                W.scale, W.camdata, W.lin, W.delta, W.part, dst);
+            unsigned long long h[16];
+            CKB(hipMemcpyAsync(h, dst, sizeof(h), hipMemcpyDeviceToHost, s));
+            CKB(hipStreamSynchronize(s));
+            if (h[9] && h[7]) {
+                auto us = [&](int k) { return (double)(h[k] - h[9]) * 0.01; };
+                fprintf(stderr, "bcr_dense1 us: loaded %.2f panels %.2f %.2f %.2f %.2f forward %.2f backward %.2f step %.2f\n",
+                        us(0), us(1), us(2), us(3), us(4), us(5), us(6), us(7));
+            }
+            return hipSuccess;
+        }
+        BPL(K_BCR_PERSIST, k_bcr_dense1<false>, dim3(1), dim3(TPB_D1), 0, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
+            W.scale, W.camdata, W.lin, W.delta, W.part, (unsigned long long*)nullptr);
+        return hipSuccess;
+    }
     static bool attr = false;
     static unsigned long long* stamps = nullptr;
     if (!attr) {

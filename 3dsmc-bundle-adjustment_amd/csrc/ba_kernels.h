@@ -137,6 +137,7 @@ struct BcrWork {
     int persist;  // 3 = factor + two helper workgroups per block (k_bcr_split<.., 2>), 2 = factor + one
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level
+    int dense1;   // one-block window solved by k_bcr_dense1 (bcr_dense1_ok)
 };
 // k_bcr_split's flag-free back-substitution hand-off: y rows double-buffered by epoch parity (Y even,
 // Racc odd — Racc belongs to the per-level path only); an empty slot holds this signalling-NaN pattern,
@@ -166,53 +167,97 @@ __device__ __forceinline__ bool skip_step(const LmState* st) { return st->done |
 // Camera / intrinsics step application (k_update_cams, or fused into k_bcr_border): delta = -s*y,
 // Sophus T*exp(delta) into the candidate slot, and the block's terms of the step scalars
 // acc = {|step|^2, model cost change 0.5 (g~ y + D~ y^2), candidate prior cost, |x_cand|^2}.
-__device__ __forceinline__ void update_camera(const DevProblem& P, const BaConsts& c, int cur, double radius,
-                                              const double* __restrict__ scale, const double* __restrict__ camdata,
-                                              int t, const double* yv, double* __restrict__ delta, double acc[4]) {
-    const int cam = P.ac_cam[t];
+// The operands of one camera's step (update_camera; k_bcr_dense1 loads them ahead of its factorization).
+struct CamStepOps {
+    int cam;
+    double x[7], sc[6], ud[6], g[6];  // pose, Jacobi scale, diag of U, gradient g = Jc^T f
+};
+__device__ __forceinline__ void load_cam_step_ops(const DevProblem& P, int cur, const double* __restrict__ scale,
+                                                  const double* __restrict__ camdata, int t, CamStepOps& o) {
+    o.cam = P.ac_cam[t];
     const double* cd = camdata + (size_t)t * CAMDATA;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        o.sc[k] = scale[6 * t + k];
+        o.ud[k] = cd[k * 6 - (k * (k - 1)) / 2];
+        o.g[k] = cd[45 + k];
+    }
+    const double* x = P.cams[cur] + 7 * o.cam;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) o.x[j] = x[j];
+}
+__device__ __forceinline__ void cam_step(const DevProblem& P, const BaConsts& c, int cur, double radius,
+                                         const CamStepOps& o, int t, const double* yv, double* __restrict__ delta,
+                                         double acc[4]) {
     double d[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const double sc = scale[6 * t + k], yk = yv[k];
+        const double sc = o.sc[k], yk = yv[k];
         d[k] = -yk * sc;
         delta[6 * t + k] = d[k];
-        const double u = sc * cd[k * 6 - (k * (k - 1)) / 2] * sc;  // diag of s U s (k_env_assemble)
+        const double u = sc * o.ud[k] * sc;  // diag of s U s (k_env_assemble)
         const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
-        acc[1] += 0.5 * ((sc * cd[45 + k]) * yk + dd * yk * yk);
+        acc[1] += 0.5 * ((sc * o.g[k]) * yk + dd * yk * yk);
     }
-    const double* x = P.cams[cur] + 7 * cam;
-    double* xn = P.cams[cur ^ 1] + 7 * cam;
+    double* xn = P.cams[cur ^ 1] + 7 * o.cam;
     double tp[7];
-    se3_plus(x, d, tp);
+    se3_plus(o.x, d, tp);
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
         xn[j] = tp[j];
-        const double df = x[j] - tp[j];
+        const double df = o.x[j] - tp[j];
         acc[0] += df * df;
         acc[3] += tp[j] * tp[j];
+    }
+}
+__device__ __forceinline__ void update_camera(const DevProblem& P, const BaConsts& c, int cur, double radius,
+                                              const double* __restrict__ scale, const double* __restrict__ camdata,
+                                              int t, const double* yv, double* __restrict__ delta, double acc[4]) {
+    CamStepOps o;
+    load_cam_step_ops(P, cur, scale, camdata, t, o);
+    cam_step(P, c, cur, radius, o, t, yv, delta, acc);
+}
+// The intrinsics' step operands (update_intrinsics) and the step from them.
+struct IntrStepOps {
+    double K[4], sk[4], uk[4], gk[4], prior[4];  // K, Jacobi scale, diag of the prior-augmented Ukk, gk, prior
+};
+__device__ __forceinline__ void load_intr_step_ops(const DevProblem& P, int cur, const double* __restrict__ scale,
+                                                   const double* __restrict__ lin, IntrStepOps& o) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        o.K[m] = P.K[cur][m];
+        o.sk[m] = scale[P.off_k + m];
+        o.uk[m] = lin[2 + 4 * m - (m * (m - 1)) / 2];
+        o.gk[m] = lin[12 + m];
+        o.prior[m] = P.prior[m];
+    }
+}
+__device__ __forceinline__ void intr_step(const DevProblem& P, const BaConsts& c, int cur, double radius,
+                                          const IntrStepOps& o, const double* yk4, double* __restrict__ delta,
+                                          double acc[4]) {
+    double* Kn = P.K[cur ^ 1];
+    for (int m = 0; m < 4; ++m) {
+        const double sk = o.sk[m], ym = yk4[m];
+        const double dk = -ym * sk;
+        delta[P.kb + m] = dk;
+        const double kn = o.K[m] + dk;
+        Kn[m] = kn;
+        const double df = o.K[m] - kn;
+        acc[0] += df * df;
+        const double u = sk * o.uk[m] * sk;  // Ukk incl. the prior block
+        const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
+        acc[1] += 0.5 * ((sk * o.gk[m]) * ym + dd * ym * ym);
+        const double fn = c.sw_k * (o.prior[m] - kn);
+        acc[2] += 0.5 * fn * fn;
+        acc[3] += kn * kn;
     }
 }
 __device__ __forceinline__ void update_intrinsics(const DevProblem& P, const BaConsts& c, int cur, double radius,
                                                   const double* __restrict__ scale, const double* __restrict__ lin,
                                                   const double* yk4, double* __restrict__ delta, double acc[4]) {
-    const double* K = P.K[cur];
-    double* Kn = P.K[cur ^ 1];
-    for (int m = 0; m < 4; ++m) {
-        const double sk = scale[P.off_k + m], ym = yk4[m];
-        const double dk = -ym * sk;
-        delta[P.kb + m] = dk;
-        const double kn = K[m] + dk;
-        Kn[m] = kn;
-        const double df = K[m] - kn;
-        acc[0] += df * df;
-        const double u = sk * lin[2 + 4 * m - (m * (m - 1)) / 2] * sk;  // Ukk incl. the prior block
-        const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
-        acc[1] += 0.5 * ((sk * lin[12 + m]) * ym + dd * ym * ym);
-        const double fn = c.sw_k * (P.prior[m] - kn);
-        acc[2] += 0.5 * fn * fn;
-        acc[3] += kn * kn;
-    }
+    IntrStepOps o;
+    load_intr_step_ops(P, cur, scale, lin, o);
+    intr_step(P, c, cur, radius, o, yk4, delta, acc);
 }
 
 struct LmParams {
@@ -344,6 +389,7 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
 // 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);
+int bcr_dense1_ok(int nblk, int kb);
 // k_bcr_split's pull slots: empty (split = true, Bw.persist >= 2) or zero (the per-level / persistent paths)
 hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s);
 // spin bound of the resident BCR kernels' inter-workgroup waits (default 1 << 22 polls; tests force a

@@ -224,6 +224,42 @@ def test_bcr_persistent_matches_level_launches(n_cams, monkeypatch):
         assert abs(sb["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], mode
 
 
+@pytest.mark.parametrize("n_cams,fixed", [(10, 0), (11, 0), (7, 3), (2, 0)])
+def test_bcr_dense1_one_block_windows(n_cams, fixed, monkeypatch):
+    """One-block windows (<= 10 active cameras; 11 cameras with the gauge camera fixed is the full 64-dof block)
+    take the dense single-workgroup solve (bcr_path 4): against the split kernel and the oracle, tolerances off,
+    6 iterations; a deterministic repeat is bitwise identical."""
+    from miba.solver import Solver
+    p = synthetic.make_problem(n_cams, 90 * n_cams, obs_per_point=(2, min(n_cams, 6)), seed=100 + n_cams,
+                               fixed_cam=fixed, sensor_f32=True)
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
+    res = {}
+    for mode, path in (("dense1", 4), ("split", 3)):
+        monkeypatch.setenv("MIBA_BCR_DENSE1", "1" if mode == "dense1" else "0")
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
+            res[mode] = (s.solve(q), q)
+            assert s.last_prepare()["bcr_path"] == path, mode
+    (sa, qa), (sb, qb) = res["dense1"], res["split"]
+    assert sa["linear_solver"] == sb["linear_solver"] == LS["bcr"]
+    assert sa["num_iterations"] == sb["num_iterations"] == 6
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sb["final_cost"]
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(qa.intr, qb.intr, rtol=1e-9)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
+    monkeypatch.setenv("MIBA_BCR_DENSE1", "1")
+    outs = []
+    for _ in range(2):
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, deterministic=1, **no_tol) as s:
+            outs.append((s.solve(q)["final_cost"], q))
+    assert outs[0][0] == outs[1][0]
+    np.testing.assert_array_equal(outs[0][1].cams, outs[1][1].cams)
+
+
 @pytest.mark.parametrize("config,iters", [("C4", 3), ("C5", 2)])
 def test_large_configs_match_oracle(config, iters):
     """BASELINE.json's largest single-window configurations (C4: 200 cams / 100k points / 1M obs,
