@@ -2208,7 +2208,14 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
 // L^T y = z on wave 0 (lane = row, v_readlane broadcasts, the next column prefetched) and applies the camera /
 // intrinsics step (block_step with y in the u column): no border system, no cross-workgroup hand-off — the split
 // kernel's factor / helper pair spends ~5 us of a ~21 us one-block launch on those (C1 stamps).
-static constexpr int TPB_D1 = 256;
+static constexpr int TPB_D1 = 512;
+// Wave roles after the load (k_bcr_split's factor workgroup, plus the solve):
+//   wave 0     the pivot chain of column block kb once its critical update is in (LDS flags, no barriers)
+//   waves 1-3  the critical update of column block kb + 1 by panel kb (one tile each)
+//   waves 6-7  the other trailing tiles (panel 0 on column blocks 2, 3; panel 1 on 3)
+//   wave 5     W_kb = L_kk^-1 and the forward substitution's block kb as each panel lands (lane = row), then the
+//              backward substitution by blocks and the camera / intrinsics step from its prefetched operands
+//   wave 4     idle (it shares wave 0's SIMD)
 // STAMP: s_memrealtime after each phase into tl[0..8] (loaded, 4 panels, forward, backward, step)
 template <bool STAMP>
 __global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict__ st, DevProblem P,
@@ -2220,13 +2227,14 @@ __global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict
                                                       double* __restrict__ part, unsigned long long* __restrict__ tl) {
 #define D1S(k)                                                                      \
     do {                                                                            \
-        if constexpr (STAMP) if (threadIdx.x == 0) tl[(k)] = realtime_now();        \
+        if constexpr (STAMP) if ((threadIdx.x & 63) == 0) tl[(k)] = realtime_now(); \
     } while (0)
-    D1S(9);
+    if constexpr (STAMP) if (threadIdx.x == 0) tl[9] = realtime_now();
     __shared__ __attribute__((aligned(16))) double T[BB * BLD];
     __shared__ double rdg[BB];
     __shared__ double Wm[4][256];          // W_kb = L_kk^-1, row-major
-    __shared__ double vr[BB], vz[BB];      // wave 0's broadcast rows of the blocked triangular solves
+    __shared__ double vr[BB], vz[BB];      // wave 5's broadcast rows of the blocked triangular solves
+    __shared__ int sync[12];               // [0] panels factored, [1..3] critical updates, [5..8] trailing per column
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane & 15, kk = lane >> 4;
     const int n = P.kb + 4;  // camera dofs, then the intrinsics rows (P.kb = 6 nac)
     const size_t ld = P.npad;
@@ -2247,20 +2255,44 @@ __global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict
             T[r * BLD + cc] = (cc <= r && r < n) ? v[q] : (r == cc ? 1.0 : 0.0);
         }
     }
-    // the step's operands (cameras on wave 0's lanes < nac, the intrinsics on lane BCR_CAMS), in flight through
-    // the factorization
+    if (tid < 12) sync[tid] = 0;
+    // wave 5: rhs and the step's operands (cameras on lanes < nac, the intrinsics on lane BCR_CAMS), in flight
+    // through the factorization
     const int cur = st->cur;
     const double radius = st->radius;
     CamStepOps cops;
     IntrStepOps iops;
-    if (wave == 0 && lane < P.nac) load_cam_step_ops(P, cur, scale, camdata, lane, cops);
-    if (wave == 0 && lane == BCR_CAMS) load_intr_step_ops(P, cur, scale, lin, iops);
-    double b = (wave == 0 && lane < n) ? rhs[lane] : 0.0;
+    double b = 0.0;
+    if (wave == 5) {
+        if (lane < P.nac) load_cam_step_ops(P, cur, scale, camdata, lane, cops);
+        if (lane == BCR_CAMS) load_intr_step_ops(P, cur, scale, lin, iops);
+        b = lane < n ? rhs[lane] : 0.0;
+    }
     __syncthreads();
     D1S(0);
-    bool bad = false;
-    for (int kb = 0; kb < 4; ++kb) {
-        if (wave == 0) {  // the pivot chain of the tall column block kb (k_bcr_split's wave 0)
+    const unsigned spin_lim = g_spin_limit;
+    auto lds_ld = [&](int k) { return __hip_atomic_load(sync + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto spin_ge = [&](int k, int v) {
+        unsigned cnt = 0;
+        while (lds_ld(k) < v) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++cnt > spin_lim) return false;
+        }
+        return true;
+    };
+    auto tile_sub = [&](int ii, int jj, int pn) {  // T(ii,jj) -= L(ii,pn) L(jj,pn)^T
+        const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * pn, BLD, T + (16 * jj) * BLD + 16 * pn, BLD, rr, kk);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
+    };
+    auto signal = [&](int k) {
+        if (lane == 0) __hip_atomic_fetch_add(sync + k, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    bool ok = true;
+    if (wave == 0) {
+        bool bad = false;
+        for (int kb = 0; kb < 4; ++kb) {
+            if (kb > 0 && !spin_ge(1 + kb - 1, 4 - kb)) { ok = false; break; }  // column block kb updated
             const int r = lane, row = 16 * kb + r;
             const bool live = row < BB;
             double a[16];
@@ -2287,44 +2319,53 @@ __global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict
 #pragma unroll
                 for (int cc = 0; cc < 16; ++cc) T[row * BLD + 16 * kb + cc] = (r >= 16 || cc <= r) ? a[cc] : 0.0;
             if (r < 16) rdg[16 * kb + r] = my_inv;
+            if (lane == 0) __hip_atomic_store(sync, kb + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            D1S(1 + kb);
         }
-        __syncthreads();
-        // trailing tiles (ii, jj), kb < jj <= ii < 4: T(ii,jj) -= L(ii,kb) L(jj,kb)^T, round-robin over the waves
-        const int m = 3 - kb, ntl = m * (m + 1) / 2;
-        for (int t = wave; t < ntl; t += TPB_D1 / 64) {
-            int q = t, ib = 0;
-            while (q > ib) { q -= ib + 1; ++ib; }
-            const int ii = kb + 1 + ib, jj = kb + 1 + q;
-            const d4b acc = mfma16_abt(T + (16 * ii) * BLD + 16 * kb, BLD, T + (16 * jj) * BLD + 16 * kb, BLD, rr, kk);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) T[(16 * ii + kk + 4 * g) * BLD + 16 * jj + rr] -= acc[g];
+        if (bad && lane == 0) raise_flag(flag, FLAG_NOT_PD);
+    } else if (wave <= 3) {
+        for (int kb = 0; kb + wave <= 3 && kb < 3; ++kb) {
+            if (!spin_ge(0, kb + 1)) { ok = false; break; }
+            if (kb + 1 >= 2 && !spin_ge(5 + kb + 1, 2)) { ok = false; break; }  // earlier panels' trailing updates
+            tile_sub(kb + wave, kb + 1, kb);
+            signal(1 + kb);
         }
-        __syncthreads();
-        D1S(1 + kb);
-    }
-    // W_kb = L_kk^-1 on wave kb (lanes 0-15, column `lane` by forward substitution; k_bcr_split's wave-5 form)
-    if (lane < 16) {
-        const int kb = wave;
-        double w[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) w[m] = (m == lane) ? 1.0 : 0.0;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            w[m] *= rdg[16 * kb + m];
-#pragma unroll
-            for (int j = m + 1; j < 16; ++j) w[j] = __builtin_fma(-T[(16 * kb + j) * BLD + 16 * kb + m], w[m], w[j]);
+    } else if (wave == 6) {  // tile (3,3): panel 0, then panel 1
+        for (int pn = 0; pn < 2 && ok; ++pn) {
+            if (!spin_ge(0, pn + 1)) { ok = false; break; }
+            tile_sub(3, 3, pn);
+            signal(5 + 3);
         }
-#pragma unroll
-        for (int m = 0; m < 16; ++m) Wm[kb][m * 16 + lane] = w[m];
-    }
-    __syncthreads();
-    if (wave == 0) {
+    } else if (wave == 7) {  // tiles (2,2), (3,2): panel 0
+        if (!spin_ge(0, 1)) ok = false;
+        else {
+            tile_sub(2, 2, 0);
+            tile_sub(3, 2, 0);
+            __hip_atomic_fetch_add(sync + 5 + 2, lane == 0 ? 2 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else if (wave == 5) {
         auto wsync = [] {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
-        // L z = b by 16-row blocks: z_kb = W_kb r_kb, then r -= L(:, kb) z_kb below (lane = row)
+        // panel by panel: W_kb (lanes 0-15, column `lane` by forward substitution), then L z = b's block kb:
+        // z_kb = W_kb r_kb, r -= L(:, kb) z_kb below (lane = row)
         for (int kb = 0; kb < 4; ++kb) {
+            if (!spin_ge(0, kb + 1)) { ok = false; break; }
+            if (lane < 16) {
+                double w[16];
+#pragma unroll
+                for (int m = 0; m < 16; ++m) w[m] = (m == lane) ? 1.0 : 0.0;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    w[m] *= rdg[16 * kb + m];
+#pragma unroll
+                    for (int j = m + 1; j < 16; ++j)
+                        w[j] = __builtin_fma(-T[(16 * kb + j) * BLD + 16 * kb + m], w[m], w[j]);
+                }
+#pragma unroll
+                for (int m = 0; m < 16; ++m) Wm[kb][m * 16 + lane] = w[m];
+            }
             const bool in = (lane >> 4) == kb;
             if (in) vr[lane] = b;
             wsync();
@@ -2341,52 +2382,51 @@ __global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict
                 for (int j = 0; j < 16; ++j) b = __builtin_fma(-T[lane * BLD + 16 * kb + j], vz[16 * kb + j], b);
             wsync();
         }
-        D1S(5);
-        // L^T y = z by blocks, last first: y_kb = W_kb^T r_kb, then r -= L(kb, :)^T y_kb above
-        for (int kb = 3; kb >= 0; --kb) {
-            const bool in = (lane >> 4) == kb;
-            if (in) vr[lane] = b;
-            wsync();
-            if (in) {
-                double y = 0.0;
+        if (ok) {
+            D1S(5);
+            // L^T y = z by blocks, last first: y_kb = W_kb^T r_kb, then r -= L(kb, :)^T y_kb above
+            for (int kb = 3; kb >= 0; --kb) {
+                const bool in = (lane >> 4) == kb;
+                if (in) vr[lane] = b;
+                wsync();
+                if (in) {
+                    double y = 0.0;
 #pragma unroll
-                for (int m = 0; m < 16; ++m) y = __builtin_fma(Wm[kb][m * 16 + (lane & 15)], vr[16 * kb + m], y);
-                b = y;
-                vz[lane] = y;
+                    for (int m = 0; m < 16; ++m) y = __builtin_fma(Wm[kb][m * 16 + (lane & 15)], vr[16 * kb + m], y);
+                    b = y;
+                    vz[lane] = y;
+                }
+                wsync();
+                if ((lane >> 4) < kb)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) b = __builtin_fma(-T[(16 * kb + j) * BLD + lane], vz[16 * kb + j], b);
+                wsync();
+            }
+            D1S(6);
+            // the step (block_step's arithmetic): y into rhs for the back-substitution, the camera / intrinsics
+            // updates from the prefetched operands, the step scalars reduced over the wave in block_step's order
+            if (lane < n) {
+                rhs[lane] = b;
+                vz[lane] = b;
             }
             wsync();
-            if ((lane >> 4) < kb)
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
+            if (lane < P.nac) cam_step(P, c, cur, radius, cops, lane, vz + 6 * lane, delta, acc);
+            else if (lane == BCR_CAMS) intr_step(P, c, cur, radius, iops, vz + P.kb, delta, acc);
 #pragma unroll
-                for (int j = 0; j < 16; ++j) b = __builtin_fma(-T[(16 * kb + j) * BLD + lane], vz[16 * kb + j], b);
-            wsync();
-        }
-        D1S(6);
-        // the step (block_step's arithmetic): y into rhs for the back-substitution, the camera / intrinsics updates
-        // from the prefetched operands, the step scalars reduced over the wave in block_step's order
-        if (lane < n) {
-            rhs[lane] = b;
-            vz[lane] = b;
-        }
-        wsync();
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
-        if (lane < P.nac) cam_step(P, c, cur, radius, cops, lane, vz + 6 * lane, delta, acc);
-        else if (lane == BCR_CAMS) intr_step(P, c, cur, radius, iops, vz + P.kb, delta, acc);
+            for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
-        if (lane == 0) {
-            part[PART_UPD_SN2 * P.part_stride] = acc[0];
-            part[PART_UPD_MCC * P.part_stride] = acc[1];
-            part[PART_UPD_COST * P.part_stride] = acc[2];
-            part[PART_UPD_XN2 * P.part_stride] = acc[3];
-            if (bad) raise_flag(flag, FLAG_NOT_PD);
+                for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+            if (lane == 0) {
+                part[PART_UPD_SN2 * P.part_stride] = acc[0];
+                part[PART_UPD_MCC * P.part_stride] = acc[1];
+                part[PART_UPD_COST * P.part_stride] = acc[2];
+                part[PART_UPD_XN2 * P.part_stride] = acc[3];
+            }
+            D1S(7);
         }
     }
-    if constexpr (STAMP) {
-        __syncthreads();
-        D1S(7);
-    }
+    if (!ok && lane == 0) raise_flag(flag, FLAG_TIMEOUT);
 #undef D1S
 }
 

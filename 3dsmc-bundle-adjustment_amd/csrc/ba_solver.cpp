@@ -1201,6 +1201,7 @@ static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     HIPCHECK(ctx, hipStreamSynchronize(s));
     BcrWork& Bw = ctx->W.bcr;
     Bw.persist = 0;
+    Bw.dense1 = 0;  // (k_bcr_dense1 waits only inside its workgroup: a forced spin bound can still time it out)
     ctx->bcr_fallback = true;
     if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
     HIPCHECK(ctx, bcr_reset_pull_slots(Bw, false, s));
