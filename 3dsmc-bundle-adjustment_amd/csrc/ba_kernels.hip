@@ -850,7 +850,10 @@ struct EnvArgs {
     int fin;  // 1: unsharded (finish the camera sums, lin); 2: landmark shard (local terms for the exchange)
 };
 
-template <bool STAMP, bool O32>
+// PF (small grids, where occupancy does not bound the launch): each chunk's point records (G, e~, K~) are loaded
+// with the chunk's observation records — in the prologue, then a chunk ahead under the MFMAs — instead of at the
+// start of phase A.
+template <bool STAMP, bool O32, bool PF = false>
 __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
@@ -970,7 +973,15 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 #pragma unroll
         for (int k = 0; k < 6; ++k) o_G[k] = pdata[(size_t)ap * PDATA + k];
     };
+    double q_pd[PF ? 21 : 1];
+    auto load_pq = [&](int a0, int a1) {
+        if constexpr (PF)
+            if (tid < a1 - a0)
+#pragma unroll
+                for (int i = 0; i < 21; ++i) q_pd[i] = pdata[(size_t)(a0 + tid) * PDATA + i];
+    };
     load_rec(ob + tid);
+    load_pq(apb, ape);
     load_ops(ob + tid < oe && r_ac >= 0);
     for (;;) {
         const int npts = ape - apb;
@@ -987,7 +998,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         SCH_STAMP(0);
         // ---- phase A
         if (tid < npts) {
-            const double* pd = pdata + (size_t)(apb + tid) * PDATA;
+            const double* pd = PF ? q_pd : pdata + (size_t)(apb + tid) * PDATA;
             double G[6], Ks[12], es[3], zk[12], z3[3];
 #pragma unroll
             for (int i = 0; i < 6; ++i) G[i] = pd[i];
@@ -1028,6 +1039,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         if (more) {
             ape_n = P.chunk_ap[ch + 2];
             load_rec(oe + tid);
+            load_pq(ape, ape_n);
         }
         // ---- rhs row aside: rhs_acc(r) += sum_k M'[r][k] ze[k] (wave 3, lane = camera row r): four
         // interleaved partial chains (k mod 4; f64 FMA dependent latency is 32 cycles), summed in a fixed order
@@ -2598,6 +2610,10 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             fprintf(stderr, "  median tile %d: %.0f cycles span %d chunks %d points %d\n", t50, tot[P.n_tiles / 2].first,
                     tspan[t50], tch[t50 + 1] - tch[t50], cap[tch[t50 + 1]] - cap[tch[t50]]);
         } else {
+            if (n_sch <= 256)  // one round of resident workgroups whatever the register count
+                OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true>), (k_schur_tile<false, false, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
+                    W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf, E);
+            else
             OPL(K_SCHUR_TILE, (k_schur_tile<false, true>), (k_schur_tile<false, false>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
                W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf, E);
         }
