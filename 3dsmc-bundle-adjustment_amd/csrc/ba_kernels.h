@@ -370,8 +370,9 @@ struct PrepRaw {
     const double2* uv;    // [n_obs]
     const double* depth;  // [n_obs]
     const int* cam_ac;    // [n_cams] camera -> active index or -1
-    const int* po_orig;   // [n_adm] point-major slot -> observation
-    const int* co_orig;   // [n_adm] camera-major slot -> observation
+    const int* po_dest;   // [n_obs] observation -> point-major slot (-1: not admissible)
+    const int* co_dest;   // [n_obs] observation -> camera-major slot (-1: not admissible)
+    int n_obs;
 };
 // fills P.po_* (and po_ap / po_pt from pt_ptr / pt_idx) and P.co_* from R
 hipError_t launch_prep_gather(const DevProblem& P, const PrepRaw& R, hipStream_t s);

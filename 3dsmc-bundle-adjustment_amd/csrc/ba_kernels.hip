@@ -2465,43 +2465,40 @@ __global__ __launch_bounds__(TPB) void k_reset(DevProblem P, LmState st0, LmStat
 }
 
 // ba_prepare: the observation layout the window uses, from the raw window (uploaded as the caller passed it) and
-// the host plan's orderings (ba_plan.cpp) — workgroups [0, nbq): point-major slot q (obs po_orig[q]); [nbq, nbq +
-// nbc): camera-major slot q (obs co_orig[q]); the rest: one active point per thread, its slots' point indices.
+// the host plan's slots (ba_plan.cpp). Workgroups [0, nbo): one observation per thread in the caller's order, read
+// once (coalesced) and scattered to its point-major and camera-major slots; the rest: one active point per thread,
+// its slots' point indices. A gather by slot instead (round 3) read the raw arrays in a permuted order, every 4-16 B
+// read pulling a whole line: 349 MB per launch at C4 for ~110 MB of data. The scatter's writes land in runs (each
+// camera's slots and each point's slots are in the caller's index order), and consecutive workgroups of the range
+// run on one XCD (dispatch is round-robin over the 8 XCDs), so a run's lines fill in one L2 before they are written.
 // O32: the 16-byte records only (every observation kernel of an obs32 window reads those); else the f64 arrays.
 template <bool O32>
-__global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, int nbq, int nbc) {
+__global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, int nbo) {
     const int b = blockIdx.x, tid = threadIdx.x;
-    if (b < nbq) {
-        const int q = b * TPB + tid;
-        if (q >= P.n_adm) return;
-        const int k = R.po_orig[q];
-        const int cam = R.cam[k];
+    if (b < nbo) {
+        const int per = nbo >> 3, rem = nbo & 7, x = b & 7;
+        const int lb = x * per + (x < rem ? x : rem) + (b >> 3);  // XCD x runs blocks [x per + min(x, rem), ...)
+        const int k = lb * TPB + tid;
+        if (k >= R.n_obs) return;
+        const int pq = R.po_dest[k], cq = R.co_dest[k];
+        if (pq < 0) return;  // not admissible (cq < 0 too)
+        const int cam = R.cam[k], pt = R.pt[k];
         const double2 uv = R.uv[k];
         const double dep = R.depth[k];
-        const_cast<int*>(P.po_ac)[q] = R.cam_ac[cam];
+        const_cast<int*>(P.po_ac)[pq] = R.cam_ac[cam];
         if constexpr (O32) {  // exact: the host checked that every admissible value is an f32
-            const_cast<float4*>(P.po_rec)[q] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(cam)};
+            const_cast<float4*>(P.po_rec)[pq] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(cam)};
+            const_cast<float4*>(P.co_rec)[cq] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(pt)};
         } else {
-            const_cast<int*>(P.po_cam)[q] = cam;
-            const_cast<double2*>(P.po_uv)[q] = uv;
-            const_cast<double*>(P.po_depth)[q] = dep;
-        }
-    } else if (b < nbq + nbc) {
-        const int q = (b - nbq) * TPB + tid;
-        if (q >= P.n_adm) return;
-        const int k = R.co_orig[q];
-        const int pt = R.pt[k];
-        const double2 uv = R.uv[k];
-        const double dep = R.depth[k];
-        if constexpr (O32) {
-            const_cast<float4*>(P.co_rec)[q] = float4{(float)uv.x, (float)uv.y, (float)dep, __int_as_float(pt)};
-        } else {
-            const_cast<int*>(P.co_pt)[q] = pt;
-            const_cast<double2*>(P.co_uv)[q] = uv;
-            const_cast<double*>(P.co_depth)[q] = dep;
+            const_cast<int*>(P.po_cam)[pq] = cam;
+            const_cast<double2*>(P.po_uv)[pq] = uv;
+            const_cast<double*>(P.po_depth)[pq] = dep;
+            const_cast<int*>(P.co_pt)[cq] = pt;
+            const_cast<double2*>(P.co_uv)[cq] = uv;
+            const_cast<double*>(P.co_depth)[cq] = dep;
         }
     } else {
-        const int a = (b - nbq - nbc) * TPB + tid;
+        const int a = (b - nbo) * TPB + tid;
         if (a >= P.n_ap) return;
         const int pi = P.pt_idx[a];
         for (int q = P.pt_ptr[a]; q < P.pt_ptr[a + 1]; ++q) {
@@ -2512,10 +2509,10 @@ __global__ __launch_bounds__(TPB) void k_prep_gather(DevProblem P, PrepRaw R, in
 }
 
 hipError_t launch_prep_gather(const DevProblem& P, const PrepRaw& R, hipStream_t s) {
-    const int nbq = nblocks(P.n_adm, TPB), nba = nblocks(P.n_ap, TPB);
-    if (nbq + nbq + nba > 0) {
-        if (P.obs32) hipLaunchKernelGGL(k_prep_gather<true>, dim3(2 * nbq + nba), dim3(TPB), 0, s, P, R, nbq, nbq);
-        else hipLaunchKernelGGL(k_prep_gather<false>, dim3(2 * nbq + nba), dim3(TPB), 0, s, P, R, nbq, nbq);
+    const int nbo = nblocks(R.n_obs, TPB), nba = nblocks(P.n_ap, TPB);
+    if (nbo + nba > 0) {
+        if (P.obs32) hipLaunchKernelGGL(k_prep_gather<true>, dim3(nbo + nba), dim3(TPB), 0, s, P, R, nbo);
+        else hipLaunchKernelGGL(k_prep_gather<false>, dim3(nbo + nba), dim3(TPB), 0, s, P, R, nbo);
     }
     return hipGetLastError();
 }

@@ -307,13 +307,17 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
     pl.pt_ptr.assign(n_ap + 1, 0);
     for (int a = 0; a < n_ap; ++a) pl.pt_ptr[a + 1] = pl.pt_ptr[a] + pl.pt_cnt[pl.pt_idx[a]];
     pl.po_orig.resize(n_adm);
+    pl.po_dest.resize(no);  // admissible entries here, the others (-1) in the camera-major pass below
     {
         const int T = n_tasks(n_ap, 8192);
         const Split sp{n_ap, T};
         host_parallel(T, [&](int t) {
             for (long long a = sp.lo(t); a < sp.lo(t + 1); ++a) {
                 const int i = pl.pt_idx[a];
-                std::copy(plist.begin() + pptr[i], plist.begin() + pptr[i + 1], pl.po_orig.begin() + pl.pt_ptr[a]);
+                for (int j = pptr[i], q = pl.pt_ptr[a]; j < pptr[i + 1]; ++j, ++q) {
+                    pl.po_orig[q] = plist[j];
+                    pl.po_dest[plist[j]] = q;
+                }
             }
         });
     }
@@ -333,6 +337,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
     std::vector<int> cstart(nc + 1, 0);
     for (int i = 0; i < nc; ++i) cstart[i + 1] = cstart[i] + pl.cam_cnt[i];
     pl.co_orig.resize(n_adm);
+    pl.co_dest.resize(no);
     {
         const int T = n_tasks(no, 65536);
         const Split sp{no, T};
@@ -353,7 +358,14 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
         host_parallel(T, [&](int t) {
             std::vector<int>& c = off[t];
             for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k)
-                if (pl.adm[k]) pl.co_orig[c[in.obs_cam[k]]++] = (int)k;
+                if (pl.adm[k]) {
+                    const int q = c[in.obs_cam[k]]++;
+                    pl.co_orig[q] = (int)k;
+                    pl.co_dest[k] = q;
+                } else {
+                    pl.co_dest[k] = -1;
+                    pl.po_dest[k] = -1;
+                }
         });
     }
     // sub-segments of <= subseg observations (one workgroup each), equal-sized within a camera; ac_seg[ac] = the

@@ -61,6 +61,7 @@ struct Plan {
     std::vector<int> ovf_obs;        // point-major obs of overflow points on an active camera
     std::vector<int> bs_chunk;       // back-substitution chunk boundaries (active points)
     std::vector<int> co_orig;        // camera-major admissible obs -> original index (per camera in index order)
+    std::vector<int> po_dest, co_dest;  // [no] original index -> point-major / camera-major slot (-1: not admissible)
     std::vector<int> seg_ptr, seg_cam, seg_ac;  // camera sub-segments
     std::vector<int> ac_seg;         // [2 * nac]: sub-segment range of each active camera
     std::vector<int> fc;             // first co-visible active camera of each active camera (this shard)

@@ -807,7 +807,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         // ---- uploads: the plan's index arrays in one staged DMA (each array 256-byte aligned in B_PLAN)
         struct Part { const int* src; size_t n; size_t off; };
         std::vector<Part> parts = {
-            {pl.po_orig.data(), (size_t)n_adm, 0}, {pl.co_orig.data(), (size_t)n_adm, 0}, {pl.cam_ac.data(), (size_t)nc, 0},
+            {pl.po_dest.data(), (size_t)no, 0}, {pl.co_dest.data(), (size_t)no, 0}, {pl.cam_ac.data(), (size_t)nc, 0},
             {pl.pt_ptr.data(), (size_t)n_ap + 1, 0}, {pl.pt_idx.data(), (size_t)n_ap, 0},
             {pl.seg_ptr.data(), pl.seg_ptr.size(), 0}, {pl.seg_cam.data(), pl.seg_cam.size(), 0},
             {pl.seg_ac.data(), pl.seg_ac.size(), 0}, {pl.ac_seg.data(), pl.ac_seg.size(), 0},
@@ -817,7 +817,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             {pl.bs_chunk.data(), pl.bs_chunk.size(), 0}, {pl.ovf_obs.data(), pl.ovf_obs.size(), 0},
             {pl.rptr.data(), (size_t)nb + 1, 0}, {pl.rows.data(), pl.rows.size(), 0},
             {pl.env_tile.data(), pl.env_tile.size(), 0}, {trange.data(), trange.size(), 0}};
-        enum { PO_ORIG, CO_ORIG, CAM_AC, PT_PTR, PT_IDX, SEG_PTR, SEG_CAM, SEG_AC, AC_SEG, AC_CAM, FCOL, TILE_CHUNK,
+        enum { PO_DEST, CO_DEST, CAM_AC, PT_PTR, PT_IDX, SEG_PTR, SEG_CAM, SEG_AC, AC_SEG, AC_CAM, FCOL, TILE_CHUNK,
                TILE_BASE, TILE_SPAN, CHUNK_AP, BS_CHUNK, OVF_OBS, RPTR, ROWS, ENV_TILE, TRANGE };
         size_t plan_ints = 0;
         for (Part& q : parts) {
@@ -931,8 +931,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             R.uv = ctx->buf[B_RAW_UV].as<double2>();
             R.depth = ctx->buf[B_RAW_DEP].as<double>();
             R.cam_ac = dptr(CAM_AC);
-            R.po_orig = dptr(PO_ORIG);
-            R.co_orig = dptr(CO_ORIG);
+            R.po_dest = dptr(PO_DEST);
+            R.co_dest = dptr(CO_DEST);
+            R.n_obs = no;
             ctx->raw = R;
             HIPCHECK(ctx, launch_prep_gather(P, R, s));
         }

@@ -125,6 +125,14 @@ static void run(const char* label, const Window& w, int subseg, int tile_slots) 
     emit("co_orig", pl.co_orig); emit("seg_ptr", pl.seg_ptr); emit("seg_cam", pl.seg_cam);
     emit("seg_ac", pl.seg_ac); emit("ac_seg", pl.ac_seg); emit("fc", pl.fc); emit("fcol", pl.fcol);
     emit("rptr", pl.rptr); emit("rows", pl.rows); emit("env_tile", pl.env_tile);
+    emit("po_dest", pl.po_dest); emit("co_dest", pl.co_dest);
+    // the device scatter's slots (k_prep_gather): each admissible observation's slot in both orders, -1 otherwise
+    bool inv = (int)pl.po_dest.size() == in.no && (int)pl.co_dest.size() == in.no;
+    for (int q = 0; inv && q < pl.n_adm; ++q)
+        inv = pl.po_dest[pl.po_orig[q]] == q && pl.co_dest[pl.co_orig[q]] == q;
+    for (int k = 0; inv && k < in.no; ++k)
+        inv = pl.adm[k] ? (pl.po_dest[k] >= 0 && pl.co_dest[k] >= 0) : (pl.po_dest[k] == -1 && pl.co_dest[k] == -1);
+    std::printf("  dest_inverse=%d\n", (int)inv);
 }
 
 int main(int argc, char** argv) {

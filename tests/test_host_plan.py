@@ -35,6 +35,9 @@ def _run(exe, threads, *args, env=None, timeout=600):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = r.stdout.splitlines()
     assert lines[0] == f"host_threads={threads}" and lines[-1] == "plan_main: ok"
+    # every window's scatter slots (po_dest / co_dest) invert its point- and camera-major orders
+    assert all(l.strip() == "dest_inverse=1" for l in lines if "dest_inverse" in l)
+    assert any("dest_inverse" in l for l in lines)
     return lines[1:], r.stderr
 
 
