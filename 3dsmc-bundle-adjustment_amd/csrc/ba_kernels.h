@@ -96,6 +96,7 @@ struct DevProblem {
     int n_bs_chunks;
     const int* ovf_obs;  // point-major obs of overflow points (active camera only)
     int n_tiles, n_ovf_obs;
+    int n_tiled_pts;  // active points [0, n_tiled_pts) belong to Schur tiles
     int n_seg, n_ap, n_adm, nac;
     int n;     // reduced system size 6*nac + 4
     int npad;  // n rounded up to 16
@@ -324,6 +325,13 @@ struct DevWork {
     // launch), the envelope tiles as atomic adds inside k_schur_tile onto an S / rhs zeroed by the previous
     // iteration's k_backsub_chunk / k_final
     int fused = 0;
+    // small windows (one resident round of the Schur launch, unsharded, default mode): the point side in the Schur
+    // tiles themselves and the camera side + non-tiled points as extra workgroups of that launch, so the LM loop
+    // has no k_lin_point (k_schur_tile<..., FP>). sw_cnt: camera-side workgroups finished (monotonic within a
+    // solve; reset by launch_reset), sw_seq: Schur launches of this solve (host side)
+    int sw = 0;
+    unsigned* sw_cnt = nullptr;
+    unsigned sw_seq = 0;
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)

@@ -527,7 +527,9 @@ __global__ __launch_bounds__(TPB) void k_env_assemble(DevProblem P, BaConsts c, 
 template <int PP_LANES, bool O32>
 __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                                  int mode, const double* __restrict__ scale, double* __restrict__ cnp,
-                                                 double* __restrict__ pdata, double* __restrict__ part, const int b);
+                                                 double* __restrict__ pdata, double* __restrict__ part, const int b,
+                                                 const int ap0 = 0, const int pb = -1, double* kkS = nullptr,
+                                                 double* kkR = nullptr);
 // Workgroups >= nb_pp assemble the envelope tiles of S (env_tile; independent of the point records),
 // so the assembly needs no launch of its own.
 template <int PP_LANES, bool O32>
@@ -549,19 +551,81 @@ __global__ __launch_bounds__(PP_TPB) void k_point_prep(DevProblem P, BaConsts c,
     }
     point_prep_block<PP_LANES, O32>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
 }
-// Point-side body of k_point_prep for point workgroup b (see k_point_prep).
+// One observation's point-side sums: acc = V packed (6) | e (3) | Kt (12)
+__device__ __forceinline__ void point_accum(double* acc, const double* jp, const double* jk, const ObsEval& ev) {
+    acc[0] += jp[0] * jp[0] + jp[3] * jp[3] + jp[6] * jp[6];
+    acc[1] += jp[0] * jp[1] + jp[3] * jp[4] + jp[6] * jp[7];
+    acc[2] += jp[0] * jp[2] + jp[3] * jp[5] + jp[6] * jp[8];
+    acc[3] += jp[1] * jp[1] + jp[4] * jp[4] + jp[7] * jp[7];
+    acc[4] += jp[1] * jp[2] + jp[4] * jp[5] + jp[7] * jp[8];
+    acc[5] += jp[2] * jp[2] + jp[5] * jp[5] + jp[8] * jp[8];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[6 + i] += jp[i] * ev.f[0] + jp[3 + i] * ev.f[1] + jp[6 + i] * ev.f[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // Kt = Jk^T Jp: jk row 0 is [k0, 0, su, 0], row 1 [0, k1, 0, su]
+        acc[9 + 0 * 3 + i] += jk[0] * jp[i];
+        acc[9 + 1 * 3 + i] += jk[5] * jp[3 + i];
+        acc[9 + 2 * 3 + i] += jk[2] * jp[i];
+        acc[9 + 3 * 3 + i] += jk[7] * jp[3 + i];
+    }
+}
+// The point side of one active point on one thread (point_prep_block with one lane per point, the same sums in the
+// same order): its record rec[PDATA], intrinsics terms kk[14], and its gradient max / bad flag max-accumulated.
+template <bool O32>
+__device__ __forceinline__ void point_rec(const DevProblem& P, const BaConsts& c, int cur, double radius,
+                                          const double* __restrict__ scale, int ap, double* rec, double* kk,
+                                          double& gmax, double& bad) {
+    const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
+    const double* K = P.K[cur];
+    const double* cams = P.cams[cur];
+    double acc[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) acc[i] = 0.0;
+    const int o0 = P.pt_ptr[ap], o1 = P.pt_ptr[ap + 1];
+    ObsRaw<O32> r_n = o0 < o1 ? po_obs<O32>(P, o0) : obs_zero<O32>();
+    for (int o = o0; o < o1; ++o) {
+        const ObsRaw<O32> r = r_n;
+        double pose[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) pose[k] = cams[7 * r.idx() + k];
+        if (o + 1 < o1) r_n = po_obs<O32>(P, o + 1);
+        ObsEval ev;
+        double jc[18], jp[9], jk[8];
+        lin_obs(c, pose, X, K, r.u(), r.v(), r.d(), ev, jc, jp, jk);
+        (void)jc;
+        point_accum(acc, jp, jk, ev);
+    }
+    point_tail(P, c, radius, scale, ap, X, acc, true, rec, kk, gmax, bad);
+}
+// The points' intrinsics Schur terms of one workgroup (out[14]: -Zk Zk^T packed, -Zk ze) added to S_kk / rhs_k.
+__device__ __forceinline__ void kk_add(const DevProblem& P, const double* out, double* S, double* rhs, bool atomic) {
+    if (threadIdx.x < 10) {
+        int m = 0, q = threadIdx.x;
+        while (q >= 4 - m) { q -= 4 - m; ++m; }
+        const int l = m + q;  // packed (m, l), l >= m
+        if (atomic) atomicAdd(&S[(size_t)(P.kb + l) * P.npad + P.kb + m], out[threadIdx.x]);
+        else S[(size_t)(P.kb + l) * P.npad + P.kb + m] += out[threadIdx.x];
+    } else if (threadIdx.x < 14) {
+        if (atomic) atomicAdd(&rhs[P.kb + threadIdx.x - 10], out[threadIdx.x]);
+        else rhs[P.kb + threadIdx.x - 10] += out[threadIdx.x];
+    }
+}
+// Point-side body of k_point_prep for point workgroup b (see k_point_prep). The small-window Schur launch
+// (k_schur_tile<..., FP>) runs it for the non-tiled points: points ap0 + point block pb, partial slot b, and the
+// intrinsics terms added to S / rhs (kkS / kkR, atomics) instead of a partial slot.
 template <int PP_LANES, bool O32>
 __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                                  int mode, const double* __restrict__ scale, double* __restrict__ cnp,
-                                                 double* __restrict__ pdata, double* __restrict__ part, const int b) {
+                                                 double* __restrict__ pdata, double* __restrict__ part, const int b,
+                                                 const int ap0, const int pb, double* kkS, double* kkR) {
     __shared__ double lds[4 * 14];
     __shared__ double out[14];
     __shared__ double red[4];
     if (st->done) return;
     const int cur = st->cur;
     const double radius = st->radius;
-    const int gt = b * PP_TPB + threadIdx.x;
-    const int ap = gt / PP_LANES, q = gt % PP_LANES;
+    const int gt = (pb < 0 ? b : pb) * PP_TPB + threadIdx.x;
+    const int ap = ap0 + gt / PP_LANES, q = gt % PP_LANES;
     double kk[14];
 #pragma unroll
     for (int i = 0; i < 14; ++i) kk[i] = 0.0;
@@ -601,21 +665,7 @@ __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaCo
             double jc[18], jp[9], jk[8];
             lin_obs(c, pose, X, K, r.u(), r.v(), r.d(), ev, jc, jp, jk);
             (void)jc;
-            acc[0] += jp[0] * jp[0] + jp[3] * jp[3] + jp[6] * jp[6];
-            acc[1] += jp[0] * jp[1] + jp[3] * jp[4] + jp[6] * jp[7];
-            acc[2] += jp[0] * jp[2] + jp[3] * jp[5] + jp[6] * jp[8];
-            acc[3] += jp[1] * jp[1] + jp[4] * jp[4] + jp[7] * jp[7];
-            acc[4] += jp[1] * jp[2] + jp[4] * jp[5] + jp[7] * jp[8];
-            acc[5] += jp[2] * jp[2] + jp[5] * jp[5] + jp[8] * jp[8];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) acc[6 + i] += jp[i] * ev.f[0] + jp[3 + i] * ev.f[1] + jp[6 + i] * ev.f[2];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {  // Kt = Jk^T Jp: jk row 0 is [k0, 0, su, 0], row 1 [0, k1, 0, su]
-                acc[9 + 0 * 3 + i] += jk[0] * jp[i];
-                acc[9 + 1 * 3 + i] += jk[5] * jp[3 + i];
-                acc[9 + 2 * 3 + i] += jk[2] * jp[i];
-                acc[9 + 3 * 3 + i] += jk[7] * jp[3 + i];
-            }
+            point_accum(acc, jp, jk, ev);
         }
         if (mode == 0) {
             double v3[3] = {acc[0], acc[3], acc[5]};
@@ -639,7 +689,8 @@ __device__ __forceinline__ void point_prep_block(const DevProblem& P, const BaCo
     bad = block_max(bad, red);
     // intrinsics terms: one partial per workgroup, summed in a fixed order by k_schur_tile's last workgroup (a
     // same-address f64 atomic per workgroup serialises at ~45 ns each: 391 x 14 of them cost ~17 us)
-    if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + b] = out[threadIdx.x];
+    if (kkS) kk_add(P, out, kkS, kkR, true);
+    else if (threadIdx.x < 14) part[(PART_PT_KK + threadIdx.x) * P.part_stride + b] = out[threadIdx.x];
     if (threadIdx.x == 0) {
         part[PART_PT_GMAX * P.part_stride + b] = gmax;
         part[PART_PT_BAD * P.part_stride + b] = bad;
@@ -848,20 +899,73 @@ struct EnvArgs {
     double* camdata_w;
     double* lin_w;
     int fin;  // 1: unsharded (finish the camera sums, lin); 2: landmark shard (local terms for the exchange)
+    // the small-window launch (k_schur_tile<..., FP>): the camera side and the non-tiled points ride in it
+    double* pdata_w;   // the point records the tiles compute (for the back-substitution)
+    double* part_w;    // per-tile gradient max / bad partials (k_final)
+    double* cpart_w;   // camera-side sub-segment partials (written by the camera-side workgroups)
+    double* seg_intr_w;
+    unsigned* sw_cnt;  // camera-side workgroups finished (monotonic within a solve)
+    unsigned sw_target;
+    int n_cs, n_gb;    // camera-side workgroups (= n_seg), non-tiled point workgroups
 };
 
 // PF (small grids, where occupancy does not bound the launch): each chunk's point records (G, e~, K~) are loaded
 // with the chunk's observation records — in the prologue, then a chunk ahead under the MFMAs — instead of at the
 // start of phase A.
-template <bool STAMP, bool O32, bool PF = false>
+//
+// FP (small windows, PF only; no k_lin_point in the LM loop): workgroups [0, n_tiles) are tiles that first compute
+// their own points' point side (point_rec, one point per thread; also in the terminal stop_next iteration, for the
+// gradient max): the records to pdata for phase A and the back-substitution, the intrinsics terms into S / rhs;
+// workgroup n_tiles idles; then n_cs camera-side workgroups (cam_side_block, each counted in sw_cnt when done),
+// n_gb workgroups for the non-tiled points (point_prep_block), and the envelope tiles, which wait until the
+// camera side of this launch is counted (every workgroup of the launch is resident: the host launches FP only
+// when they fit one round). A wait that times out raises FLAG_TIMEOUT (the iteration is re-run without FP).
+__device__ __forceinline__ bool sw_wait(const unsigned* cnt, unsigned target) {
+    for (unsigned i = 0; i < (1u << 20); ++i) {
+        if (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+template <bool STAMP, bool O32, bool PF = false, bool FP = false>
 __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                     const double* __restrict__ scale,
                                                     const double* __restrict__ pdata, double* __restrict__ S,
                                                     double* __restrict__ rhs, unsigned long long* __restrict__ stamps,
                                                     int nblk_pt, const double* __restrict__ part,
                                                     double* __restrict__ tbuf, EnvArgs E) {
+    static_assert(!FP || PF, "the fused point side keeps each point's record in registers (PF)");
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
+    if constexpr (FP) {
+        const int b = (int)blockIdx.x - P.n_tiles - 1;
+        if (b >= 0 && b < E.n_cs) {  // camera side (gated on an accepted step), counted whatever it did
+            cam_side_block<O32>(P, c, st, 1, E.cpart_w, E.seg_intr_w, E.lin_w + 1, b);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __threadfence();
+                atomicAdd(E.sw_cnt, 1u);
+            }
+            return;
+        }
+        if (b >= E.n_cs && b < E.n_cs + E.n_gb) {  // non-tiled points (intrinsics terms into S unless stop_next)
+            const bool sn = st->stop_next;
+            point_prep_block<1, O32>(P, c, st, 1, scale, nullptr, E.pdata_w, E.part_w, P.n_tiles + b - E.n_cs,
+                                     P.n_tiled_pts, b - E.n_cs, sn ? nullptr : S, rhs);
+            return;
+        }
+        if (b >= E.n_cs + E.n_gb) {  // envelope tiles, after this launch's camera side
+            if (st->done) return;
+            __shared__ int sw_ok;
+            if (threadIdx.x == 0) sw_ok = sw_wait(E.sw_cnt, E.sw_target) ? 1 : 0;
+            __syncthreads();
+            env_tile(P, c, st, b - E.n_cs - E.n_gb, E.tiles, E.camdata, E.lin, scale, S, rhs, E.chol_flag, E.fin,
+                     E.cpart, E.seg_intr, E.camdata_w, E.lin_w, true);
+            if (!sw_ok && threadIdx.x == 0) atomicOr(E.chol_flag, FLAG_TIMEOUT);
+            return;
+        }
+        if (b == -1 || st->done) return;  // (workgroup n_tiles: the intrinsics terms go straight into S)
+    } else {
     if ((int)blockIdx.x > P.n_tiles) {  // envelope tiles (fused path): also in the terminal stop_next iteration
         if (!st->done)
             env_tile(P, c, st, blockIdx.x - P.n_tiles - 1, E.tiles, E.camdata, E.lin, scale, S, rhs, E.chol_flag, E.fin,
@@ -869,7 +973,8 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         return;
     }
     if (skip_step(st)) return;
-    if ((int)blockIdx.x == P.n_tiles) {
+    }
+    if (!FP && (int)blockIdx.x == P.n_tiles) {
         // last workgroup: S_kk += the points' intrinsics Schur terms (k_point_prep's per-workgroup partials,
         // fixed order), rhs_k likewise. No tile writes S_kk or rhs_k.
         double acc[14];
@@ -946,6 +1051,11 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     int apb = P.chunk_ap[ch], ape = P.chunk_ap[ch + 1];
     int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
     const int n_last = P.n_adm - 1;
+    // the point records: FP writes them first (through a pointer that is not __restrict__) and reads them back
+    const double* pdr = FP ? E.pdata_w : pdata;
+    double fp_kk[FP ? 14 : 1], fp_gmax = 0.0, fp_bad = 0.0;  // FP: the tile's intrinsics terms, gradient max, bad
+#pragma unroll
+    for (int i = 0; i < (FP ? 14 : 1); ++i) fp_kk[i] = 0.0;
     // level 1: observation record of this thread
     int r_ac, r_ap, r_pt;
     ObsRaw<O32> r_o;  // camera index, pixel, depth
@@ -971,16 +1081,40 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 #pragma unroll
         for (int k = 0; k < 3; ++k) o_sp[k] = scale[P.off_pt + 3 * ap + k];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) o_G[k] = pdata[(size_t)ap * PDATA + k];
+        for (int k = 0; k < 6; ++k) o_G[k] = pdr[(size_t)ap * PDATA + k];
     };
     double q_pd[PF ? 21 : 1];
     auto load_pq = [&](int a0, int a1) {
         if constexpr (PF)
             if (tid < a1 - a0)
 #pragma unroll
-                for (int i = 0; i < 21; ++i) q_pd[i] = pdata[(size_t)(a0 + tid) * PDATA + i];
+                for (int i = 0; i < 21; ++i) q_pd[i] = pdr[(size_t)(a0 + tid) * PDATA + i];
     };
-    load_rec(ob + tid);
+    if constexpr (FP) load_rec(ob + tid);  // (independent of the point side: in flight under it)
+    if constexpr (FP) {
+        // the tile's points first, one per thread (point_rec: the records to pdata, read back below like the
+        // PF path's), their intrinsics terms / gradient max / bad flag kept for the end of the tile
+        const double radius = st->radius;
+        for (int ap = apb + tid; ap < P.chunk_ap[ch_end]; ap += TPB) {
+            double rec[PDATA], kkt[14];
+            point_rec<O32>(P, c, cur, radius, scale, ap, rec, kkt, fp_gmax, fp_bad);
+#pragma unroll
+            for (int i = 0; i < 14; ++i) fp_kk[i] += kkt[i];
+#pragma unroll
+            for (int i = 0; i < PDATA; ++i) E.pdata_w[(size_t)ap * PDATA + i] = rec[i];
+        }
+        if (st->stop_next) {  // terminal iteration: no step; the decision needs the points' gradient max
+            fp_gmax = block_max(fp_gmax, zeL);
+            fp_bad = block_max(fp_bad, zeL);
+            if (tid == 0) {
+                E.part_w[PART_PT_GMAX * P.part_stride + tile] = fp_gmax;
+                E.part_w[PART_PT_BAD * P.part_stride + tile] = fp_bad;
+            }
+            return;
+        }
+        __syncthreads();
+    }
+    if constexpr (!FP) load_rec(ob + tid);
     load_pq(apb, ape);
     load_ops(ob + tid < oe && r_ac >= 0);
     for (;;) {
@@ -998,7 +1132,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         SCH_STAMP(0);
         // ---- phase A
         if (tid < npts) {
-            const double* pd = PF ? q_pd : pdata + (size_t)(apb + tid) * PDATA;
+            const double* pd = PF ? q_pd : pdr + (size_t)(apb + tid) * PDATA;
             double G[6], Ks[12], es[3], zk[12], z3[3];
 #pragma unroll
             for (int i = 0; i < 6; ++i) G[i] = pd[i];
@@ -1169,6 +1303,16 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         const double v = -rhs_acc;
         if (tbuf) tbuf[(size_t)tile * SCH_TBUF + er * SCH_TBUF_LD + lane] = v;
         else atomicAdd(&rhs[6 * base + lane], v);
+    }
+    if constexpr (FP) {  // the tile's points: intrinsics terms into S / rhs, gradient max / bad for k_final
+        block_sum<14>(fp_kk, Mt, Mt + 64);  // (Mt is free after the last chunk's barrier)
+        kk_add(P, Mt + 64, S, rhs, true);
+        fp_gmax = block_max(fp_gmax, zeL);
+        fp_bad = block_max(fp_bad, zeL);
+        if (tid == 0) {
+            E.part_w[PART_PT_GMAX * P.part_stride + tile] = fp_gmax;
+            E.part_w[PART_PT_BAD * P.part_stride + tile] = fp_bad;
+        }
     }
     if constexpr (STAMP) {
         __syncthreads();
@@ -2519,6 +2663,8 @@ hipError_t launch_prep_gather(const DevProblem& P, const PrepRaw& R, hipStream_t
 
 hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, const double* cams0, const double* pts0,
                         const double* K0, int n_cams, int n_points, hipStream_t s) {
+    if (W.sw_cnt) CK(hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));  // the small-window launch's counter
+    W.sw_seq = 0;
     const int ncd = 7 * n_cams, npd = 3 * n_points;
     // fused path: S (npad^2, even: npad is a multiple of 16) and rhs are zeroed here too
     const size_t nS2 = W.fused ? (size_t)P.npad * P.npad / 2 : 0;
@@ -2541,6 +2687,19 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     // point records + intrinsics Schur partials, then the envelope of S: clear + camera / intrinsics
     // blocks, LM diagonal, pad (rank 0 only), the points' intrinsics terms, rhs, chol_flag
     EnvArgs E{};
+    if (W.sw) {  // small window: one launch (k_schur_tile<..., FP>), no k_lin_point
+        E = EnvArgs{W.env_tile, W.n_env, W.camdata, W.lin, W.chol_flag, W.camdata_part, W.seg_intr, W.camdata, W.lin, 1,
+                    W.pdata, W.part, W.camdata_part, W.seg_intr, W.sw_cnt, (++W.sw_seq) * (unsigned)P.n_seg, P.n_seg,
+                    pp_blocks(P.n_ap - P.n_tiled_pts, 1)};
+        const int n_sch = P.n_tiles + 1 + E.n_cs + E.n_gb + E.n_env;
+        OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true, true>), (k_schur_tile<false, false, true, true>), dim3(n_sch),
+            dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, (unsigned long long*)nullptr, 0, W.part,
+            (double*)nullptr, E);
+        if (P.n_ovf_obs > 0)
+            OPL(K_OBS_PAIRS, k_obs_pairs<true>, k_obs_pairs<false>, dim3(nblocks(P.n_ovf_obs, TPB)), dim3(TPB), 0, s, P, c,
+                W.st, W.scale, W.pdata, W.S, W.rhs);
+        return hipSuccess;
+    }
     if (W.fused) {  // point side + gated camera side in one launch; the envelope tiles ride in k_schur_tile
         CK(launch_lin_point(P, c, 1, W, s, pf));
         // unsharded: the envelope tiles finish the camera sums and lin (fin 1); landmark shard: they write this
@@ -2713,7 +2872,8 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
     if (P.n_ap > 0)
         OPL(K_BACKSUB_EVAL, k_backsub_chunk<true>, k_backsub_chunk<false>, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
-    const int nb_pt = pp_parts(P);
+    // the points' gradient max / bad partials: per point workgroup, or per Schur tile + non-tiled point workgroup
+    const int nb_pt = W.sw ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts, 1) : pp_parts(P);
     // the split BCR kernel's call epoch (the persistent kernel's is advanced by k_bcr_border)
     unsigned* const ep = (P.solver == 2 && W.bcr.persist >= 2) ? W.bcr.flags : nullptr;
     if (!W.comm.on()) {

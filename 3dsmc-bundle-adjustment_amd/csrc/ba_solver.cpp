@@ -659,6 +659,7 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     ctx->pinfo.obs_uploaded = any_vals ? 1 : 0;
     ctx->pinfo.upload_ms = now_ms() - tu;
     ctx->pinfo.bcr_path = P.solver == 2 ? (ctx->W.bcr.dense1 ? 4 : ctx->W.bcr.persist) : -1;
+    ctx->pinfo.lin_path = ctx->W.sw;
     ctx->prepared = true;
     ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;
     return 1;
@@ -862,7 +863,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         const std::vector<int>& tile_base = pl.tile_base;
         const std::vector<int>& ovf_obs = pl.ovf_obs;
         const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
-        const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS, 1});
+        // (+ the small-window launch's per-tile and non-tiled point partials, §3 of DESIGN)
+        const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS,
+                                          (int)pl.tile_base.size() + pp_blocks(n_ap - n_tiled, 1), 1});
         HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
         // landmark sharding: pack buffers of the envelope tiles of S, exchange scalars
         if (shard) {
@@ -920,6 +923,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         P.bs_chunk = dptr(BS_CHUNK);
         P.n_bs_chunks = n_bs_chunks;
         P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
+        P.n_tiled_pts = n_tiled;
         ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
         P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
         P.n = n; P.npad = npad; P.kb = 6 * nac;
@@ -1021,6 +1025,19 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             // landmark shards: the same choice on every rank (it fixes the collective sequence), so only uniform inputs
             W.fused = (shard ? (!o.deterministic && !off)
                              : (!W.det_tbuf && n_ap > 0 && n_seg > 0 && !off)) ? 1 : 0;
+            // small windows: the point side inside the Schur tiles, the camera side and the non-tiled points as
+            // extra workgroups of the Schur launch (no k_lin_point in the LM loop) when the whole launch is one
+            // resident round (its envelope tiles wait for its camera side); MIBA_SW=0 keeps the two launches
+            const char* e2 = std::getenv("MIBA_SW");
+            const int n_sw = P.n_tiles + 1 + n_seg + pp_blocks(n_ap - n_tiled, 1) + n_env;
+            // one-block windows only (<= BCR_CAMS active cameras): on C3 (50 cameras, 5 blocks) the fused launch
+            // measured 3 us per LM iteration slower, on C1 1.3 us faster
+            W.sw = (W.fused && !shard && P.n_tiles > 0 && n_sw <= 256 && nac <= BCR_CAMS && !(e2 && e2[0] == '0')) ? 1
+                                                                                                                : 0;
+            if (e2 && e2[0] == '2') W.sw = (W.fused && !shard && P.n_tiles > 0 && n_sw <= 256) ? 1 : 0;  // A/B
+            W.sw_cnt = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 2);
+            W.sw_seq = 0;
+            HIPCHECK(ctx, hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));
         }
         BaConsts& C = ctx->C;
         ctx->n_adm_all = n_adm_all;
@@ -1116,6 +1133,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->pinfo.upload_ms = (tp_raw - tp0) + (now_ms() - tp_plan);
         ctx->pinfo.obs_uploaded = 1;
         ctx->pinfo.bcr_path = P.solver == 2 ? (ctx->W.bcr.dense1 ? 4 : ctx->W.bcr.persist) : -1;
+        ctx->pinfo.lin_path = ctx->W.sw;
         return BA_OK;
     };
     int rc = finish();
@@ -1203,6 +1221,7 @@ static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     BcrWork& Bw = ctx->W.bcr;
     Bw.persist = 0;
     Bw.dense1 = 0;  // (k_bcr_dense1 waits only inside its workgroup: a forced spin bound can still time it out)
+    ctx->W.sw = 0;  // the small-window Schur launch's envelope tiles wait for its camera side
     ctx->bcr_fallback = true;
     if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
     HIPCHECK(ctx, bcr_reset_pull_slots(Bw, false, s));

@@ -138,6 +138,7 @@ class BaPrepareInfo(C.Structure):
         ("plan_ms", C.c_double),
         ("upload_ms", C.c_double),
         ("total_ms", C.c_double),
+        ("lin_path", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

@@ -194,6 +194,9 @@ typedef struct ba_prepare_info {
     double plan_ms;          /* host plan build (0 on a reuse) */
     double upload_ms;        /* staging + enqueue of the uploads and the device gather */
     double total_ms;         /* the whole prepare, device work included */
+    int32_t lin_path;        /* linearisation of the LM loop: 1 = small window, the point side inside the Schur
+                                tiles and the camera side in the Schur launch (no separate linearisation launch);
+                                0 = a linearisation launch before the Schur launch */
 } ba_prepare_info;
 int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info);
 

@@ -277,3 +277,48 @@ def test_large_configs_match_oracle(config, iters):
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sg, so)
     np.testing.assert_allclose(p.cams, q.cams, rtol=0, atol=1e-9)
     np.testing.assert_allclose(p.intr, q.intr, rtol=1e-9)
+
+
+@pytest.mark.parametrize("case", ["C1", "C3", "gauge_ovf_shuffled", "f64_layout_gauge3"])
+def test_small_window_fused_schur(case, monkeypatch):
+    """Small windows take the one-launch linearisation (ba_prepare_info.lin_path 1: the point side inside the Schur
+    tiles, the camera side and the non-tiled points as extra workgroups of the Schur launch). Against the two-launch
+    path (MIBA_SW=0) and the oracle, tolerances off, 6 iterations; gauge-only points (a single observation on the
+    fixed camera), overflow points (duplicate observations), inadmissible depths, shuffled observations and the f64
+    layout included."""
+    from miba.solver import Solver
+    if case in ("C1", "C3"):
+        p = synthetic.make_config(case)
+    elif case == "gauge_ovf_shuffled":
+        p = synthetic.make_problem(10, 900, obs_per_point=(1, 6), seed=71, fixed_cam=0, dup_frac=0.03,
+                                   bad_depth_frac=0.02, shuffle_obs=True, sensor_f32=True)
+    else:
+        p = synthetic.make_problem(24, 1500, obs_per_point=(1, 8), seed=72, fixed_cam=3, dup_frac=0.01)
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
+    # the default takes it for one-block windows (<= 10 active cameras); MIBA_SW=2 forces it on larger ones
+    on = "1" if p.n_cams <= 11 else "2"
+    res = {}
+    for sw in (on, "0"):
+        monkeypatch.setenv("MIBA_SW", sw)
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
+            res[sw] = (s.solve(q), q)
+            assert s.last_prepare()["lin_path"] == (sw != "0"), sw
+    (sa, qa), (sb, qb) = res[on], res["0"]
+    assert sa["num_iterations"] == sb["num_iterations"] == 6
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] == so["num_successful_steps"]
+    assert sa["termination_type"] == sb["termination_type"]
+    assert abs(sa["initial_cost"] - sb["initial_cost"]) <= 1e-12 * sb["initial_cost"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sb["final_cost"]
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(qa.intr, qb.intr, rtol=1e-9)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
+    # the same window again on the same context (plan cache): the same result
+    monkeypatch.setenv("MIBA_SW", on)
+    with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
+        r1 = s.solve(p.copy())
+        r2 = s.solve(p.copy())
+        assert s.last_prepare()["lin_path"] == 1
+    assert abs(r1["final_cost"] - r2["final_cost"]) <= 1e-12 * r1["final_cost"]
