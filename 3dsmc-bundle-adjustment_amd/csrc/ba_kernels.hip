@@ -937,6 +937,8 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     static_assert(!FP || PF, "the fused point side keeps each point's record in registers (PF)");
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
+    __shared__ double psum[FP ? 21 * CHUNK_OBS : 1];                      // FP: per-observation point sums
+    __shared__ double gL[FP ? 6 * CHUNK_PTS : 1];                         // FP: the chunk's G (phase A)
     if constexpr (FP) {
         const int b = (int)blockIdx.x - P.n_tiles - 1;
         if (b >= 0 && b < E.n_cs) {  // camera side (gated on an accepted step), counted whatever it did
@@ -964,7 +966,8 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
             if (!sw_ok && threadIdx.x == 0) atomicOr(E.chol_flag, FLAG_TIMEOUT);
             return;
         }
-        if (b == -1 || st->done) return;  // (workgroup n_tiles: the intrinsics terms go straight into S)
+        if (b == -1) return;  // (workgroup n_tiles: the tiles add the intrinsics terms themselves)
+        if (st->done) return;
     } else {
     if ((int)blockIdx.x > P.n_tiles) {  // envelope tiles (fused path): also in the terminal stop_next iteration
         if (!st->done)
@@ -1066,12 +1069,17 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     };
     // level 2: operands of the observation
     double o_pose[7], o_X[3], o_sc[6], o_sp[3], o_G[6];
-    bool o_ok = false;
-    auto load_ops = [&](bool ok) {
+    bool o_ok = false, o_in = false;
+    // in: this thread has an observation of the chunk; ok: ... on an active camera (a column of M'). FP evaluates
+    // every observation of the chunk (the point side's sums include the gauge camera's)
+    auto load_ops = [&](bool in) {
+        const bool ok = in && r_ac >= 0;
         o_ok = ok;
+        o_in = in;
+        const bool ev = FP ? in : ok;
         const int ac = ok ? r_ac : 0, ap = ok ? r_ap : 0;
-        const double* pose = P.cams[cur] + 7 * (ok ? r_o.idx() : 0);
-        const double* X = P.pts[cur] + 3 * (ok ? r_pt : 0);
+        const double* pose = P.cams[cur] + 7 * (ev ? r_o.idx() : 0);
+        const double* X = P.pts[cur] + 3 * (ev ? r_pt : 0);
 #pragma unroll
         for (int k = 0; k < 7; ++k) o_pose[k] = pose[k];
 #pragma unroll
@@ -1080,45 +1088,74 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         for (int k = 0; k < 6; ++k) o_sc[k] = scale[6 * ac + k];
 #pragma unroll
         for (int k = 0; k < 3; ++k) o_sp[k] = scale[P.off_pt + 3 * ap + k];
+        if constexpr (!FP)  // FP: G from this chunk's point threads (gL)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) o_G[k] = pdr[(size_t)ap * PDATA + k];
+            for (int k = 0; k < 6; ++k) o_G[k] = pdr[(size_t)ap * PDATA + k];
     };
     double q_pd[PF ? 21 : 1];
     auto load_pq = [&](int a0, int a1) {
-        if constexpr (PF)
+        if constexpr (PF && !FP)  // (FP: the chunk's point threads compute them)
             if (tid < a1 - a0)
 #pragma unroll
                 for (int i = 0; i < 21; ++i) q_pd[i] = pdr[(size_t)(a0 + tid) * PDATA + i];
     };
-    if constexpr (FP) load_rec(ob + tid);  // (independent of the point side: in flight under it)
-    if constexpr (FP) {
-        // the tile's points first, one per thread (point_rec: the records to pdata, read back below like the
-        // PF path's), their intrinsics terms / gradient max / bad flag kept for the end of the tile
-        const double radius = st->radius;
+    const double radius = FP ? st->radius : 0.0;
+    if (FP && st->stop_next) {
+        // terminal iteration: no step; the decision needs the points' gradient max (point_rec, one point per thread)
         for (int ap = apb + tid; ap < P.chunk_ap[ch_end]; ap += TPB) {
             double rec[PDATA], kkt[14];
             point_rec<O32>(P, c, cur, radius, scale, ap, rec, kkt, fp_gmax, fp_bad);
-#pragma unroll
-            for (int i = 0; i < 14; ++i) fp_kk[i] += kkt[i];
-#pragma unroll
-            for (int i = 0; i < PDATA; ++i) E.pdata_w[(size_t)ap * PDATA + i] = rec[i];
         }
-        if (st->stop_next) {  // terminal iteration: no step; the decision needs the points' gradient max
-            fp_gmax = block_max(fp_gmax, zeL);
-            fp_bad = block_max(fp_bad, zeL);
-            if (tid == 0) {
-                E.part_w[PART_PT_GMAX * P.part_stride + tile] = fp_gmax;
-                E.part_w[PART_PT_BAD * P.part_stride + tile] = fp_bad;
-            }
-            return;
+        fp_gmax = block_max(fp_gmax, zeL);
+        fp_bad = block_max(fp_bad, zeL);
+        if (tid == 0) {
+            E.part_w[PART_PT_GMAX * P.part_stride + tile] = fp_gmax;
+            E.part_w[PART_PT_BAD * P.part_stride + tile] = fp_bad;
         }
-        __syncthreads();
+        return;
     }
-    if constexpr (!FP) load_rec(ob + tid);
+    load_rec(ob + tid);
     load_pq(apb, ape);
-    load_ops(ob + tid < oe && r_ac >= 0);
+    load_ops(ob + tid < oe);
     for (;;) {
         const int npts = ape - apb;
+        double Wt[FP ? 18 : 1];  // FP: this observation's W~, from its one Jacobian evaluation
+        if constexpr (FP) {
+            // the point side of the chunk's points from the same evaluation phase A uses: each observation's sums to
+            // psum, then one thread per point adds its observations' in order (the sums of point_rec, bitwise)
+            if (o_in) {
+                ObsEval ev;
+                double jc[18], jp[9], jk[8], a[21];
+                lin_obs(c, o_pose, o_X, K, r_o.u(), r_o.v(), r_o.d(), ev, jc, jp, jk);
+                if (o_ok) w_tilde(jc, jp, o_sc, o_sp, Wt);
+#pragma unroll
+                for (int i = 0; i < 21; ++i) a[i] = 0.0;
+                point_accum(a, jp, jk, ev);
+#pragma unroll
+                for (int i = 0; i < 21; ++i) psum[i * CHUNK_OBS + tid] = a[i];
+            }
+            __syncthreads();
+            if (tid < npts) {
+                const int ap = apb + tid;
+                const int q0 = P.pt_ptr[ap] - ob, q1 = P.pt_ptr[ap + 1] - ob;
+                const double* Xp = P.pts[cur] + 3 * P.pt_idx[ap];
+                double acc[21], rec[PDATA], kkt[14];
+#pragma unroll
+                for (int i = 0; i < 21; ++i) acc[i] = 0.0;
+                for (int q = q0; q < q1; ++q)
+#pragma unroll
+                    for (int i = 0; i < 21; ++i) acc[i] += psum[i * CHUNK_OBS + q];
+                point_tail(P, c, radius, scale, ap, Xp, acc, true, rec, kkt, fp_gmax, fp_bad);
+#pragma unroll
+                for (int i = 0; i < 14; ++i) fp_kk[i] += kkt[i];
+#pragma unroll
+                for (int i = 0; i < PDATA; ++i) E.pdata_w[(size_t)ap * PDATA + i] = rec[i];
+#pragma unroll
+                for (int i = 0; i < 21; ++i) q_pd[i] = rec[i];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) gL[6 * tid + k] = rec[k];
+            }
+        }
         {
             // every thread the same number of 16-byte stores, unrolled: straight-line ds_write_b128 with immediate
             // offsets (the strided loop spent ~120 instructions of issue per thread on 15 stores)
@@ -1151,11 +1188,18 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         }
         if (o_ok) {
             const int pl = r_ap - apb;
-            ObsEval ev;
-            double jc[18], jp[9], jk[8];
-            lin_obs(c, o_pose, o_X, K, r_o.u(), r_o.v(), r_o.d(), ev, jc, jp, jk);
             double W[18];
-            w_tilde(jc, jp, o_sc, o_sp, W);
+            if constexpr (FP) {
+#pragma unroll
+                for (int i = 0; i < 18; ++i) W[i] = Wt[i];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) o_G[k] = gL[6 * pl + k];
+            } else {
+                ObsEval ev;
+                double jc[18], jp[9], jk[8];
+                lin_obs(c, o_pose, o_X, K, r_o.u(), r_o.v(), r_o.d(), ev, jc, jp, jk);
+                w_tilde(jc, jp, o_sc, o_sp, W);
+            }
             const double g00 = o_G[0], g10 = o_G[1], g11 = o_G[2], g20 = o_G[3], g21 = o_G[4], g22 = o_G[5];
             double* c0 = Mt + (3 * pl) * SCH_LDM + 6 * (r_ac - base);
 #pragma unroll
@@ -1268,7 +1312,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         if (!more) break;
         // ---- prefetch: level-2 operands of the next chunk
         const int oe_n = P.pt_ptr[ape_n];
-        load_ops(oe + tid < oe_n && r_ac >= 0);
+        load_ops(oe + tid < oe_n);
         ++ch;
         apb = ape; ape = ape_n;
         ob = oe; oe = oe_n;
@@ -1304,14 +1348,25 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         if (tbuf) tbuf[(size_t)tile * SCH_TBUF + er * SCH_TBUF_LD + lane] = v;
         else atomicAdd(&rhs[6 * base + lane], v);
     }
-    if constexpr (FP) {  // the tile's points: intrinsics terms into S / rhs, gradient max / bad for k_final
-        block_sum<14>(fp_kk, Mt, Mt + 64);  // (Mt is free after the last chunk's barrier)
-        kk_add(P, Mt + 64, S, rhs, true);
-        fp_gmax = block_max(fp_gmax, zeL);
-        fp_bad = block_max(fp_bad, zeL);
-        if (tid == 0) {
-            E.part_w[PART_PT_GMAX * P.part_stride + tile] = fp_gmax;
-            E.part_w[PART_PT_BAD * P.part_stride + tile] = fp_bad;
+    if constexpr (FP) {
+        // the tile's points: intrinsics terms into S / rhs, gradient max / bad for k_final. Only the point threads
+        // (tid < CHUNK_PTS: wave 0) hold any, so wave 0 reduces them alone, without a workgroup barrier
+        static_assert(CHUNK_PTS <= 64, "the point threads are wave 0's");
+        if (wave == 0) {
+            wave_sum<14>(fp_kk);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                fp_gmax = fmax(fp_gmax, __shfl_xor(fp_gmax, off));
+                fp_bad = fmax(fp_bad, __shfl_xor(fp_bad, off));
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < 14; ++i) zeL[i] = fp_kk[i];  // (zeL is free after the last chunk)
+                E.part_w[PART_PT_GMAX * P.part_stride + tile] = fp_gmax;
+                E.part_w[PART_PT_BAD * P.part_stride + tile] = fp_bad;
+            }
+            __builtin_amdgcn_wave_barrier();
+            kk_add(P, zeL, S, rhs, true);  // (lanes 0..13)
         }
     }
     if constexpr (STAMP) {
@@ -2692,6 +2747,26 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                     W.pdata, W.part, W.camdata_part, W.seg_intr, W.sw_cnt, (++W.sw_seq) * (unsigned)P.n_seg, P.n_seg,
                     pp_blocks(P.n_ap - P.n_tiled_pts, 1)};
         const int n_sch = P.n_tiles + 1 + E.n_cs + E.n_gb + E.n_env;
+        static int fp_stamps = -1;
+        static unsigned long long* fst = nullptr;
+        if (fp_stamps < 0) {
+            const char* e = getenv("MIBA_SCHUR_STAMPS");
+            fp_stamps = (e && e[0] == '1') ? 1 : 0;
+        }
+        if (fp_stamps == 1 && P.obs32) {  // diagnostic: per-tile phase cycles (zero, A incl. the point side, B, flush)
+            if (!fst) CK(hipMalloc(&fst, sizeof(unsigned long long) * 5 * 256));
+            PL(K_SCHUR_TILE, (k_schur_tile<true, true, true, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale,
+               W.pdata, W.S, W.rhs, fst, 0, W.part, (double*)nullptr, E);
+            std::vector<unsigned long long> h5((size_t)5 * P.n_tiles);
+            CK(hipMemcpyAsync(h5.data(), fst, sizeof(h5[0]) * h5.size(), hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            double sum[5] = {0, 0, 0, 0, 0};
+            for (int t = 0; t < P.n_tiles; ++t)
+                for (int k = 0; k < 5; ++k) sum[k] += (double)h5[5 * t + k];
+            fprintf(stderr, "schur_tile FP %d tiles, mean cycles/tile: point side + zero stores %.0f, barrier %.0f, phaseA %.0f, "
+                    "phaseB %.0f, flush %.0f\n", P.n_tiles, sum[4] / P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles,
+                    sum[2] / P.n_tiles, sum[3] / P.n_tiles);
+        } else
         OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true, true>), (k_schur_tile<false, false, true, true>), dim3(n_sch),
             dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, (unsigned long long*)nullptr, 0, W.part,
             (double*)nullptr, E);
