@@ -330,6 +330,9 @@ struct DevWork {
     // has no k_lin_point (k_schur_tile<..., FP>). sw_cnt: camera-side workgroups finished (monotonic within a
     // solve; reset by launch_reset), sw_seq: Schur launches of this solve (host side)
     int sw = 0;
+    // larger windows (unsharded, default mode): the tiled points' point side in the Schur tiles (k_schur_tile<..., FP>,
+    // one Jacobian evaluation per observation for it and M'), k_lin_point runs the camera side + the non-tiled points
+    int fpl = 0;
     unsigned* sw_cnt = nullptr;
     unsigned sw_seq = 0;
 };

@@ -707,8 +707,10 @@ __global__ __launch_bounds__(TPB) void k_lin_point(DevProblem P, BaConsts c, con
                                                    const double* __restrict__ scale, double* __restrict__ cnp,
                                                    double* __restrict__ pdata, double* __restrict__ part, int nb_pp,
                                                    double* __restrict__ cpart, double* __restrict__ seg_intr,
-                                                   double* __restrict__ gmax_word, int mode) {
-    if ((int)blockIdx.x < nb_pp) point_prep_block<PP_LANES, O32>(P, c, st, mode, scale, cnp, pdata, part, blockIdx.x);
+                                                   double* __restrict__ gmax_word, int mode, int ap0, int slot0) {
+    // (ap0 / slot0: the fused-point-side Schur path runs only the non-tiled points here, into slots after the tiles')
+    if ((int)blockIdx.x < nb_pp)
+        point_prep_block<PP_LANES, O32>(P, c, st, mode, scale, cnp, pdata, part, slot0 + blockIdx.x, ap0, blockIdx.x);
     else cam_side_block<O32>(P, c, st, mode, cpart, seg_intr, gmax_word,
                         P.xcd_map ? xcd_seg(blockIdx.x, nb_pp, P.n_seg) : (int)blockIdx.x - nb_pp);
 }
@@ -927,19 +929,20 @@ __device__ __forceinline__ bool sw_wait(const unsigned* cnt, unsigned target) {
     }
     return false;
 }
-template <bool STAMP, bool O32, bool PF = false, bool FP = false>
-__global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, const LmState* __restrict__ st,
-                                                    const double* __restrict__ scale,
-                                                    const double* __restrict__ pdata, double* __restrict__ S,
-                                                    double* __restrict__ rhs, unsigned long long* __restrict__ stamps,
-                                                    int nblk_pt, const double* __restrict__ part,
-                                                    double* __restrict__ tbuf, EnvArgs E) {
-    static_assert(!FP || PF, "the fused point side keeps each point's record in registers (PF)");
+template <bool STAMP, bool O32, bool PF, bool FP, bool SW>
+__device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const LmState* __restrict__ st,
+                                                const double* __restrict__ scale, const double* __restrict__ pdata,
+                                                double* __restrict__ S, double* __restrict__ rhs,
+                                                unsigned long long* __restrict__ stamps, int nblk_pt,
+                                                const double* __restrict__ part, double* __restrict__ tbuf, EnvArgs E) {
+    static_assert(!SW || FP, "the small-window launch runs the point side in its tiles");
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
-    __shared__ double psum[FP ? 21 * CHUNK_OBS : 1];                      // FP: per-observation point sums
     __shared__ double gL[FP ? 6 * CHUNK_PTS : 1];                         // FP: the chunk's G (phase A)
-    if constexpr (FP) {
+    // FP: per-observation point sums, in M' before the chunk clears it
+    static_assert(21 * CHUNK_OBS <= SCH_K * SCH_LDM, "the point sums fit M'");
+    double* const psum = Mt;
+    if constexpr (SW) {
         const int b = (int)blockIdx.x - P.n_tiles - 1;
         if (b >= 0 && b < E.n_cs) {  // camera side (gated on an accepted step), counted whatever it did
             cam_side_block<O32>(P, c, st, 1, E.cpart_w, E.seg_intr_w, E.lin_w + 1, b);
@@ -975,17 +978,21 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
                      E.cpart, E.seg_intr, E.camdata_w, E.lin_w, true);
         return;
     }
-    if (skip_step(st)) return;
+    if constexpr (FP) {  // (FP tiles run in the terminal stop_next iteration too: the decision needs their gradient max)
+        if (st->done || ((int)blockIdx.x == P.n_tiles && st->stop_next)) return;
+    } else if (skip_step(st)) return;
     }
-    if (!FP && (int)blockIdx.x == P.n_tiles) {
+    if (!SW && (int)blockIdx.x == P.n_tiles) {
         // last workgroup: S_kk += the points' intrinsics Schur terms (k_point_prep's per-workgroup partials,
-        // fixed order), rhs_k likewise. No tile writes S_kk or rhs_k.
+        // fixed order), rhs_k likewise. No tile writes S_kk or rhs_k (FP: the non-tiled points' partials, slots
+        // after the tiles'; the tiles add theirs).
         double acc[14];
 #pragma unroll
         for (int q = 0; q < 14; ++q) acc[q] = 0.0;
+        const int s0 = FP ? P.n_tiles : 0;
         for (int i = threadIdx.x; i < nblk_pt; i += TPB)
 #pragma unroll
-            for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + i];
+            for (int q = 0; q < 14; ++q) acc[q] += part[(PART_PT_KK + q) * P.part_stride + s0 + i];
         block_sum<14>(acc, Mt, Mt + 64);
         const double* out = Mt + 64;
         if (threadIdx.x < 10) {
@@ -1092,7 +1099,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 #pragma unroll
             for (int k = 0; k < 6; ++k) o_G[k] = pdr[(size_t)ap * PDATA + k];
     };
-    double q_pd[PF ? 21 : 1];
+    double q_pd[(PF || FP) ? 21 : 1];
     auto load_pq = [&](int a0, int a1) {
         if constexpr (PF && !FP)  // (FP: the chunk's point threads compute them)
             if (tid < a1 - a0)
@@ -1155,6 +1162,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
 #pragma unroll
                 for (int k = 0; k < 6; ++k) gL[6 * tid + k] = rec[k];
             }
+            __syncthreads();  // (psum is M': read before the clear)
         }
         {
             // every thread the same number of 16-byte stores, unrolled: straight-line ds_write_b128 with immediate
@@ -1169,7 +1177,7 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
         SCH_STAMP(0);
         // ---- phase A
         if (tid < npts) {
-            const double* pd = PF ? q_pd : pdr + (size_t)(apb + tid) * PDATA;
+            const double* pd = (PF || FP) ? q_pd : pdr + (size_t)(apb + tid) * PDATA;
             double G[6], Ks[12], es[3], zk[12], z3[3];
 #pragma unroll
             for (int i = 0; i < 6; ++i) G[i] = pd[i];
@@ -1377,6 +1385,22 @@ __global__ __launch_bounds__(TPB) void k_schur_tile(DevProblem P, BaConsts c, co
     }
 #undef SCH_STAMP
 }
+#define SCH_ARGS                                                                                                       \
+    DevProblem P, BaConsts c, const LmState *__restrict__ st, const double *__restrict__ scale,                       \
+        const double *__restrict__ pdata, double *__restrict__ S, double *__restrict__ rhs,                           \
+        unsigned long long *__restrict__ stamps, int nblk_pt, const double *__restrict__ part,                       \
+        double *__restrict__ tbuf, EnvArgs E
+template <bool STAMP, bool O32, bool PF = false, bool FP = false, bool SW = false>
+__global__ __launch_bounds__(TPB) void k_schur_tile(SCH_ARGS) {
+    schur_tile_body<STAMP, O32, PF, FP, SW>(P, c, st, scale, pdata, S, rhs, stamps, nblk_pt, part, tbuf, E);
+}
+// The fused point side on larger windows: held to two workgroups per CU (the LDS allows two; the registers the
+// point side adds would otherwise leave one), a few spilled registers in exchange
+template <bool O32>
+__global__ __launch_bounds__(TPB, 2) void k_schur_tile_fpl(SCH_ARGS) {
+    schur_tile_body<false, O32, false, true, false>(P, c, st, scale, pdata, S, rhs, stamps, nblk_pt, part, tbuf, E);
+}
+#undef SCH_ARGS
 
 // Deterministic mode (ba_options.deterministic): every Schur tile wrote its flush into its own slab
 // tbuf[tile] (rows: 6 span camera dofs | 4 intrinsics | rhs; columns: 6 span camera dofs) instead of
@@ -2591,15 +2615,18 @@ int schur_tile_slots() {
 // k_lin_point over nb point workgroups + the camera sub-segments (mode 1: LM loop, mode 0: IterationZero)
 static hipError_t launch_lin_point(const DevProblem& P, const BaConsts& c, int mode, DevWork& W, hipStream_t s,
                                    Prof* pf) {
-    const int nb = pp_blocks(P.n_ap);
+    // W.fpl (LM loop): the tiled points' point side runs in the Schur tiles; here only the non-tiled points
+    const bool fpl = mode == 1 && W.fpl;
+    const int ap0 = fpl ? P.n_tiled_pts : 0, slot0 = fpl ? P.n_tiles : 0;
+    const int nb = pp_blocks(P.n_ap - ap0);
     const int kid = mode ? K_LIN_POINT : K_CAM_SIDE;
     if (nb + P.n_seg > 0) switch (pp_lanes()) {
         case 1: OPL(kid, (k_lin_point<1, true>), (k_lin_point<1, false>), dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
-                   W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
+                   W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode, ap0, slot0); break;
         case 2: OPL(kid, (k_lin_point<2, true>), (k_lin_point<2, false>), dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
-                   W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
+                   W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode, ap0, slot0); break;
         default: OPL(kid, (k_lin_point<4, true>), (k_lin_point<4, false>), dim3(nb + P.n_seg), dim3(TPB), 0, s, P, c, W.st, W.scale, W.cnp, W.pdata,
-                    W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode); break;
+                    W.part, nb, W.camdata_part, W.seg_intr, W.lin + 1, mode, ap0, slot0); break;
     }
     return hipSuccess;
 }
@@ -2755,7 +2782,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
         }
         if (fp_stamps == 1 && P.obs32) {  // diagnostic: per-tile phase cycles (zero, A incl. the point side, B, flush)
             if (!fst) CK(hipMalloc(&fst, sizeof(unsigned long long) * 5 * 256));
-            PL(K_SCHUR_TILE, (k_schur_tile<true, true, true, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale,
+            PL(K_SCHUR_TILE, (k_schur_tile<true, true, true, true, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale,
                W.pdata, W.S, W.rhs, fst, 0, W.part, (double*)nullptr, E);
             std::vector<unsigned long long> h5((size_t)5 * P.n_tiles);
             CK(hipMemcpyAsync(h5.data(), fst, sizeof(h5[0]) * h5.size(), hipMemcpyDeviceToHost, s));
@@ -2767,7 +2794,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                     "phaseB %.0f, flush %.0f\n", P.n_tiles, sum[4] / P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles,
                     sum[2] / P.n_tiles, sum[3] / P.n_tiles);
         } else
-        OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true, true>), (k_schur_tile<false, false, true, true>), dim3(n_sch),
+        OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true, true, true>), (k_schur_tile<false, false, true, true, true>), dim3(n_sch),
             dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, (unsigned long long*)nullptr, 0, W.part,
             (double*)nullptr, E);
         if (P.n_ovf_obs > 0)
@@ -2784,6 +2811,10 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                                   W.camdata_loc, W.camdata_loc + ncd, 2}
                         : EnvArgs{W.env_tile, W.n_env, W.camdata, W.lin, W.chol_flag, W.camdata_part, W.seg_intr,
                                   W.camdata, W.lin, 1};
+        if (W.fpl) {  // the tiles write the point records and their partials
+            E.pdata_w = W.pdata;
+            E.part_w = W.part;
+        }
     } else if (P.n_ap > 0)
         CK(launch_point_prep(P, c, 1, W, s, pf));  // + the envelope tiles
     else
@@ -2841,7 +2872,11 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             fprintf(stderr, "  median tile %d: %.0f cycles span %d chunks %d points %d\n", t50, tot[P.n_tiles / 2].first,
                     tspan[t50], tch[t50 + 1] - tch[t50], cap[tch[t50 + 1]] - cap[tch[t50]]);
         } else {
-            if (n_sch <= 256)  // one round of resident workgroups whatever the register count
+            if (W.fpl)  // the point side in the tiles (one Jacobian evaluation per observation); non-tiled points' partials
+                OPL(K_SCHUR_TILE, (k_schur_tile_fpl<true>), (k_schur_tile_fpl<false>),
+                    dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, (unsigned long long*)nullptr,
+                    pp_blocks(P.n_ap - P.n_tiled_pts), W.part, W.det_tbuf, E);
+            else if (n_sch <= 256)  // one round of resident workgroups whatever the register count
                 OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true>), (k_schur_tile<false, false, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S,
                     W.rhs, (unsigned long long*)nullptr, pp_parts(P), W.part, W.det_tbuf, E);
             else
@@ -2948,7 +2983,8 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
         OPL(K_BACKSUB_EVAL, k_backsub_chunk<true>, k_backsub_chunk<false>, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
            W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     // the points' gradient max / bad partials: per point workgroup, or per Schur tile + non-tiled point workgroup
-    const int nb_pt = W.sw ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts, 1) : pp_parts(P);
+    const int nb_pt = W.sw ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts, 1)
+                           : (W.fpl ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts) : pp_parts(P));
     // the split BCR kernel's call epoch (the persistent kernel's is advanced by k_bcr_border)
     unsigned* const ep = (P.solver == 2 && W.bcr.persist >= 2) ? W.bcr.flags : nullptr;
     if (!W.comm.on()) {

@@ -865,7 +865,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
         // (+ the small-window launch's per-tile and non-tiled point partials, §3 of DESIGN)
         const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS,
-                                          (int)pl.tile_base.size() + pp_blocks(n_ap - n_tiled, 1), 1});
+                                          (int)pl.tile_base.size() + pp_blocks(n_ap - n_tiled, PP_LANES_MAX), 1});
         HIPCHECK(ctx, ctx->buf[B_CAMDATA].ensure(sizeof(double) * ((size_t)CAMDATA * std::max(nac, 1) + 16)));
         // landmark sharding: pack buffers of the envelope tiles of S, exchange scalars
         if (shard) {
@@ -1035,6 +1035,11 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             W.sw = (W.fused && !shard && P.n_tiles > 0 && n_sw <= 256 && nac <= BCR_CAMS && !(e2 && e2[0] == '0')) ? 1
                                                                                                                 : 0;
             if (e2 && e2[0] == '2') W.sw = (W.fused && !shard && P.n_tiles > 0 && n_sw <= 256) ? 1 : 0;  // A/B
+            // larger windows, opt-in (MIBA_FPL=1): the tiled points' point side in the Schur tiles. k_lin_point
+            // 48 -> 25 us at C4 but the tiles 76 -> 133 us (their per-chunk point reduction and tail run on one
+            // wave between two barriers, and the registers spill), 4140 -> 3650 LM it/s
+            const char* e3 = std::getenv("MIBA_FPL");
+            W.fpl = (W.fused && !shard && !W.det_tbuf && P.n_tiles > 0 && !W.sw && e3 && e3[0] == '1') ? 1 : 0;
             W.sw_cnt = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 2);
             W.sw_seq = 0;
             HIPCHECK(ctx, hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));

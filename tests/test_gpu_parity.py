@@ -322,3 +322,30 @@ def test_small_window_fused_schur(case, monkeypatch):
         r2 = s.solve(p.copy())
         assert s.last_prepare()["lin_path"] == 1
     assert abs(r1["final_cost"] - r2["final_cost"]) <= 1e-12 * r1["final_cost"]
+
+
+@pytest.mark.parametrize("case", ["C2", "gauge_ovf_40"])
+def test_fused_point_side_larger_windows(case, monkeypatch):
+    """The opt-in larger-window variant (MIBA_FPL=1: the tiled points' point side inside the Schur tiles, one
+    Jacobian evaluation per observation for it and M'; k_lin_point keeps the camera side and the non-tiled points)
+    against the default path and the oracle, tolerances off, 5 iterations."""
+    from miba.solver import Solver
+    if case == "C2":
+        p = synthetic.make_config("C2")
+    else:
+        p = synthetic.make_problem(40, 4000, obs_per_point=(1, 9), seed=73, fixed_cam=5, dup_frac=0.02,
+                                   bad_depth_frac=0.02, shuffle_obs=True, sensor_f32=True)
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=5, **no_tol))
+    res = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("MIBA_FPL", v)
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=5, **no_tol) as s:
+            res[v] = (s.solve(q), q)
+    (sa, qa), (sb, qb) = res["1"], res["0"]
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sb["final_cost"]
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
