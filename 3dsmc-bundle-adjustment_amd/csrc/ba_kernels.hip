@@ -939,6 +939,10 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
     __shared__ __attribute__((aligned(16))) double Mt[SCH_K * SCH_LDM];  // Mt[k][row] = M'[row][k]
     __shared__ double zeL[SCH_K];                                         // rhs row of M' when aside
     __shared__ double gL[FP ? 6 * CHUNK_PTS : 1];                         // FP: the chunk's G (phase A)
+    // FP: the chunk's point records (phase A's per-point part) and each point thread's intrinsics terms, in LDS
+    // rather than registers (the point side's registers would otherwise cost the tile its second workgroup per CU)
+    __shared__ double qL[FP ? 21 * CHUNK_PTS : 1];
+    __shared__ double kkL[FP ? 14 * CHUNK_PTS : 1];
     // FP: per-observation point sums, in M' before the chunk clears it
     static_assert(21 * CHUNK_OBS <= SCH_K * SCH_LDM, "the point sums fit M'");
     double* const psum = Mt;
@@ -1063,9 +1067,9 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
     const int n_last = P.n_adm - 1;
     // the point records: FP writes them first (through a pointer that is not __restrict__) and reads them back
     const double* pdr = FP ? E.pdata_w : pdata;
-    double fp_kk[FP ? 14 : 1], fp_gmax = 0.0, fp_bad = 0.0;  // FP: the tile's intrinsics terms, gradient max, bad
-#pragma unroll
-    for (int i = 0; i < (FP ? 14 : 1); ++i) fp_kk[i] = 0.0;
+    double fp_gmax = 0.0, fp_bad = 0.0;  // FP: the tile's points' gradient max, bad flag (point threads)
+    if constexpr (FP)
+        for (int i = tid; i < 14 * CHUNK_PTS; i += TPB) kkL[i] = 0.0;  // (first read after the first chunk's barrier)
     // level 1: observation record of this thread
     int r_ac, r_ap, r_pt;
     ObsRaw<O32> r_o;  // camera index, pixel, depth
@@ -1099,7 +1103,7 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
 #pragma unroll
             for (int k = 0; k < 6; ++k) o_G[k] = pdr[(size_t)ap * PDATA + k];
     };
-    double q_pd[(PF || FP) ? 21 : 1];
+    double q_pd[(PF && !FP) ? 21 : 1];
     auto load_pq = [&](int a0, int a1) {
         if constexpr (PF && !FP)  // (FP: the chunk's point threads compute them)
             if (tid < a1 - a0)
@@ -1154,11 +1158,11 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
                     for (int i = 0; i < 21; ++i) acc[i] += psum[i * CHUNK_OBS + q];
                 point_tail(P, c, radius, scale, ap, Xp, acc, true, rec, kkt, fp_gmax, fp_bad);
 #pragma unroll
-                for (int i = 0; i < 14; ++i) fp_kk[i] += kkt[i];
+                for (int i = 0; i < 14; ++i) kkL[14 * tid + i] += kkt[i];
 #pragma unroll
                 for (int i = 0; i < PDATA; ++i) E.pdata_w[(size_t)ap * PDATA + i] = rec[i];
 #pragma unroll
-                for (int i = 0; i < 21; ++i) q_pd[i] = rec[i];
+                for (int i = 0; i < 21; ++i) qL[21 * tid + i] = rec[i];
 #pragma unroll
                 for (int k = 0; k < 6; ++k) gL[6 * tid + k] = rec[k];
             }
@@ -1177,7 +1181,7 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
         SCH_STAMP(0);
         // ---- phase A
         if (tid < npts) {
-            const double* pd = (PF || FP) ? q_pd : pdr + (size_t)(apb + tid) * PDATA;
+            const double* pd = FP ? qL + 21 * tid : (PF ? q_pd : pdr + (size_t)(apb + tid) * PDATA);
             double G[6], Ks[12], es[3], zk[12], z3[3];
 #pragma unroll
             for (int i = 0; i < 6; ++i) G[i] = pd[i];
@@ -1361,6 +1365,9 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
         // (tid < CHUNK_PTS: wave 0) hold any, so wave 0 reduces them alone, without a workgroup barrier
         static_assert(CHUNK_PTS <= 64, "the point threads are wave 0's");
         if (wave == 0) {
+            double fp_kk[14];
+#pragma unroll
+            for (int i = 0; i < 14; ++i) fp_kk[i] = lane < CHUNK_PTS ? kkL[14 * lane + i] : 0.0;
             wave_sum<14>(fp_kk);
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) {
