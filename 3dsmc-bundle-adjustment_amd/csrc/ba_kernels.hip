@@ -2844,6 +2844,11 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                 CK(hipMalloc(&sst, sizeof(unsigned long long) * 5 * P.n_tiles));
                 scap = P.n_tiles;
             }
+            if (W.fpl)  // (the opt-in fused point side, stamped)
+                OPL(K_SCHUR_TILE, (k_schur_tile<true, true, false, true>), (k_schur_tile<true, false, false, true>),
+                    dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, sst,
+                    pp_blocks(P.n_ap - P.n_tiled_pts), W.part, W.det_tbuf, E);
+            else
             OPL(K_SCHUR_TILE, (k_schur_tile<true, true>), (k_schur_tile<true, false>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs,
                sst, pp_parts(P), W.part, W.det_tbuf, E);
             std::vector<unsigned long long> h5((size_t)5 * P.n_tiles), h((size_t)4 * P.n_tiles);
