@@ -407,6 +407,8 @@ hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s);
 // spin bound of the resident BCR kernels' inter-workgroup waits (default 1 << 22 polls; tests force a
 // tiny bound to exercise the timeout path)
 hipError_t bcr_set_spin_limit(unsigned limit);
+// the small-window launch's wait for its camera side (ba_kernels.hip sw_wait)
+hipError_t sw_set_spin_limit(unsigned limit);
 // workgroups of k_schur_tile resident at once on the current device (CUs x blocks per CU)
 int schur_tile_slots();
 hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, double* res, double* jc, double* jp,

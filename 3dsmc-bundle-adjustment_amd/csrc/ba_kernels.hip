@@ -922,8 +922,11 @@ struct EnvArgs {
 // n_gb workgroups for the non-tiled points (point_prep_block), and the envelope tiles, which wait until the
 // camera side of this launch is counted (every workgroup of the launch is resident: the host launches FP only
 // when they fit one round). A wait that times out raises FLAG_TIMEOUT (the iteration is re-run without FP).
+// Polls before the wait gives up: sw_set_spin_limit (MIBA_BCR_SPIN_LIMIT forces the timeout path in the tests).
+__device__ unsigned g_sw_spin_limit = 1u << 20;
 __device__ __forceinline__ bool sw_wait(const unsigned* cnt, unsigned target) {
-    for (unsigned i = 0; i < (1u << 20); ++i) {
+    const unsigned lim = g_sw_spin_limit;
+    for (unsigned i = 0; i < lim; ++i) {
         if (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
         __builtin_amdgcn_s_sleep(1);
     }
@@ -3023,6 +3026,10 @@ hipError_t launch_debug_lin(const DevProblem& P, const BaConsts& c, DevWork& W, 
         else hipLaunchKernelGGL(k_debug_lin<false>, dim3(nblocks(P.n_adm, TPB)), dim3(TPB), 0, s, P, c, W.st, res, jc, jp, jk);
     }
     return hipGetLastError();
+}
+
+hipError_t sw_set_spin_limit(unsigned limit) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sw_spin_limit), &limit, sizeof(limit));
 }
 
 }  // namespace miba

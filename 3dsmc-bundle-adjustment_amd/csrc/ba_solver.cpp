@@ -108,6 +108,7 @@ struct ba_context {
     bool prepared = false;
     int n_tiles = 0, n_ovf_obs = 0, n_tiled_pts = 0;
     int n_adm_all = 0;  // admissible observations over all landmark shards
+    int sw_full = 0;    // DevWork::sw as the last full prepare chose it (a timeout re-run clears W.sw)
     int prep_nc = -1, prep_np = -1, prep_no = -1;
     int last_iter = -1;        // iterations of the last solve (ba_iteration_log rows - 1)
     // shard_min_obs: a window below the threshold is gathered onto every rank and solved there alone; the
@@ -568,7 +569,8 @@ static int upload_params(ba_context* ctx, const ba_problem* p) {
 // The MIBA_* settings ba_prepare reads (layout / solver choices): part of the plan cache key.
 static unsigned long long env_key() {
     static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
-                                        "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED"};
+                                        "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED", "MIBA_SW", "MIBA_FPL",
+                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES"};
     unsigned long long h = 1469598103934665603ull;
     for (const char* n : names) {
         const char* v = std::getenv(n);
@@ -594,6 +596,23 @@ static int bcr_setup(ba_context* ctx) {
     }
     ctx->bcr_fallback = false;
     return bcr_init_handoffs(ctx);
+}
+
+// The cost constants of the window (weights, Huber scales, LM diagonal bounds) from the context's options and N.
+// Every prepare sets them, the plan-cache reuse path included: ba_set_options may change a weight or a Huber
+// scale between two solves of one window structure.
+static void set_consts(ba_context* ctx) {
+    const ba_options& o = ctx->opts;
+    BaConsts& C = ctx->C;
+    // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
+    // and the window reduces to the IntrinsicsPrior block, :236-241)
+    const double N = (double)std::max(ctx->n_adm_all, 1);
+    C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
+    C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
+    C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
+    C.a_r = o.hub_p_repr; C.b_r = o.hub_p_repr * o.hub_p_repr;
+    C.a_d = o.hub_p_unpr; C.b_d = o.hub_p_unpr * o.hub_p_unpr;
+    C.min_diag = o.min_lm_diagonal; C.max_diag = o.max_lm_diagonal;
 }
 
 // Plan cache: the window has the structure of the last full prepare (sizes, gauge, deterministic option and layout
@@ -655,6 +674,10 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * P.part_stride, s));
     if (P.solver == 2 && ctx->bcr_fallback)
         if (int rc = bcr_setup(ctx)) return rc;
+    // a hand-off timeout cleared the small-window launch for the rest of that solve: the next one takes the path
+    // the full prepare chose again (no sticky fallback)
+    ctx->W.sw = ctx->sw_full;
+    set_consts(ctx);
     ctx->pinfo.plan_reused = 1;
     ctx->pinfo.obs_uploaded = any_vals ? 1 : 0;
     ctx->pinfo.upload_ms = now_ms() - tu;
@@ -1044,17 +1067,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             W.sw_seq = 0;
             HIPCHECK(ctx, hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));
         }
-        BaConsts& C = ctx->C;
         ctx->n_adm_all = n_adm_all;
-        // all shards' admissible observations (N = 0: no observation block exists, so the 1/N weights are unused
-        // and the window reduces to the IntrinsicsPrior block, :236-241)
-        const double N = (double)std::max(n_adm_all, 1);
-        C.sw_r = std::sqrt(1.0 / N);             // ReprojectionConstraint weight 1/N (:280)
-        C.sw_d = std::sqrt(o.weight_unpr / N);   // DepthPrior WEIGHT_UNPR/N (:290)
-        C.sw_k = std::sqrt(o.weight_intrinsics); // IntrinsicsPrior (:238)
-        C.a_r = o.hub_p_repr; C.b_r = o.hub_p_repr * o.hub_p_repr;
-        C.a_d = o.hub_p_unpr; C.b_d = o.hub_p_unpr * o.hub_p_unpr;
-        C.min_diag = o.min_lm_diagonal; C.max_diag = o.max_lm_diagonal;
+        ctx->sw_full = W.sw;
+        set_consts(ctx);
         ctx->nblk_pt = nblk_pt;
         ctx->prepared = true;
         ctx->prep_nc = nc; ctx->prep_np = np; ctx->prep_no = no;
@@ -1203,13 +1218,16 @@ static void print_row(int it, double cost, double dc, double g, double st, doubl
 static int apply_spin_limit(ba_context* ctx) {
     static std::mutex mu;
     static std::vector<unsigned> applied;  // per device; 0 = not yet set
-    const char* e = std::getenv("MIBA_BCR_SPIN_LIMIT");  // tests: force the hand-off timeout path
+    // tests: force the hand-off timeout path of the resident BCR kernels and of the small-window launch's wait
+    const char* e = std::getenv("MIBA_BCR_SPIN_LIMIT");
     unsigned want = e ? (unsigned)std::strtoul(e, nullptr, 10) : (1u << 22);
     if (want == 0) want = 1;
+    const unsigned want_sw = e ? want : (1u << 20);
     std::lock_guard<std::mutex> lock(mu);
     if ((int)applied.size() <= ctx->device) applied.resize(ctx->device + 1, 0u);
     if (applied[ctx->device] != want) {
         HIPCHECK(ctx, bcr_set_spin_limit(want));
+        HIPCHECK(ctx, sw_set_spin_limit(want_sw));
         applied[ctx->device] = want;
     }
     return BA_OK;

@@ -19,7 +19,9 @@ start; MIBA_BENCH_WARM_EACH=0 turns it off): the host-side prepare leaves the
 GPU idle for ~20 ms, and without it the timed solve runs ~3.5 % slower while
 the clocks ramp back up (profiles/r02_bench_c4_warm_ab.txt).
 
---gpus N (torchrun, one rank per GPU, RCCL over xGMI): strong scaling of ONE
+--gpus N (one rank per GPU, RCCL over xGMI; under torchrun WORLD_SIZE must equal N, and without a launcher
+bench.py starts the N rank processes itself, after checking that N devices are visible — it refuses, exit 2, rather
+than report a smaller run as an N-GPU number): strong scaling of ONE
 window: the BASELINE window's landmarks are split N ways (miba.shard.
 split_landmarks, balanced by observation count), every rank holds the cameras
 and its landmark block, and per LM iteration the ranks all-reduce the camera-side
@@ -62,7 +64,9 @@ NO_TOL = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_toleranc
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each). Under torchrun it must equal WORLD_SIZE; without a launcher and N > 1 "
+                         "bench.py starts the N rank processes itself (one per visible device)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4", choices=["C1", "C2", "C3", "C4", "C5"])
@@ -280,9 +284,86 @@ def latency_bench(args):
     print(json.dumps(out), flush=True)
 
 
+def rank_plan(gpus, latency, env, n_visible, argv, port):
+    """What this process does for `--gpus`: ("run", None) — this process is the one rank of a 1-GPU run or one
+    rank of an outside launcher (torchrun) whose WORLD_SIZE agrees; ("spawn", [(cmd, env), ...]) — start N rank
+    processes (no outside launcher, N > 1); ("error", message) — a world-size mismatch, too few visible devices or
+    a config that does not shard. Decided before anything touches the GPU (the parent never initialises HIP)."""
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        w = int(world)
+        if gpus is not None and gpus != w:
+            return "error", f"--gpus {gpus} disagrees with WORLD_SIZE={w} set by the launcher"
+        if w > 1 and latency:
+            return "error", "--config C1 / C3 is the single-GPU latency bench (TUM-size windows are never sharded)"
+        return "run", None
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        return "error", f"--gpus {n}: need at least one GPU"
+    if n == 1:
+        return "run", None
+    if latency:
+        return "error", "--config C1 / C3 is the single-GPU latency bench (TUM-size windows are never sharded)"
+    if n_visible < n:
+        return "error", f"--gpus {n} but only {n_visible} HIP device(s) visible: refusing to report a {n}-GPU number"
+    procs = []
+    for r in range(n):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(([sys.executable, os.path.abspath(__file__)] + list(argv), e))
+    return "spawn", procs
+
+
+def spawn_ranks(procs) -> int:
+    """Run the rank processes (rank 0's stdout is the bench line); a failed rank ends the others."""
+    import subprocess
+    ps = [subprocess.Popen(cmd, env=env, stdout=None if r == 0 else subprocess.DEVNULL)
+          for r, (cmd, env) in enumerate(procs)]
+    rc = 0
+    try:
+        pending = set(range(len(ps)))
+        while pending:
+            for r in list(pending):
+                c = ps[r].poll()
+                if c is None:
+                    continue
+                pending.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c
+                    print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    for q in pending:
+                        ps[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
 def main():
     args = parse()
-    if args.config in ("C1", "C3") and not args.problem:
+    latency = args.config in ("C1", "C3") and not args.problem
+    if os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
+        import torch  # device_count() does not initialise the GPU on this image; nothing else is touched here
+        kind, what = rank_plan(args.gpus, latency, os.environ, torch.cuda.device_count(), sys.argv[1:], free_port())
+    else:
+        kind, what = rank_plan(args.gpus, latency, os.environ, 0, sys.argv[1:], 0)
+    if kind == "error":
+        print(f"bench.py: {what}", file=sys.stderr)
+        raise SystemExit(2)
+    if kind == "spawn":
+        raise SystemExit(spawn_ranks(what))
+    if latency:
         return latency_bench(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -97,6 +97,37 @@ def test_bcr_handoff_timeout_reruns_the_iteration_in_the_same_solve(monkeypatch)
     assert abs(sg3["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
 
 
+def test_one_block_window_timeout_reruns_and_restores_the_small_window_path(monkeypatch):
+    """ADVICE r4 (medium / low): the default one-block path (k_bcr_dense1 + the small-window fused Schur launch,
+    whose envelope tiles wait for the launch's camera side) under a forced one-poll spin bound. The wait times
+    out, the iteration re-runs with the per-level launches and the two-launch linearisation inside the same
+    solve (BA_OK, oracle parity); the next solve of the same window (plan cache) takes the one-block path again."""
+    p = synthetic.make_config("C1")
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=8))
+    with _solver(max_num_iterations=8) as s:
+        s.solve(p.copy())
+        info0 = s.last_prepare()
+        assert info0["bcr_path"] == 4 and info0["lin_path"] == 1, info0
+        monkeypatch.setenv("MIBA_BCR_SPIN_LIMIT", "1")
+        q = p.copy()
+        sg = s.solve(q)
+        note = s.last_error()
+        monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
+        q2 = p.copy()
+        sg2 = s.solve(q2)
+        info2 = s.last_prepare()
+        note2 = s.last_error()
+    assert "re-run with the per-level BCR launches" in note, note
+    assert info2["plan_reused"] == 1 and info2["bcr_path"] == 4 and info2["lin_path"] == 1, info2
+    assert note2 == "", note2
+    for g in (sg, sg2):
+        assert g["termination"] == so["termination"], (g, so)
+        assert g["num_iterations"] == so["num_iterations"]
+        assert g["num_successful_steps"] == so["num_successful_steps"]
+        assert abs(g["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (g, so)
+    np.testing.assert_allclose(q.cams, q2.cams, rtol=0, atol=1e-10)
+
+
 def test_two_contexts_solve_concurrently_on_one_gpu():
     """Two host threads, one context each, solving C2 windows at the same time on GPU 0: both resident BCR
     grids and every other launch share the device; both solves return BA_OK and match the oracle."""

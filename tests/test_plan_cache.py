@@ -162,3 +162,26 @@ def test_prepare_then_solve_prepared_on_a_reused_plan():
         log = s.iteration_log()
     assert info["plan_reused"] == 1 and info["total_ms"] > 0
     _same((q, sm, log), _fresh(p, iters=5))
+
+
+@pytest.mark.parametrize("change", [dict(weight_unpr=3.0), dict(hub_p_repr=2e-3, hub_p_unpr=5e-4),
+                                    dict(weight_intrinsics=1e-4), dict(min_lm_diagonal=1e-2)],
+                         ids=["weight_unpr", "huber", "weight_intrinsics", "min_lm_diagonal"])
+def test_changed_cost_options_on_a_reused_plan(change):
+    """the plan cache keys the structure only, so the cost constants (weights, Huber scales, LM
+    diagonal bounds) must follow ba_set_options on the reuse path: solve, change an option, solve the same window
+    again (plan reused) and compare with a fresh context that starts with the changed options."""
+    p = _prob("shuffled_bad_depth")
+    with _solver(max_num_iterations=6, deterministic=1, **NO_TOL) as s:
+        s.solve(p.copy())
+        s.set_options(**change)
+        q = p.copy()
+        sm = s.solve(q)
+        info = s.last_prepare()
+        log = s.iteration_log()
+    assert info["plan_reused"] == 1, info
+    fresh = _fresh(p, **change)
+    _same((q, sm, log), fresh)
+    # and the change did matter (the old constants would have given another solve)
+    base = _fresh(p)
+    assert not np.array_equal(base[2], fresh[2]), "the option change did not change the solve"
