@@ -32,6 +32,7 @@
 
 #include "ba_device.h"
 #include "ba_kernels.h"
+#include "ba_solve_util.h"
 
 namespace miba {
 
@@ -50,10 +51,6 @@ static constexpr int RSZ = BB * RC;
 static constexpr int NCONTRIB_WG = 11;  // 44 contribution tiles / 4 waves
 typedef double d4b __attribute__((ext_vector_type(4)));
 
-// chol_flag is raised by several workgroups at once: fetch-or, so a timeout is never overwritten
-__device__ __forceinline__ void raise_flag(int* flag, int bit) {
-    __hip_atomic_fetch_or(flag, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Diagnostic phase stamps (MIBA_BCR_STAMPS=1 launches the STAMP=true variants).
 __device__ __forceinline__ unsigned long long bcr_stamp() {
@@ -71,17 +68,6 @@ __device__ __forceinline__ unsigned long long bcr_stamp() {
         }                                                                                        \
     } while (0)
 
-__device__ __forceinline__ unsigned long long realtime_now() {
-    unsigned long long t;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-__device__ __forceinline__ double bcast_b(double v, int l) {
-    const unsigned long long u = __double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
 // 1/sqrt(x): v_rsq_f64 (~2^-24) + one Newton step in FMA form (rel. error ~4e-15,
 // measured by tools/rsq_f64_check.hip) — three dependent f64 ops on the pivot path.
 __device__ __forceinline__ double rsqrt_1nr(double x) {
@@ -814,43 +800,6 @@ __global__ __launch_bounds__(TPB_C) void k_bcr_back(const LmState* __restrict__ 
 // step of its cameras (was k_update_cams): lanes < BCR_CAMS, workgroup 0 also the intrinsics; one
 // partial per workgroup of the step scalars for k_final. PUB: inside k_bcr_split, after every
 // block's back-substitution flag, so Bp and Y are read with sc1 loads; bk = [b_k | S_kk packed].
-// 4x4 border system (C - sum B^T V) y_k = b_k - sum B^T u on one thread: bk = [b_k | S_kk lower packed],
-// red[m * 5 + c] = (B^T [u | V])[m][c]. bad: a non-positive pivot (replaced by 1).
-__device__ __forceinline__ void border_solve4(const double* bk, const double* red, double* yk, bool& bad) {
-    double Cm[16], bp[4];
-    int q = 0;
-    for (int mm = 0; mm < 4; ++mm)
-        for (int l = 0; l <= mm; ++l, ++q) {
-            const double v = bk[4 + q];
-            Cm[mm * 4 + l] = v - red[mm * 5 + 1 + l];
-            Cm[l * 4 + mm] = v - red[l * 5 + 1 + mm];
-        }
-    for (int mm = 0; mm < 4; ++mm) bp[mm] = bk[mm] - red[mm * 5];
-    double Lm[16] = {0};
-    for (int j = 0; j < 4; ++j) {
-        double d = Cm[j * 4 + j];
-        for (int k = 0; k < j; ++k) d -= Lm[j * 4 + k] * Lm[j * 4 + k];
-        if (!(d > 0.0)) { bad = true; d = 1.0; }
-        Lm[j * 4 + j] = sqrt(d);
-        for (int r = j + 1; r < 4; ++r) {
-            double v = Cm[r * 4 + j];
-            for (int k = 0; k < j; ++k) v -= Lm[r * 4 + k] * Lm[j * 4 + k];
-            Lm[r * 4 + j] = v / Lm[j * 4 + j];
-        }
-    }
-    double z[4];
-    for (int r = 0; r < 4; ++r) {
-        double v = bp[r];
-        for (int k = 0; k < r; ++k) v -= Lm[r * 4 + k] * z[k];
-        z[r] = v / Lm[r * 4 + r];
-    }
-    for (int r = 3; r >= 0; --r) {
-        double v = z[r];
-        for (int k = r + 1; k < 4; ++k) v -= Lm[k * 4 + r] * z[k];
-        z[r] = v / Lm[r * 4 + r];
-    }
-    for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
-}
 
 static constexpr int TPB_BD = 64;
 static constexpr int BP_CHUNK = 32;  // blocks' border partials (20 doubles) / Grams (25) staged in LDS per round
@@ -2602,6 +2551,7 @@ int bcr_persist_ok(int nblk) {
 }
 
 hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s, Prof* pf) {
+    if (Bw.band) return launch_bcr_band(P, c, W, Bw.band, s, pf);  // narrow band: one workgroup (ba_band.hip)
     if (Bw.dense1) {  // one-block window: the dense single-workgroup solve (bcr_dense1_ok)
         static unsigned long long* dst = nullptr;
         static int dmode = -1;

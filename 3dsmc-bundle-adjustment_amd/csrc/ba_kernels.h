@@ -139,6 +139,8 @@ struct BcrWork {
                   // helper (k_bcr_split<.., 1>), 1 = one resident workgroup per block (k_bcr_persist),
                   // 0 = one launch per level
     int dense1;   // one-block window solved by k_bcr_dense1 (bcr_dense1_ok)
+    int band;     // narrow-band window solved in one workgroup by k_bcr_band (ba_band.hip): cameras per block
+                  // (1..3 = max(camera band, 1)), 0 = off (bcr_band_ok)
 };
 // k_bcr_split's flag-free back-substitution hand-off: y rows double-buffered by epoch parity (Y even,
 // Racc odd — Racc belongs to the per-level path only); an empty slot holds this signalling-NaN pattern,
@@ -402,6 +404,9 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);
 int bcr_dense1_ok(int nblk, int kb);
+// cameras per block of the one-workgroup band solve for this window (0: not eligible; MIBA_BCR_BAND)
+int bcr_band_ok(int nac, int cam_band, int kb);
+hipError_t launch_bcr_band(const DevProblem& P, const BaConsts& c, DevWork& W, int bc, hipStream_t s, Prof* pf);
 // k_bcr_split's pull slots: empty (split = true, Bw.persist >= 2) or zero (the per-level / persistent paths)
 hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s);
 // spin bound of the resident BCR kernels' inter-workgroup waits (default 1 << 22 polls; tests force a

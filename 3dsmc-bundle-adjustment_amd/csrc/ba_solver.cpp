@@ -584,11 +584,15 @@ static unsigned long long env_key() {
 // zero), the resident path probed (bcr_persist_ok; MIBA_BCR overrides), the hand-off state initialised. Every
 // full prepare probes again, also after a hand-off timeout moved the last window to the per-level launches
 // (ba_prepare_info.bcr_path reports the path).
+// ba_prepare_info.bcr_path of the reduced-solve path (include/ba.h)
+static int bcr_path_id(const BcrWork& Bw) { return Bw.band ? 5 : Bw.dense1 ? 4 : Bw.persist; }
+
 static int bcr_setup(ba_context* ctx) {
     BcrWork& Bw = ctx->W.bcr;
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, ctx->buf[B_BCR].cap, ctx->stream));
     Bw.persist = bcr_persist_ok(Bw.nblk);
     Bw.dense1 = bcr_dense1_ok(Bw.nblk, ctx->P.kb);
+    Bw.band = bcr_band_ok(ctx->P.nac, ctx->P.cam_band, ctx->P.kb);
     if (const char* e = std::getenv("MIBA_BCR")) {
         if (!std::strcmp(e, "launch")) Bw.persist = 0;
         else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
@@ -681,7 +685,7 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     ctx->pinfo.plan_reused = 1;
     ctx->pinfo.obs_uploaded = any_vals ? 1 : 0;
     ctx->pinfo.upload_ms = now_ms() - tu;
-    ctx->pinfo.bcr_path = P.solver == 2 ? (ctx->W.bcr.dense1 ? 4 : ctx->W.bcr.persist) : -1;
+    ctx->pinfo.bcr_path = P.solver == 2 ? bcr_path_id(ctx->W.bcr) : -1;
     ctx->pinfo.lin_path = ctx->W.sw;
     ctx->prepared = true;
     ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;
@@ -1152,7 +1156,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->pinfo.plan_ms = tp_plan - tp_raw;
         ctx->pinfo.upload_ms = (tp_raw - tp0) + (now_ms() - tp_plan);
         ctx->pinfo.obs_uploaded = 1;
-        ctx->pinfo.bcr_path = P.solver == 2 ? (ctx->W.bcr.dense1 ? 4 : ctx->W.bcr.persist) : -1;
+        ctx->pinfo.bcr_path = P.solver == 2 ? bcr_path_id(ctx->W.bcr) : -1;
         ctx->pinfo.lin_path = ctx->W.sw;
         return BA_OK;
     };
@@ -1602,7 +1606,8 @@ extern "C" int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, i
     for (int k = 0; k < K_COUNT && n < max_n; ++k, ++n) {
         std::memset(&out[n], 0, sizeof(ba_kernel_stat));
         // the resident BCR id times whichever resident kernel the window runs: name it after that kernel
-        const char* nm = (k == K_BCR_PERSIST && ctx->W.bcr.dense1) ? "bcr_dense1"
+        const char* nm = (k == K_BCR_PERSIST && ctx->W.bcr.band) ? "bcr_band"
+                         : (k == K_BCR_PERSIST && ctx->W.bcr.dense1) ? "bcr_dense1"
                          : (k == K_BCR_PERSIST && ctx->W.bcr.persist >= 2) ? "bcr_split" : kKernelNames[k];
         std::snprintf(out[n].name, sizeof(out[n].name), "%s", nm);
         out[n].launches = ctx->k_launches[k];

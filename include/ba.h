@@ -186,7 +186,8 @@ typedef struct ba_prepare_info {
     int32_t obs_uploaded;    /* 1: observation values were uploaded (always on a rebuild; on a reuse only when
                                 some pixel / depth value changed) */
     int32_t host_threads;    /* host plan threads (MIBA_HOST_THREADS, else min(16, OMP_NUM_THREADS, affinity)) */
-    int32_t bcr_path;        /* reduced-solve path of the prepared window: 4 = one-block window, dense
+    int32_t bcr_path;        /* reduced-solve path of the prepared window: 5 = narrow camera band (<= 3), the
+                                whole system cyclic-reduced in one workgroup's LDS; 4 = one-block window, dense
                                 single-workgroup solve; 3 / 2 = resident split kernel with two / one helper
                                 workgroups per block, 1 = resident one-workgroup kernel, 0 = per-level launches,
                                 -1 = not the block cyclic reduction (band / dense) */

@@ -349,3 +349,80 @@ def test_fused_point_side_larger_windows(case, monkeypatch):
     assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
     np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
     np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
+
+
+BAND_CASES = {
+    # the reference's sliding window: camera_band 1 (every landmark on two consecutive keyframes)
+    "C3": (lambda: synthetic.make_config("C3"), 1),
+    # landmark tracks of 2-3 / 2-4 keyframes: camera_band 2 / 3 (blocks of 12 / 18 dofs)
+    "band2": (lambda: synthetic.make_problem(50, 4000, obs_per_point=(2, 3), seed=31, sensor_f32=True), 2),
+    "band3": (lambda: synthetic.make_problem(50, 4000, obs_per_point=(2, 4), seed=32, sensor_f32=True), 3),
+    # gauge in the middle, shuffled, inadmissible depths, duplicate links (overflow points), a partial last block
+    "gauge_mid_dup": (lambda: synthetic.make_problem(37, 2600, obs_per_point=(1, 3), seed=33, fixed_cam=17,
+                                                     dup_frac=0.02, bad_depth_frac=0.02, shuffle_obs=True,
+                                                     sensor_f32=True), 2),
+    # 100 keyframes: more eliminated blocks at level 0 than half-waves (two rounds), 7 levels
+    "long100": (lambda: synthetic.make_problem(100, 6000, obs_per_point=(2, 2), seed=34, sensor_f32=True), 1),
+    # the f64 observation layout
+    "f64_band1": (lambda: synthetic.make_problem(21, 1500, obs_per_point=(2, 2), seed=35), 1),
+}
+
+
+@pytest.mark.parametrize("case", sorted(BAND_CASES))
+def test_band_one_workgroup_solve(case, monkeypatch):
+    """Narrow-band windows (camera band <= 3, more than one 64-dof BCR block) take the one-workgroup cyclic
+    reduction (ba_prepare_info.bcr_path 5, ba_band.hip): against the split BCR kernel (MIBA_BCR_BAND=0) and the
+    oracle, tolerances off, 6 iterations; a deterministic repeat is bitwise identical."""
+    from miba.solver import Solver
+    make, band = BAND_CASES[case]
+    p = make()
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MIBA_BCR_BAND", mode)
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
+            res[mode] = (s.solve(q), q)
+            info = s.last_prepare()
+        assert (info["bcr_path"] == 5) == (mode == "1"), (mode, info)
+    (sa, qa), (sb, qb) = res["1"], res["0"]
+    assert sa["camera_band"] == band, sa
+    assert sa["linear_solver"] == sb["linear_solver"] == LS["bcr"]
+    assert sa["num_iterations"] == sb["num_iterations"] == 6
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sb["final_cost"], (sa, sb)
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sa, so)
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(qa.intr, qb.intr, rtol=1e-9)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-7)
+    monkeypatch.setenv("MIBA_BCR_BAND", "1")
+    outs = []
+    for _ in range(2):
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, deterministic=1, **no_tol) as s:
+            outs.append((s.solve(q)["final_cost"], q))
+    assert outs[0][0] == outs[1][0]
+    np.testing.assert_array_equal(outs[0][1].cams, outs[1][1].cams)
+
+
+def test_band_solve_on_one_block_windows(monkeypatch):
+    """MIBA_BCR_BAND=2: the band solve also on a one-block window (C1, beside the small-window Schur launch)
+    against k_bcr_dense1 and the oracle."""
+    from miba.solver import Solver
+    p = synthetic.make_config("C1")
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
+    res = {}
+    for mode, path in (("2", 5), ("1", 4)):
+        monkeypatch.setenv("MIBA_BCR_BAND", mode)
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
+            res[mode] = (s.solve(q), q)
+            info = s.last_prepare()
+        assert info["bcr_path"] == path and info["lin_path"] == 1, (mode, info)
+    (sa, qa), (sb, qb) = res["2"], res["1"]
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sb["final_cost"]
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-8)
