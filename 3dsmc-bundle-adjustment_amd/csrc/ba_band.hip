@@ -34,6 +34,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "ba_device.h"
 #include "ba_kernels.h"
@@ -41,19 +42,13 @@
 
 namespace miba {
 
-// workgroup size: 16 waves (32 half-wave block units) for blocks of one camera; 8 waves for blocks of 2-3 cameras
-// (half as many blocks, and the wider blocks' pivot rows / triangular solves need the 256-VGPR budget of 2 waves
-// per SIMD: at 4 waves per SIMD they spill 420 / 1280 B per lane)
-template <int BC>
-struct BandTpb {
-    static constexpr int TPB = BC == 1 ? 1024 : 512;
-    static constexpr int NW = TPB / 64;
-};
+// one workgroup of 8 waves (2 per SIMD: the 256-VGPR budget; at 16 waves the kernel spilled, and the element-parallel
+// phases are issue-bound, so more waves per SIMD add nothing)
+static constexpr int BAND_TPB = 512;
 static constexpr int BAND_OPS = 25;    // staged camera-step operands per active camera: sc 6 | ud 6 | g 6 | x 7
 static constexpr int BAND_IOPS = 20;   // intrinsics: K 4 | sk 4 | uk 4 | gk 4 | prior 4
-static constexpr int BAND_GR = 16;     // per-block border Gram slot (14 used)
-static constexpr int BAND_NL = 8;      // loads in flight per thread in the load phase
 static constexpr int BAND_STAMPS = 24;
+static constexpr int BAND_FSTAMPS = 8 * 8;  // STAMP: inside each level's factor phase, unit 0 of wave 0
 
 // LDS layout (doubles) of one window: per block j (nb blocks of G dofs, block-major = dof order)
 //   D  G x G   diagonal block, then L_j (lower; upper zero) once j is eliminated
@@ -61,11 +56,10 @@ static constexpr int BAND_STAMPS = 24;
 //   XR G x G   XR_j
 //   BB G x 4   border rows B_j, then XB_j
 //   BV G       rhs b_j, then x_j;   RI G   1 / diag(L_j);   YV G   y_j
-//   GR 16      border Gram of block j
 // then bk = [b_k | S_kk lower packed] (14) | red (20) | y_k (4), the intrinsics' and cameras' step operands and
 // the active cameras' indices (ints, two per double).
 struct BandLayout {
-    int D, CL, XR, BB, BV, RI, YV, GR, BK, RED, YK, IOPS, OPS, AC, total;
+    int D, CL, XR, BB, BV, RI, YV, BK, RED, YK, IOPS, OPS, AC, ST, total;
 };
 __host__ __device__ inline BandLayout band_layout(int G, int nb, int nac) {
     BandLayout L;
@@ -77,13 +71,13 @@ __host__ __device__ inline BandLayout band_layout(int G, int nb, int nac) {
     L.BV = o;   o += nb * G;
     L.RI = o;   o += nb * G;
     L.YV = o;   o += nb * G;
-    L.GR = o;   o += nb * BAND_GR;
     L.BK = o;   o += 16;
     L.RED = o;  o += 24;
     L.YK = o;   o += 8;
     L.IOPS = o; o += BAND_IOPS;
     L.OPS = o;  o += nac * BAND_OPS;
     L.AC = o;   o += (nac + 1) / 2 + 1;
+    L.ST = o;   o += BAND_STAMPS + BAND_FSTAMPS;
     L.total = o;
     return L;
 }
@@ -92,6 +86,82 @@ __host__ __device__ inline BandLayout band_layout(int G, int nb, int nac) {
 __device__ __forceinline__ double bcast_half(double v, int j, bool hi) {
     const double lo = bcast_b(v, j), up = bcast_b(v, 32 + j);
     return hi ? up : lo;
+}
+// A block's rows live on one unit of U lanes: a 16-lane DPP row when the block has <= 16 dofs (four blocks per wave;
+// the broadcast of lane J to its row is one v_mov_b32_dpp row_newbcast per dword, gfx90a+), else a half-wave
+// (v_readlane pairs and a select — on the chain that costs ~2x the DPP move, measured)
+template <int G>
+struct BandUnit {
+    static constexpr int U = G <= 16 ? 16 : 32;
+    static constexpr int PER_WAVE = 64 / U;
+};
+template <int U, int J>
+__device__ __forceinline__ double ubc(double v, bool hi) {
+    if constexpr (U == 16) {
+        const unsigned long long u = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x150 + J, 0xF, 0xF, false);
+        const int up = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x150 + J, 0xF, 0xF, false);
+        return __longlong_as_double((long long)(((unsigned long long)(unsigned)up << 32) | (unsigned)lo));
+    } else {
+        return bcast_half(v, J, hi);
+    }
+}
+// compile-time loop (the DPP lane select is an immediate)
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+// 4x4 border system as border_solve4 (bk = [b_k | S_kk lower packed], red[m * 5 + c] = (B^T [u | V])[m][c]), the
+// Cholesky pivots by v_rsq_f64 + one Newton step and the solves by products: no square root or division on the path
+// (border_solve4's IEEE square roots and divisions took ~1.5 us here). bad: a non-positive pivot.
+__device__ __forceinline__ void border_solve4_rsq(const double* bk, const double* red, double* yk, bool& bad) {
+    double Cm[16], bp[4];
+    int q = 0;
+    for (int mm = 0; mm < 4; ++mm)
+        for (int l = 0; l <= mm; ++l, ++q) {
+            const double v = bk[4 + q];
+            Cm[mm * 4 + l] = v - red[mm * 5 + 1 + l];
+        }
+    for (int mm = 0; mm < 4; ++mm) bp[mm] = bk[mm] - red[mm * 5];
+    double Lm[16] = {0}, ri[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double d = Cm[j * 4 + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) d = __builtin_fma(-Lm[j * 4 + k], Lm[j * 4 + k], d);
+        if (!(d > 0.0 && d < INFINITY)) { bad = true; d = 1.0; }
+        const double y = __builtin_amdgcn_rsq(d);
+        const double ee = __builtin_fma(-d * y, y, 1.0);
+        const double yi = __builtin_fma(0.5 * y, ee, y);  // 1 / L_jj
+        ri[j] = yi;
+        Lm[j * 4 + j] = d * yi;
+#pragma unroll
+        for (int r = j + 1; r < 4; ++r) {
+            double v = Cm[r * 4 + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v = __builtin_fma(-Lm[r * 4 + k], Lm[j * 4 + k], v);
+            Lm[r * 4 + j] = v * yi;
+        }
+    }
+    double z[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double v = bp[r];
+#pragma unroll
+        for (int k = 0; k < r; ++k) v = __builtin_fma(-Lm[r * 4 + k], z[k], v);
+        z[r] = v * ri[r];
+    }
+#pragma unroll
+    for (int r = 3; r >= 0; --r) {
+        double v = z[r];
+#pragma unroll
+        for (int k = r + 1; k < 4; ++k) v = __builtin_fma(-Lm[k * 4 + r], z[k], v);
+        z[r] = v * ri[r];
+    }
+    for (int mm = 0; mm < 4; ++mm) yk[mm] = z[mm];
 }
 // wide blocks (G = 18): a compiler barrier between the steps of an unrolled triangular solve keeps the compiler
 // from hoisting every LDS operand of the solve into registers at once (752 B per lane of spills without it)
@@ -104,8 +174,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Operands of one output element of a survivor update (decoded once per thread, before the level loop): the element
+// is dest = (keep ? dest : 0) - sum_u a1[u G] b1[u bs] - [second source] sum_u a2[u G] b2[u bs], a1 / a2 the column r
+// of XR_i1 / XL_i2; b1 / b2 a column of one of the block arrays at the blocks i1 / i2 (stride bblk per block); dest
+// in the survivor's block, mirrored for the diagonal block's upper half.
+struct BandItem {
+    int ok, r, b1_arr, b2_arr, boff, bs, dst_arr, doff, mirror, two, keep;
+};
+
 template <int BC, bool STAMP>
-__global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __restrict__ st, DevProblem P,
+__global__ __launch_bounds__(BAND_TPB) void k_bcr_band(const LmState* __restrict__ st, DevProblem P,
                                                        const double* __restrict__ S, double* __restrict__ rhs,
                                                        int* __restrict__ flag, BaConsts c,
                                                        const double* __restrict__ scale,
@@ -115,11 +193,18 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
                                                        unsigned long long* __restrict__ tl) {
     constexpr int G = 6 * BC;
     constexpr int GG = G * G;
-    constexpr int TPB_BAND = BandTpb<BC>::TPB, NW_BAND = BandTpb<BC>::NW;
+    constexpr int TPB = BAND_TPB, NW = BAND_TPB / 64;
     constexpr int NCOL = 2 * G + 5;  // [XL | XR | x | XB] columns of the forward solve
+    constexpr int U = BandUnit<G>::U, UPW = BandUnit<G>::PER_WAVE;
+    constexpr bool FUSE = G == 6;  // the forward solve inside the factor unit (blocks of one camera)
+    constexpr int ND = G * (G + 1) / 2;
+    constexpr int NSI = ND + G + 4 * G + GG;      // output elements per survivor: D lower | b | B | fill
+    constexpr int NQ = (NSI + TPB - 1) / TPB;     // elements per thread and survivor
+    constexpr int GRP = NSI <= TPB ? TPB / NSI : 1;  // survivors per pass
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool hi = lane >= 32;
+    const int ul = lane & (U - 1);
     const int nac = P.nac, ncd = P.kb;  // active cameras, camera dofs (= 6 nac = first intrinsics row)
     const size_t ld = P.npad;
     const BandLayout Ly = band_layout(G, nb, nac);
@@ -130,103 +215,150 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
     double* const BV = lds + Ly.BV;
     double* const RI = lds + Ly.RI;
     double* const YV = lds + Ly.YV;
-    double* const GR = lds + Ly.GR;
     int* const AC = reinterpret_cast<int*>(lds + Ly.AC);
+    // STAMP: s_memrealtime after each phase, kept in LDS until the end (a global store before a barrier would make
+    // the barrier's workgroup fence wait for its acknowledgement)
+    unsigned long long* const stl = reinterpret_cast<unsigned long long*>(lds + Ly.ST);
     int ts = 0;
     auto stamp = [&]() {
         if constexpr (STAMP) {
             __syncthreads();
-            if (tid == 0) tl[ts] = realtime_now();
+            if (tid == 0) stl[ts] = realtime_now();
             ++ts;
         }
     };
-    if constexpr (STAMP) if (tid == 0) tl[BAND_STAMPS - 1] = realtime_now();
-    // ---- load: S blocks, border, rhs, corner and the step operands, NL loads in flight per thread (clamped
-    // addresses, selects after), the LM-state check behind them
+    if constexpr (STAMP) if (tid == 0) stl[BAND_STAMPS - 1] = realtime_now();
+    // STAMP: wave 0 lane 0 inside the factor phase of level m (no barrier): slot BAND_STAMPS + 8 m + k
+    auto fst = [&](int m, int k) {
+        if constexpr (STAMP) if (tid == 0 && m < 8) stl[BAND_STAMPS + 8 * m + k] = realtime_now();
+    };
     const bool skip = skip_step(st);
     const int cur = st->cur;
-    const int nD = nb * GG, nBB = nb * G * 4, nBV = nb * G;
-    const int e_cl = nD, e_bb = 2 * nD, e_bv = e_bb + nBB, e_bk = e_bv + nBV, e_io = e_bk + 14, e_op = e_io + BAND_IOPS;
-    const int E = e_op + 18 * nac;
-    const int acv = tid < nac ? P.ac_cam[tid] : 0;
-    for (int e0 = 0; e0 < E; e0 += TPB_BAND * BAND_NL) {
-        double v[BAND_NL];
-        int dst[BAND_NL];
+    // ---- load. Camera dof rows: one thread per row dr of block j, its 2G contiguous doubles of S row dr at columns
+    // (j - 1) G .. j G + G - 1 (the coupling A(j, j - 1) and the diagonal block's lower part; the upper part stays
+    // zero, the pivot chain reads only the lower), its border entries S[kb + k][dr] and rhs[dr]; identity past the
+    // last camera dof. Cameras: their step operands (the pose after the camera index), on the threads from the top.
+    const int nrow = nb * G;
+    {
+        // the 2G doubles of S row dr at columns (j - 1) G .. j G + G - 1, element e = 2G dr + cc: consecutive threads
+        // read consecutive columns (a thread per row read 2G lines per wave and instruction: 4.2 us at C3)
+        constexpr int NL = 8;
+        const int ne2 = nrow * 2 * G;
+        for (int e0 = 0; e0 < ne2; e0 += NL * TPB) {
+            double v[NL];
 #pragma unroll
-        for (int q = 0; q < BAND_NL; ++q) {
-            const int e = e0 + TPB_BAND * q + tid;
-            const double* p = S;
-            size_t idx = 0;
-            bool ok = false;
-            double cst = 0.0;
-            int d = -1;
-            if (e < e_cl) {  // diagonal blocks, both halves (identity past the last camera dof)
-                const int j = e / GG, r = (e / G) % G, cc = e % G;
-                const int dr = j * G + r, dc = j * G + cc;
-                ok = dr < ncd && dc < ncd;
-                idx = dr >= dc ? (size_t)dr * ld + dc : (size_t)dc * ld + dr;
-                cst = r == cc ? 1.0 : 0.0;
-                d = Ly.D + e;
-            } else if (e < e_bb) {  // couplings A(j, j - 1)
-                const int f = e - e_cl, j = f / GG, r = (f / G) % G, cc = f % G;
-                const int dr = j * G + r, dc = (j - 1) * G + cc;
-                ok = j >= 1 && dr < ncd;
-                idx = (size_t)dr * ld + dc;
-                d = Ly.CL + f;
-            } else if (e < e_bv) {  // border rows B_j (S rows kb .. kb + 3 at the block's columns)
-                const int f = e - e_bb, dr = f >> 2, k = f & 3;
-                ok = dr < ncd;
-                idx = (size_t)(ncd + k) * ld + dr;
-                d = Ly.BB + f;
-            } else if (e < e_bk) {  // rhs
-                const int dr = e - e_bv;
-                ok = dr < ncd;
-                p = rhs;
-                idx = dr;
-                d = Ly.BV + dr;
-            } else if (e < e_io) {  // bk: b_k, then S_kk lower packed
-                const int f = e - e_bk;
-                ok = true;
-                if (f < 4) {
-                    p = rhs;
-                    idx = ncd + f;
-                } else {
-                    int q2 = f - 4, mm = 0;
-                    while (q2 > mm) { q2 -= mm + 1; ++mm; }
-                    idx = (size_t)(ncd + mm) * ld + ncd + q2;
-                }
-                d = Ly.BK + f;
-            } else if (e < e_op) {  // the intrinsics' step operands (load_intr_step_ops)
-                const int f = e - e_io, kind = f >> 2, m = f & 3;
-                ok = true;
-                p = kind == 0 ? P.K[cur] : kind == 1 ? scale : kind == 4 ? P.prior : lin;
-                idx = kind == 0 ? m : kind == 1 ? P.off_k + m : kind == 2 ? 2 + 4 * m - (m * (m - 1)) / 2
-                                                              : kind == 3 ? 12 + m : m;
-                d = Ly.IOPS + f;
-            } else if (e < E) {  // the cameras' step operands (load_cam_step_ops, but the pose: below)
-                const int f = e - e_op, t = f / 18, k = f % 18;
-                ok = true;
-                p = k < 6 ? scale : camdata;
-                idx = k < 6 ? 6 * (size_t)t + k
-                            : (size_t)t * CAMDATA + (k < 12 ? (k - 6) * 6 - ((k - 6) * (k - 7)) / 2 : 45 + k - 12);
-                d = Ly.OPS + t * BAND_OPS + k;
+            for (int q = 0; q < NL; ++q) {
+                const int e = e0 + q * TPB + tid;
+                const int dr = e / (2 * G), cc = e - dr * (2 * G), j = dr / G, r = dr - j * G;
+                const int col = (j - 1) * G + cc;
+                const bool okc = e < ne2 && dr < ncd && col >= 0 && (cc < G || cc - G <= r);
+                v[q] = S[okc ? (size_t)dr * ld + col : 0];
+                v[q] = okc ? v[q] : ((e < ne2 && dr >= ncd && cc - G == r) ? 1.0 : 0.0);  // identity past the dofs
             }
-            v[q] = p[ok ? idx : 0];
-            v[q] = ok ? v[q] : cst;
-            dst[q] = d;
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int e = e0 + q * TPB + tid;
+                if (e < ne2) {
+                    const int dr = e / (2 * G), cc = e - dr * (2 * G), j = dr / G, r = dr - j * G;
+                    lds[(cc < G ? Ly.CL : Ly.D) + j * GG + r * G + (cc < G ? cc : cc - G)] = v[q];
+                }
+            }
+        }
+    }
+    for (int dr = tid; dr < nrow; dr += TPB) {  // border entries S[kb + k][dr] and rhs[dr] (coalesced over dr)
+        const bool ok = dr < ncd;
+        double bb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bb[k] = S[(size_t)(ncd + k) * ld + (ok ? dr : 0)];
+            bb[k] = ok ? bb[k] : 0.0;
+        }
+        double bv = rhs[ok ? dr : 0];
+        bv = ok ? bv : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) BBm[dr * 4 + k] = bb[k];
+        BV[dr] = bv;
+    }
+    for (int t = TPB - 1 - tid; t < nac; t += TPB) {  // the cameras' step operands (load_cam_step_ops)
+        const int cam = P.ac_cam[t];
+        const double* cd = camdata + (size_t)t * CAMDATA;
+        double o[18];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            o[k] = scale[6 * (size_t)t + k];
+            o[6 + k] = cd[k * 6 - (k * (k - 1)) / 2];
+            o[12 + k] = cd[45 + k];
         }
 #pragma unroll
-        for (int q = 0; q < BAND_NL; ++q)
-            if (dst[q] >= 0) lds[dst[q]] = v[q];
+        for (int k = 0; k < 18; ++k) lds[Ly.OPS + t * BAND_OPS + k] = o[k];
+        AC[t] = cam;
+    }
+    if (tid >= TPB / 2 && tid < TPB / 2 + 34) {  // bk = [b_k | S_kk lower packed] (14) | intrinsics' step operands (20)
+        const int f = tid - TPB / 2;
+        const double* p;
+        size_t idx;
+        int dst;
+        if (f < 4) {
+            p = rhs; idx = ncd + f; dst = Ly.BK + f;
+        } else if (f < 14) {
+            const int q2 = f - 4, mm = q2 < 1 ? 0 : q2 < 3 ? 1 : q2 < 6 ? 2 : 3, l = q2 - mm * (mm + 1) / 2;
+            p = S; idx = (size_t)(ncd + mm) * ld + ncd + l; dst = Ly.BK + f;
+        } else {
+            const int g = f - 14, kind = g >> 2, m = g & 3;
+            p = kind == 0 ? P.K[cur] : kind == 1 ? scale : kind == 4 ? P.prior : lin;
+            idx = kind == 0 ? m : kind == 1 ? P.off_k + m : kind == 2 ? 2 + 4 * m - (m * (m - 1)) / 2 : kind == 3 ? 12 + m : m;
+            dst = Ly.IOPS + g;
+        }
+        lds[dst] = p[idx];
     }
     if (skip) return;
-    if (tid < nac) AC[tid] = acv;
     const double radius = st->radius;
+    // ---- this thread's survivor-update elements: decoded once (blocks of <= 12 dofs; the wider blocks' two elements
+    // per thread would hold 22 registers through the level loop, and the kernel spilled: decoded per use there)
+    auto decode = [&](int k) {
+        const int q = NQ == 1 ? tid % NSI : tid + k * TPB;
+        BandItem I;
+        I.ok = (NQ == 1 ? tid / NSI < GRP : q < NSI) ? 1 : 0;
+        I.two = 1;
+        I.keep = 1;
+        I.mirror = -1;
+        if (q < ND) {  // D_j (r, cc), cc <= r: XR_i1^T XR_i1 + XL_i2^T XL_i2
+            int r = 0;
+            while ((r + 1) * (r + 2) / 2 <= q) ++r;
+            const int cc = q - r * (r + 1) / 2;
+            I.r = r; I.b1_arr = Ly.XR; I.b2_arr = Ly.CL; I.boff = cc; I.bs = G;
+            I.dst_arr = Ly.D; I.doff = r * G + cc; I.mirror = cc * G + r;
+        } else if (q < ND + G) {  // b_j: x
+            I.r = q - ND; I.b1_arr = I.b2_arr = Ly.BV; I.boff = 0; I.bs = 1;
+            I.dst_arr = Ly.BV; I.doff = I.r;
+        } else if (q < ND + 5 * G) {  // B_j (r, k)
+            const int f = q - ND - G;
+            I.r = f >> 2; I.b1_arr = I.b2_arr = Ly.BB; I.boff = f & 3; I.bs = 4;
+            I.dst_arr = Ly.BB; I.doff = f;
+        } else {  // the fill A(j, j - 2s) = -XR_i1^T XL_i1
+            const int f = q < NSI ? q - ND - 5 * G : 0, r = f / G, cc = f - r * G;
+            I.r = r; I.b1_arr = I.b2_arr = Ly.CL; I.boff = cc; I.bs = G; I.two = 0; I.keep = 0;
+            I.dst_arr = Ly.CL; I.doff = f;
+        }
+        return I;
+    };
+    constexpr bool PRE = G <= 12;
+    BandItem it[PRE ? NQ : 1];
+    if constexpr (PRE)
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) it[k] = decode(k);
+    const int grp = NQ == 1 ? tid / NSI : 0;
+    // per-block strides of the arrays (doubles): D / CL / XR GG, BB 4G, BV G
+    auto bstride = [&](int arr) { return arr == Ly.BB ? 4 * G : arr == Ly.BV ? G : GG; };
     __syncthreads();
-    // the poses of the step (a dependent load: the camera index first), held in a register until the step
+    // the poses of the step (a dependent load: the camera index first), in flight through the elimination
     const int nx = 7 * nac;
-    double xv = 0.0;
-    if (tid < nx) xv = P.cams[cur][7 * (size_t)AC[tid / 7] + tid % 7];
+    double xv[2] = {0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = tid + q * TPB;
+        if (e < nx) xv[q] = P.cams[cur][7 * (size_t)AC[e / 7] + e % 7];
+    }
     stamp();  // 0: loaded
     // K = floor(log2 nb): the root is block 2^K - 1, eliminated at level K with no neighbour
     int K = 0;
@@ -235,65 +367,130 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
     for (int m = 0; m <= K; ++m) {
         const int s = 1 << m;
         const int ne = ((nb >> m) + 1) >> 1;  // blocks i with i + 1 = odd * 2^m, i < nb
-        // ---- factor + forward solve, one half-wave per eliminated block
-        for (int s0 = 0; s0 < ne; s0 += 2 * NW_BAND) {
-            const int slot = s0 + 2 * wave + (hi ? 1 : 0);
+        // ---- factor, one unit (U lanes, lane = row) per eliminated block
+        for (int s0 = 0; s0 < ne; s0 += UPW * NW) {
+            const int slot = s0 + wave * UPW + lane / U;
             const bool act = slot < ne;
             const int i = act ? ((2 * slot + 1) << m) - 1 : 0;
-            const int r = hl < G ? hl : G - 1;
+            const int r = ul < G ? ul : G - 1;
+            if (s0 == 0) fst(m, 0);
             double a[G];
 #pragma unroll
             for (int k = 0; k < G; ++k) a[k] = Dm[i * GG + r * G + k];
             double my_inv = 0.0;
-            double dn = bcast_half(a[0], 0, hi);
-#pragma unroll
-            for (int j = 0; j < G; ++j) {
+            double dn = ubc<U, 0>(a[0], hi);
+            if (s0 == 0) fst(m, 1);
+            sfor<0, G>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
                 const double dd = dn;
                 bad = bad || (act && !(dd > 0.0 && dd < INFINITY));
                 const double y = __builtin_amdgcn_rsq(dd);
                 const double ee = __builtin_fma(-dd * y, y, 1.0);
                 const double l = __builtin_fma(0.5 * a[j] * y, ee, a[j] * y);
-                my_inv = (hl == j) ? __builtin_fma(0.5 * y, ee, y) : my_inv;
+                my_inv = (ul == j) ? __builtin_fma(0.5 * y, ee, y) : my_inv;
                 a[j] = l;
-                if (j + 1 < G) {
-                    dn = bcast_half(__builtin_fma(-l, l, a[j + 1]), j + 1, hi);
-#pragma unroll
-                    for (int k = j + 1; k < G; ++k) a[k] = __builtin_fma(-l, bcast_half(l, k, hi), a[k]);
+                if constexpr (j + 1 < G) {
+                    dn = ubc<U, j + 1>(__builtin_fma(-l, l, a[j + 1]), hi);
+                    sfor<j + 1, G>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        a[k] = __builtin_fma(-l, ubc<U, k>(l, hi), a[k]);
+                    });
                 }
-            }
-            if (act && hl < G) {
+            });
+            if (s0 == 0) fst(m, 2);
+            if (act && ul < G) {
 #pragma unroll
-                for (int k = 0; k < G; ++k) Dm[i * GG + hl * G + k] = k <= hl ? a[k] : 0.0;
-                RI[i * G + hl] = my_inv;
+                for (int k = 0; k < G; ++k) Dm[i * GG + ul * G + k] = k <= ul ? a[k] : 0.0;
+                RI[i * G + ul] = my_inv;
             }
             wave_sync();
-            // lane = column of [A(i, i - s) | A(i, i + s) = A(i + s, i)^T | b_i | B_i]
-            const int rb = i + s;
-            const bool has_r = rb < nb;
-            const double* Li = Dm + i * GG;
-            const double* ri = RI + i * G;
-            for (int col = hl; act && col < NCOL; col += 32) {
-                // the column as (base, stride): A(i, i - s) column col in place (-> XL); A(i + s, i) row col - G
-                // (-> XR, stored to XR_i); b_i (-> x); B_i column k (-> XB)
-                double* src;
-                double* out;
-                int stride;
-                if (col < G) {
-                    src = out = CL + i * GG + col;
-                    stride = G;
-                } else if (col < 2 * G) {
-                    src = CL + (has_r ? rb : i) * GG + (col - G) * G;
-                    out = XR + i * GG + col - G;
-                    stride = has_r ? 1 : 0;  // (no right neighbour: a zero column, read below as 0)
-                } else if (col == 2 * G) {
-                    src = out = BV + i * G;
-                    stride = 1;
-                } else {
-                    src = out = BBm + i * G * 4 + col - 2 * G - 1;
-                    stride = 4;
+            if (s0 == 0) fst(m, 3);
+            // forward solve by the same unit (lane = column; lanes < NCOL - U take a second column, interleaved), no
+            // workgroup barrier between a block's factorisation and its solve:
+            // [XL | XR | x | XB] = L_i^-1 [A(i, i - s) | A(i, i + s) = A(i + s, i)^T | b_i | B_i]
+            // (blocks of one camera; the wider blocks' two columns per lane spill: they take the separate phase below)
+            if (FUSE && act) {
+                const int rb = i + s;
+                const bool has_r = rb < nb;
+                const double* Li = Dm + i * GG;
+                const double* ri = RI + i * G;
+                constexpr int NCP = (NCOL + U - 1) / U;  // columns per lane
+                double x[NCP][G];
+                double* out[NCP];
+                int ostride[NCP];
+                bool live[NCP];
+#pragma unroll
+                for (int p = 0; p < NCP; ++p) {
+                    const int col = ul + p * U;
+                    live[p] = col < NCOL;
+                    // the column as (base, stride): A(i, i - s) column col in place (-> XL); A(i + s, i) row col - G
+                    // (-> XR_i); b_i (-> x); B_i column k (-> XB)
+                    const double* src;
+                    int stride;
+                    if (col < G) {
+                        out[p] = CL + i * GG + col; src = out[p]; stride = G; ostride[p] = G;
+                    } else if (col < 2 * G) {
+                        src = CL + (has_r ? rb : i) * GG + (col - G) * G; out[p] = XR + i * GG + col - G; stride = 1;
+                        ostride[p] = G;
+                    } else if (col == 2 * G) {
+                        out[p] = BV + i * G; src = out[p]; stride = 1; ostride[p] = 1;
+                    } else {
+                        const int k = live[p] ? col - 2 * G - 1 : 0;
+                        out[p] = BBm + i * G * 4 + k; src = out[p]; stride = 4; ostride[p] = 4;
+                    }
+                    const bool zero = !live[p] || (col >= G && col < 2 * G && !has_r);
+#pragma unroll
+                    for (int q = 0; q < G; ++q) x[p][q] = zero ? 0.0 : src[q * stride];
                 }
-                const bool zero = col >= G && col < 2 * G && !has_r;
-                const int ostride = (col >= G && col < 2 * G) ? G : stride;
+                if (s0 == 0) fst(m, 4);
+#pragma unroll
+                for (int j = 0; j < G; ++j) {
+                    const double rj = ri[j];
+#pragma unroll
+                    for (int p = 0; p < NCP; ++p) x[p][j] *= rj;
+#pragma unroll
+                    for (int q = j + 1; q < G; ++q) {
+                        const double lq = Li[q * G + j];
+#pragma unroll
+                        for (int p = 0; p < NCP; ++p) x[p][q] = __builtin_fma(-lq, x[p][j], x[p][q]);
+                    }
+                    narrow_live_range<G>();
+                }
+                if (s0 == 0) fst(m, 5);
+#pragma unroll
+                for (int p = 0; p < NCP; ++p)
+                    if (live[p])
+#pragma unroll
+                        for (int q = 0; q < G; ++q) out[p][q * ostride[p]] = x[p][q];
+            }
+            if (s0 == 0) fst(m, 6);
+        }
+        __syncthreads();
+        if constexpr (!FUSE) {
+            // ---- forward solve (blocks of 2-3 cameras): thread (fgrp, fcol) takes column fcol of the blocks fgrp,
+            // fgrp + FGRP, ...
+            const int fcol = tid % NCOL, fgrp = tid / NCOL;
+            constexpr int FGRP = TPB / NCOL;
+            for (int g = fgrp; g < ne && fgrp < FGRP; g += FGRP) {
+                const int i = ((2 * g + 1) << m) - 1;
+                const int rb = i + s;
+                const bool has_r = rb < nb;
+                const double* Li = Dm + i * GG;
+                const double* ri = RI + i * G;
+                const double* src;
+                double* out;
+                int stride, ostride;
+                if (fcol < G) {
+                    out = CL + i * GG + fcol; src = out; stride = G; ostride = G;
+                } else if (fcol < 2 * G) {
+                    src = CL + (has_r ? rb : i) * GG + (fcol - G) * G; out = XR + i * GG + fcol - G; stride = 1;
+                    ostride = G;
+                } else if (fcol == 2 * G) {
+                    out = BV + i * G; src = out; stride = 1; ostride = 1;
+                } else {
+                    out = BBm + i * G * 4 + fcol - 2 * G - 1; src = out; stride = 4; ostride = 4;
+                }
+                const bool zero = fcol >= G && fcol < 2 * G && !has_r;
                 double x[G];
 #pragma unroll
                 for (int q = 0; q < G; ++q) x[q] = zero ? 0.0 : src[q * stride];
@@ -307,118 +504,88 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
 #pragma unroll
                 for (int q = 0; q < G; ++q) out[q * ostride] = x[q];
             }
+            __syncthreads();
         }
-        __syncthreads();
-        // ---- survivors pull their eliminated neighbours' Schur terms; eliminated blocks form their border Gram
-        constexpr int ND = G * (G + 1) / 2, NSI = ND + G + 4 * G + GG;
+        stamp();  // 1 + 2m: level m factored
+        // ---- survivors pull their eliminated neighbours' Schur terms (every thread the same code: its elements'
+        // operands were decoded before the loop); eliminated blocks form their border Gram
         const int ns = m < K ? nb >> (m + 1) : 0;  // survivors j with j + 1 = multiple of 2^(m+1)
-        const int total = ns * NSI + ne * 14;
-        for (int e = tid; e < total; e += TPB_BAND) {
-            if (e < ns * NSI) {
-                const int t = e / NSI, q = e % NSI;
-                const int j = ((t + 1) << (m + 1)) - 1, i1 = j - s, i2 = j + s;
-                const bool h2 = i2 < nb;
-                const double* xr1 = XR + i1 * GG;  // XR_i1 (rows: i1's dofs, columns: j's)
-                const double* xl2 = CL + (h2 ? i2 : i1) * GG;  // XL_i2 (columns: j's dofs)
-                if (q < ND) {  // D_j (r, cc), cc <= r, written to both halves
-                    int r = 0, cc = q;
-                    while (cc > r) { cc -= r + 1; ++r; }
-                    double a1 = 0.0, a2 = 0.0;
+        for (int t = grp; t < ns; t += GRP) {
+            const int j = ((t + 1) << (m + 1)) - 1, i1 = j - s, i2 = j + s;
+            const bool h2 = i2 < nb;
 #pragma unroll
-                    for (int u = 0; u < G; ++u) a1 = __builtin_fma(xr1[u * G + r], xr1[u * G + cc], a1);
-                    if (h2)
+            for (int k = 0; k < NQ; ++k) {
+                BandItem I;
+                if constexpr (PRE) I = it[k];
+                else I = decode(k);
+                if (!I.ok) continue;
+                const double* a1 = XR + i1 * GG + I.r;                 // column r of XR_i1
+                const double* a2 = CL + (h2 ? i2 : i1) * GG + I.r;     // column r of XL_i2
+                const double* b1 = lds + I.b1_arr + i1 * bstride(I.b1_arr) + I.boff;
+                const double* b2 = lds + I.b2_arr + (h2 ? i2 : i1) * bstride(I.b2_arr) + I.boff;
+                double acc1 = 0.0, acc2 = 0.0;
 #pragma unroll
-                        for (int u = 0; u < G; ++u) a2 = __builtin_fma(xl2[u * G + r], xl2[u * G + cc], a2);
-                    const double nv = (Dm[j * GG + r * G + cc] - a1) - a2;
-                    Dm[j * GG + r * G + cc] = nv;
-                    Dm[j * GG + cc * G + r] = nv;
-                } else if (q < ND + G) {  // b_j
-                    const int r = q - ND;
-                    double a1 = 0.0, a2 = 0.0;
-#pragma unroll
-                    for (int u = 0; u < G; ++u) a1 = __builtin_fma(xr1[u * G + r], BV[i1 * G + u], a1);
-                    if (h2)
-#pragma unroll
-                        for (int u = 0; u < G; ++u) a2 = __builtin_fma(xl2[u * G + r], BV[i2 * G + u], a2);
-                    BV[j * G + r] = (BV[j * G + r] - a1) - a2;
-                } else if (q < ND + 5 * G) {  // B_j (r, k)
-                    const int f = q - ND - G, r = f >> 2, k = f & 3;
-                    double a1 = 0.0, a2 = 0.0;
-#pragma unroll
-                    for (int u = 0; u < G; ++u) a1 = __builtin_fma(xr1[u * G + r], BBm[(i1 * G + u) * 4 + k], a1);
-                    if (h2)
-#pragma unroll
-                        for (int u = 0; u < G; ++u) a2 = __builtin_fma(xl2[u * G + r], BBm[(i2 * G + u) * 4 + k], a2);
-                    BBm[(j * G + r) * 4 + k] = (BBm[(j * G + r) * 4 + k] - a1) - a2;
-                } else {  // the fill A(j, j - 2s) = -XR_i1^T XL_i1
-                    const int f = q - ND - 5 * G, r = f / G, cc = f % G;
-                    const double* xl1 = CL + i1 * GG;
-                    double a1 = 0.0;
-#pragma unroll
-                    for (int u = 0; u < G; ++u) a1 = __builtin_fma(xr1[u * G + r], xl1[u * G + cc], a1);
-                    CL[j * GG + r * G + cc] = -a1;
+                for (int u = 0; u < G; ++u) {
+                    acc1 = __builtin_fma(a1[u * G], b1[u * I.bs], acc1);
+                    acc2 = __builtin_fma(a2[u * G], b2[u * I.bs], acc2);
+                    if (u % 6 == 5) narrow_live_range<G>();
                 }
-            } else {  // border Gram of eliminated block i: XB^T XB (10, lower packed) | XB^T x (4)
-                const int f = e - ns * NSI, g = f / 14, q = f % 14;
-                const int i = ((2 * g + 1) << m) - 1;
-                const double* xb = BBm + i * G * 4;
-                int k = 0, l = 0;
-                if (q < 10) {
-                    l = q;
-                    while (l > k) { l -= k + 1; ++k; }
-                } else {
-                    k = q - 10;
-                }
-                double acc = 0.0;
-#pragma unroll
-                for (int u = 0; u < G; ++u)
-                    acc = __builtin_fma(xb[u * 4 + k], q < 10 ? xb[u * 4 + l] : BV[i * G + u], acc);
-                GR[i * BAND_GR + q] = acc;
+                double* d = lds + I.dst_arr + j * bstride(I.dst_arr);
+                const double v = ((I.keep ? d[I.doff] : 0.0) - acc1) - ((I.two && h2) ? acc2 : 0.0);
+                d[I.doff] = v;
+                if (I.mirror >= 0) d[I.mirror] = v;
             }
         }
-        __syncthreads();
-        stamp();  // 1 + m: level m done
+        if (ns > 0) {
+            __syncthreads();
+            stamp();  // 2 + 2m: level m's survivors updated
+        }
     }
-    // ---- border system: the blocks' Grams summed in block order (four interleaved partial chains combined in a
-    // fixed order), then (C - B^T V) y_k = b_k - B^T u on one lane
+    // ---- border system. Every block's XB and x are final once it is eliminated, and the blocks are stored in dof
+    // order, so sum_i XB_i^T [XB_i | x_i] is one dot product over the camera dof rows: 14 sums, each split over 32
+    // lanes (rows r = lane, lane + 32, ...) and reduced in a fixed order; then (C - B^T V) y_k = b_k - B^T u on one lane
     double* const red = lds + Ly.RED;
     double* const yk = lds + Ly.YK;
-    if (wave == 0) {
-        const int q = lane >> 2, p = lane & 3;
-        double acc = 0.0;
-        if (q < 14)
-            for (int i = p; i < nb; i += 4) acc += GR[i * BAND_GR + q];
-        acc += __shfl_xor(acc, 1);  // (p0 + p1), (p2 + p3)
-        acc += __shfl_xor(acc, 2);  // (p0 + p1) + (p2 + p3)
-        if (q < 14 && p == 0) {
-            int k = 0, l = q;
-            if (q < 10) {
-                while (l > k) { l -= k + 1; ++k; }
-                red[k * 5 + 1 + l] = acc;
-                red[l * 5 + 1 + k] = acc;
-            } else {
-                red[(q - 10) * 5] = acc;
+    {
+        constexpr int SPL = 32;
+        for (int o = tid / SPL; o < 14; o += TPB / SPL) {
+            const int p = tid % SPL;
+            const int k = o < 1 ? 0 : o < 3 ? 1 : o < 6 ? 2 : o < 10 ? 3 : o - 10;
+            const int l = o < 10 ? o - k * (k + 1) / 2 : 0;
+            double acc = 0.0;
+            for (int rr = p; rr < nrow; rr += SPL)
+                acc = __builtin_fma(BBm[rr * 4 + k], o < 10 ? BBm[rr * 4 + l] : BV[rr], acc);
+#pragma unroll
+            for (int off = 1; off < SPL; off <<= 1) acc += __shfl_xor(acc, off);  // fixed butterfly order
+            if (p == 0) {
+                if (o < 10) {
+                    red[k * 5 + 1 + l] = acc;
+                    red[l * 5 + 1 + k] = acc;
+                } else {
+                    red[k * 5] = acc;
+                }
             }
         }
-        wave_sync();
-        if (lane == 0) {
+        __syncthreads();
+        if (tid == 0) {
             bool bb = false;
-            border_solve4(lds + Ly.BK, red, yk, bb);
+            border_solve4_rsq(lds + Ly.BK, red, yk, bb);
             bad = bad || bb;
         }
     }
-    if (bad && hl == 0) raise_flag(flag, FLAG_NOT_PD);
+    if (bad && ul == 0) raise_flag(flag, FLAG_NOT_PD);
     __syncthreads();
-    stamp();  // K + 2: border
-    // ---- back-substitution, top level first: y_i = L_i^-T (x_i - XL_i y_l - XR_i y_r - XB_i y_k)
+    stamp();  // 2K + 3: border
+    // ---- back-substitution, top level first, one unit (lane = row) per block:
+    // y_i = L_i^-T (x_i - XL_i y_l - XR_i y_r - XB_i y_k)
     for (int m = K; m >= 0; --m) {
         const int s = 1 << m;
         const int ne = ((nb >> m) + 1) >> 1;
-        for (int s0 = 0; s0 < ne; s0 += 2 * NW_BAND) {
-            const int slot = s0 + 2 * wave + (hi ? 1 : 0);
+        for (int s0 = 0; s0 < ne; s0 += UPW * NW) {
+            const int slot = s0 + wave * UPW + lane / U;
             const bool act = slot < ne;
             const int i = act ? ((2 * slot + 1) << m) - 1 : 0;
-            const int r = hl < G ? hl : G - 1;
+            const int r = ul < G ? ul : G - 1;
             const int lb = i - s, rb = i + s;
             const bool hl_ = lb >= 0, hr = rb < nb;
             double w0 = BV[i * G + r], w1 = 0.0, w2 = 0.0;
@@ -434,26 +601,28 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
             double w = ((w0 - w1) - w2) - w3;
             const double* Li = Dm + i * GG;
             double yv = 0.0;
-#pragma unroll
-            for (int R = G - 1; R >= 0; --R) {
-                const double yR = bcast_half(w, R, hi) * RI[i * G + R];
-                yv = hl == R ? yR : yv;
-                if (hl < R) w = __builtin_fma(-Li[R * G + r], yR, w);
-                if (R % 6 == 0) narrow_live_range<G>();
-            }
-            if (act && hl < G) YV[i * G + hl] = yv;
+            sfor<0, G>([&](auto Rc) {
+                constexpr int R = G - 1 - decltype(Rc)::value;
+                const double yR = ubc<U, R>(w, hi) * RI[i * G + R];
+                yv = ul == R ? yR : yv;
+                if (ul < R) w = __builtin_fma(-Li[R * G + r], yR, w);
+            });
+            if (act && ul < G) YV[i * G + ul] = yv;
         }
         __syncthreads();
     }
-    stamp();  // K + 3: back-substitution
-    // ---- y to rhs (the points' back-substitution reads it), the poses into the staged operands
-    for (int d = tid; d < ncd + 4; d += TPB_BAND) rhs[d] = d < ncd ? YV[d] : yk[d - ncd];
-    if (tid < nx) lds[Ly.OPS + (tid / 7) * BAND_OPS + 18 + tid % 7] = xv;
+    stamp();  // 2K + 4: back-substitution
+    // ---- y to rhs (the points' back-substitution reads it); the step (block_step's arithmetic and grouping: wave w =
+    // cameras [10 w, 10 w + 10), w = 0 also the intrinsics; part slot w)
+    for (int d = tid; d < ncd + 4; d += TPB) rhs[d] = d < ncd ? YV[d] : yk[d - ncd];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = tid + q * TPB;
+        if (e < nx) lds[Ly.OPS + (e / 7) * BAND_OPS + 18 + e % 7] = xv[q];
+    }
     __syncthreads();
-    // ---- the step (block_step's arithmetic and grouping: wave w = cameras [10 w, 10 w + 10), w = 0 also the
-    // intrinsics; part slot w)
     const int nupd = (nac + BCR_CAMS - 1) / BCR_CAMS;
-    for (int w = wave; w < nupd; w += NW_BAND) {
+    for (int w = wave; w < nupd; w += NW) {
         double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
         const int t = w * BCR_CAMS + lane;
         if (lane < BCR_CAMS && t < nac) {
@@ -482,10 +651,12 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
             }
             intr_step(P, c, cur, radius, o, yk, delta, acc);
         }
+        // (lanes >= 16 hold no term: a 16-lane butterfly in a fixed order)
+        static_assert(BCR_CAMS + 1 <= 16, "the step's terms sit on lanes < 16");
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
+        for (int off = 8; off > 0; off >>= 1)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+            for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off, 16);
         if (lane == 0) {
             part[PART_UPD_SN2 * P.part_stride + w] = acc[0];
             part[PART_UPD_MCC * P.part_stride + w] = acc[1];
@@ -493,7 +664,10 @@ __global__ __launch_bounds__(BandTpb<BC>::TPB) void k_bcr_band(const LmState* __
             part[PART_UPD_XN2 * P.part_stride + w] = acc[3];
         }
     }
-    stamp();  // K + 4: step
+    stamp();  // 2K + 5: step
+    if constexpr (STAMP)
+        for (int k = tid; k < BAND_STAMPS + BAND_FSTAMPS; k += TPB)
+            tl[k] = k < ts || k >= BAND_STAMPS - 1 ? stl[k] : 0ull;
 }
 
 static size_t band_lds_bytes(int bc, int nb, int nac) { return sizeof(double) * (size_t)band_layout(6 * bc, nb, nac).total; }
@@ -538,14 +712,14 @@ static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork&
     }
     const size_t lds = band_lds_bytes(BC, nb, P.nac);
     if (smode) {
-        if (!dst) CKD(hipMalloc(&dst, BAND_STAMPS * sizeof(unsigned long long)));
-        CKD(hipMemsetAsync(dst, 0, BAND_STAMPS * sizeof(unsigned long long), s));
+        if (!dst) CKD(hipMalloc(&dst, (BAND_STAMPS + BAND_FSTAMPS) * sizeof(unsigned long long)));
+        CKD(hipMemsetAsync(dst, 0, (BAND_STAMPS + BAND_FSTAMPS) * sizeof(unsigned long long), s));
         if (pf) pf->begin(K_BCR_PERSIST, s);
-        hipLaunchKernelGGL((k_bcr_band<BC, true>), dim3(1), dim3(BandTpb<BC>::TPB), lds, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
+        hipLaunchKernelGGL((k_bcr_band<BC, true>), dim3(1), dim3(BAND_TPB), lds, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
                            W.scale, W.camdata, W.lin, W.delta, W.part, nb, dst);
         if (pf) pf->end(s);
         CKD(hipGetLastError());
-        unsigned long long h[BAND_STAMPS];
+        unsigned long long h[BAND_STAMPS + BAND_FSTAMPS];
         CKD(hipMemcpyAsync(h, dst, sizeof(h), hipMemcpyDeviceToHost, s));
         CKD(hipStreamSynchronize(s));
         if (h[0]) {  // (0: the launch exited at once, skip_step)
@@ -553,13 +727,25 @@ static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork&
             while ((2 << K) <= nb) ++K;
             std::fprintf(stderr, "bcr_band<%d> nb=%d us:", BC, nb);
             const unsigned long long t0 = h[BAND_STAMPS - 1];
-            for (int k = 0; k <= K + 4; ++k) std::fprintf(stderr, " %.2f", (double)(h[k] - t0) / 100.0);
-            std::fprintf(stderr, "  (loaded, levels 0..%d, border, back, step)\n", K);
+            double prev = 0.0;
+            for (int k = 0; k < BAND_STAMPS - 1 && h[k]; ++k) {
+                const double t = (double)(h[k] - t0) / 100.0;
+                std::fprintf(stderr, " %.2f", t - prev);
+                prev = t;
+            }
+            std::fprintf(stderr, "  = %.2f us (phase durations: load, [factor, update] x levels 0..%d (the root: factor "
+                                 "only), border, back, step)\n", prev, K);
+            for (int m = 0; m <= K && m < 8; ++m) {  // inside the factor phase: wave 0's first unit
+                const unsigned long long* f = h + BAND_STAMPS + 8 * m;
+                std::fprintf(stderr, "  level %d factor unit: D rows %.2f chain %.2f L stored %.2f cols loaded %.2f solve %.2f "
+                                     "stored %.2f us\n", m, (f[1] - f[0]) / 100.0, (f[2] - f[1]) / 100.0, (f[3] - f[2]) / 100.0,
+                             (f[4] - f[3]) / 100.0, (f[5] - f[4]) / 100.0, (f[6] - f[5]) / 100.0);
+            }
         }
         return hipSuccess;
     }
     if (pf) pf->begin(K_BCR_PERSIST, s);
-    hipLaunchKernelGGL((k_bcr_band<BC, false>), dim3(1), dim3(BandTpb<BC>::TPB), lds, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
+    hipLaunchKernelGGL((k_bcr_band<BC, false>), dim3(1), dim3(BAND_TPB), lds, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
                        W.scale, W.camdata, W.lin, W.delta, W.part, nb, (unsigned long long*)nullptr);
     if (pf) pf->end(s);
     return hipGetLastError();

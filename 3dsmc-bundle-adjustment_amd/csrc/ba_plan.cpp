@@ -5,7 +5,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <mutex>
@@ -125,9 +127,27 @@ inline int n_tasks(long long n, long long grain) {
 int host_threads() { return pool().size(); }
 void host_parallel(int n, const std::function<void(int)>& fn) { pool().run(n, fn); }
 
+// MIBA_PLAN_TIMES=1: per-phase wall times of the plan on stderr (diagnostic)
+struct PhaseTimer {
+    bool on;
+    double t;
+    const char* stage;
+    explicit PhaseTimer(const char* s) : on(std::getenv("MIBA_PLAN_TIMES") != nullptr), t(now()), stage(s) {}
+    static double now() {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void mark(const char* what) {
+        if (!on) return;
+        const double n = now();
+        std::fprintf(stderr, "plan %s/%s %.3f ms\n", stage, what, n - t);
+        t = n;
+    }
+};
+
 // ---------------------------------------------------------------- stage 1
 void plan_count(const PlanInput& in, Plan& pl) {
     const int nc = in.nc, np = in.np, no = in.no;
+    PhaseTimer tm("count");
     pl.err.clear();
     pl.cam_cnt.assign(nc, 0);
     pl.pt_cnt.assign(np, 0);
@@ -168,12 +188,14 @@ void plan_count(const PlanInput& in, Plan& pl) {
         pl.obs32 = pl.obs32 && f32ok[t];
         for (int i = 0; i < nc; ++i) pl.cam_cnt[i] += cc[t][i];
     }
+    tm.mark("all");
 }
 
 // ---------------------------------------------------------------- stage 2
 void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const PlanParams& pp, Plan& pl) {
     const int nc = in.nc, np = in.np, no = in.no;
     const int n_adm = pl.n_adm;
+    PhaseTimer tm("order");
     // active cameras (Ceres removes unused blocks; the gauge block is constant, :299)
     pl.cam_ac.assign(nc, -1);
     pl.ac_cam.clear();
@@ -196,6 +218,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
                 if (pl.adm[k]) plist[__atomic_fetch_add(cp + in.obs_pt[k], 1, __ATOMIC_RELAXED)] = (int)k;
         });
     }
+    tm.mark("point_lists");
     pl.pmin.assign(np, INT_MAX);
     pl.pmax.assign(np, -1);
     std::vector<signed char> pclass(np, -1);  // 0 tiled, 1 overflow (Schur via atomics), 2 gauge-only
@@ -242,6 +265,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
             }
         });
     }
+    tm.mark("point_sort_class");
     // points by class; tiled and overflow points by first camera, ties in point order (a stable counting sort)
     std::vector<int> cls[3];
     {
@@ -298,6 +322,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
             build_tiles(tile_pts);
         }
     }
+    tm.mark("class_sort_tiles");
     // active point order: tiled (tile order), overflow, gauge-only; point-major obs in that order
     pl.pt_idx.clear();
     pl.pt_idx.reserve(cls[0].size() + cls[1].size() + cls[2].size());
@@ -321,6 +346,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
             }
         });
     }
+    tm.mark("point_major");
     pl.ovf_obs.clear();
     for (int q = pl.pt_ptr[pl.n_tiled]; q < pl.pt_ptr[n_ap]; ++q)
         if (cam_ac[in.obs_cam[pl.po_orig[q]]] >= 0) pl.ovf_obs.push_back(q);
@@ -332,6 +358,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
         pl.bs_chunk.push_back(b);
         a = b;
     }
+    tm.mark("ovf_bs");
     // camera-major obs (one segment per camera with admissible obs, gauge included; each camera's in index
     // order): a two-pass counting scatter over ranges of the observations
     std::vector<int> cstart(nc + 1, 0);
@@ -368,6 +395,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
                 }
         });
     }
+    tm.mark("camera_major");
     // sub-segments of <= subseg observations (one workgroup each), equal-sized within a camera; ac_seg[ac] = the
     // sub-segment range of active camera ac (empty when this shard has no observation of it)
     pl.seg_ptr.assign(1, 0); pl.seg_cam.clear(); pl.seg_ac.clear();
@@ -405,6 +433,7 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
         for (int t = 0; t < T; ++t)
             for (int a = 0; a < nac; ++a) pl.fc[a] = std::min(pl.fc[a], loc[t][a]);
     }
+    tm.mark("segments_fc");
 }
 
 // ---------------------------------------------------------------- stage 3
