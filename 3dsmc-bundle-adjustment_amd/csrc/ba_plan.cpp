@@ -122,6 +122,95 @@ inline int n_tasks(long long n, long long grain) {
     return (int)want;
 }
 
+
+// tiles over the tiled points (sequence i < n0 in the point order: first / last active camera, observation count):
+// window [base, base + span), span <= tile_win, <= tile_pts points; chunks of <= chunk_pts points and <= chunk_obs
+// observations. tile_pts spreads the points over one wave of resident workgroups (no second, partly empty wave of
+// tiles), grown until the tile count fits the resident slots.
+template <class Fmin, class Fmax, class Fcnt>
+void build_tiles(int n0, Fmin pmin, Fmax pmax, Fcnt cnt, const PlanParams& pp, Plan& pl) {
+    auto count = [&](int tile_pts) {  // the tile boundaries alone (the trial sizes of the growth loop)
+        int n = 0;
+        for (int i = 0; i < n0; ++n) {
+            const int base = pmin(i);
+            int j = i;
+            while (j < n0 && j - i < tile_pts && pmax(j) - base < pp.tile_win) ++j;
+            i = j;
+        }
+        return n;
+    };
+    auto build = [&](int tile_pts) {
+        pl.tile_chunk.assign(1, 0); pl.tile_base.clear(); pl.tile_span.clear(); pl.chunk_ap.assign(1, 0);
+        int i = 0;
+        while (i < n0) {
+            const int base = pmin(i);
+            int j = i, hi = base;
+            while (j < n0 && j - i < tile_pts && pmax(j) - base < pp.tile_win) { hi = std::max(hi, pmax(j)); ++j; }
+            int c0 = i;
+            while (c0 < j) {
+                int c1 = c0, nob = 0;
+                while (c1 < j && c1 - c0 < pp.chunk_pts && nob + cnt(c1) <= pp.chunk_obs) { nob += cnt(c1); ++c1; }
+                pl.chunk_ap.push_back(c1);
+                c0 = c1;
+            }
+            pl.tile_chunk.push_back((int)pl.chunk_ap.size() - 1);
+            pl.tile_base.push_back(base);
+            pl.tile_span.push_back(hi - base + 1);
+            i = j;
+        }
+    };
+    const int slots = pp.tile_slots - 1;  // one resident slot for the intrinsics-term workgroup
+    int tile_pts = 128;
+    if (slots > 0) tile_pts = std::max(pp.chunk_pts, (n0 + slots - 1) / slots);
+    if (pp.tile_pts_env > 0) tile_pts = pp.tile_pts_env;
+    for (int grow = 0; pp.tile_pts_env <= 0 && slots > 0 && grow < 16 && count(tile_pts) > slots; ++grow)
+        tile_pts += std::max(1, tile_pts / 8);
+    build(tile_pts);
+}
+
+// back-substitution chunks over all active points: <= bs_pts points and <= bs_obs observations
+void build_bs_chunks(int n_ap, const PlanParams& pp, Plan& pl) {
+    pl.bs_chunk.assign(1, 0);
+    for (int a = 0; a < n_ap;) {
+        int b = a + 1;
+        while (b < n_ap && b - a < pp.bs_pts && pl.pt_ptr[b + 1] - pl.pt_ptr[a] <= pp.bs_obs) ++b;
+        pl.bs_chunk.push_back(b);
+        a = b;
+    }
+}
+
+// sub-segments of <= subseg observations (one workgroup each), equal-sized within a camera; ac_seg[ac] = the
+// sub-segment range of active camera ac (empty when this shard has no observation of it)
+void build_segments(int nc, const std::vector<int>& cstart, const PlanParams& pp, Plan& pl) {
+    const int nac = pl.nac;
+    pl.seg_ptr.assign(1, 0); pl.seg_cam.clear(); pl.seg_ac.clear();
+    pl.ac_seg.assign(2 * (size_t)std::max(nac, 1), 0);
+    for (int i = 0; i < nc; ++i)
+        if (pl.cam_cnt[i] > 0) {
+            const int first = (int)pl.seg_cam.size();
+            const int cnt = pl.cam_cnt[i], nseg = (cnt + pp.subseg - 1) / pp.subseg;
+            const int ac = pl.cam_ac[i];
+            for (int k = 1; k <= nseg; ++k) {
+                pl.seg_cam.push_back(i);
+                pl.seg_ac.push_back(ac);
+                pl.seg_ptr.push_back(cstart[i] + (int)(((long long)cnt * k) / nseg));
+            }
+            if (ac >= 0) {
+                pl.ac_seg[2 * ac] = first;
+                pl.ac_seg[2 * ac + 1] = (int)pl.seg_cam.size();
+            }
+        }
+}
+
+// active cameras (Ceres removes unused blocks; the gauge block is constant, :299)
+void build_active_cameras(int nc, const std::vector<int>& cam_seen, int fixed_cam, Plan& pl) {
+    pl.cam_ac.assign(nc, -1);
+    pl.ac_cam.clear();
+    for (int i = 0; i < nc; ++i)
+        if (cam_seen[i] && i != fixed_cam) { pl.cam_ac[i] = (int)pl.ac_cam.size(); pl.ac_cam.push_back(i); }
+    pl.nac = (int)pl.ac_cam.size();
+}
+
 }  // namespace
 
 int host_threads() { return pool().size(); }
@@ -155,7 +244,9 @@ void plan_count(const PlanInput& in, Plan& pl) {
     pl.n_adm = 0;
     const int T = n_tasks(no, 32768);
     const Split sp{no, T};
-    std::vector<std::vector<int>> cc(T);
+    // per-range camera counts, kept for plan_order's camera-major scatter over the same ranges
+    pl.obs_tasks = T;
+    pl.task_cam.assign((size_t)T * nc, 0);
     std::vector<int> nadm(T, 0);
     std::vector<long long> bad(T, -1);  // first out-of-range observation of each range
     std::vector<unsigned char> f32ok(T, 1);
@@ -163,8 +254,7 @@ void plan_count(const PlanInput& in, Plan& pl) {
     // an f64 value that survives the round trip through f32 unchanged (NaN does not)
     auto f32_exact = [](double v) { return (double)(float)v == v; };
     host_parallel(T, [&](int t) {
-        std::vector<int>& c = cc[t];
-        c.assign(nc, 0);
+        int* c = pl.task_cam.data() + (size_t)t * nc;
         int na = 0;
         bool f32 = in.obs_uv != nullptr;
         for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k) {
@@ -186,7 +276,7 @@ void plan_count(const PlanInput& in, Plan& pl) {
     for (int t = 0; t < T; ++t) {
         pl.n_adm += nadm[t];
         pl.obs32 = pl.obs32 && f32ok[t];
-        for (int i = 0; i < nc; ++i) pl.cam_cnt[i] += cc[t][i];
+        for (int i = 0; i < nc; ++i) pl.cam_cnt[i] += pl.task_cam[(size_t)t * nc + i];
     }
     tm.mark("all");
 }
@@ -196,37 +286,68 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
     const int nc = in.nc, np = in.np, no = in.no;
     const int n_adm = pl.n_adm;
     PhaseTimer tm("order");
-    // active cameras (Ceres removes unused blocks; the gauge block is constant, :299)
-    pl.cam_ac.assign(nc, -1);
-    pl.ac_cam.clear();
-    for (int i = 0; i < nc; ++i)
-        if (cam_seen[i] && i != in.fixed_cam) { pl.cam_ac[i] = (int)pl.ac_cam.size(); pl.ac_cam.push_back(i); }
-    const int nac = pl.nac = (int)pl.ac_cam.size();
+    pl.dev = false;
+    build_active_cameras(nc, cam_seen, in.fixed_cam, pl);
+    const int nac = pl.nac;
     const int* cam_ac = pl.cam_ac.data();
     // CSR of admissible obs by original point index, each list ordered by (active camera, obs index): the order
     // of a stable sort by active camera of the obs in index order
     std::vector<int> pptr(np + 1, 0);
     for (int i = 0; i < np; ++i) pptr[i + 1] = pptr[i] + pl.pt_cnt[i];
     std::vector<int> plist(n_adm);
+    // one pass over the observations fills both: the point lists (atomic slots, sorted below) and the camera-major
+    // order (one segment per camera with admissible obs, gauge included; each camera's in index order), a counting
+    // scatter whose per-range offsets come from plan_count's per-range camera counts over the same ranges
+    std::vector<int> cstart(nc + 1, 0);
+    for (int i = 0; i < nc; ++i) cstart[i + 1] = cstart[i] + pl.cam_cnt[i];
+    pl.co_orig.resize(n_adm);
+    pl.co_dest.resize(no);
+    pl.po_dest.resize(no);  // the admissible entries in the point-major pass below
     {
         std::vector<int> cur(pptr.begin(), pptr.end() - 1);
         int* cp = cur.data();
-        const int T = n_tasks(no, 65536);
+        const int T = pl.obs_tasks;
         const Split sp{no, T};
+        std::vector<int> off(pl.task_cam);
+        {
+            std::vector<int> run(cstart.begin(), cstart.end() - 1);
+            for (int t = 0; t < T; ++t)
+                for (int i = 0; i < nc; ++i) {
+                    int& o = off[(size_t)t * nc + i];
+                    const int v = o;
+                    o = run[i];
+                    run[i] += v;
+                }
+        }
         host_parallel(T, [&](int t) {
+            int* c = off.data() + (size_t)t * nc;
             for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k)
-                if (pl.adm[k]) plist[__atomic_fetch_add(cp + in.obs_pt[k], 1, __ATOMIC_RELAXED)] = (int)k;
+                if (pl.adm[k]) {
+                    plist[__atomic_fetch_add(cp + in.obs_pt[k], 1, __ATOMIC_RELAXED)] = (int)k;
+                    const int q = c[in.obs_cam[k]]++;
+                    pl.co_orig[q] = (int)k;
+                    pl.co_dest[k] = q;
+                } else {
+                    pl.co_dest[k] = -1;
+                    pl.po_dest[k] = -1;
+                }
         });
     }
-    tm.mark("point_lists");
+    tm.mark("point_camera_lists");
     pl.pmin.assign(np, INT_MAX);
     pl.pmax.assign(np, -1);
     std::vector<signed char> pclass(np, -1);  // 0 tiled, 1 overflow (Schur via atomics), 2 gauge-only
+    // envelope of S: fc[a] = first co-visible active camera of active camera a (the min over the first cameras of
+    // the points it observes), gathered from each point's sorted list
+    pl.fc.resize(nac);
+    for (int a = 0; a < nac; ++a) pl.fc[a] = a;
     {
         const int T = n_tasks(np, 8192);
         const Split sp{np, T};
+        std::vector<int> floc((size_t)T * std::max(nac, 1), INT_MAX);
         host_parallel(T, [&](int t) {
             std::vector<long long> key;
+            int* f = floc.data() + (size_t)t * std::max(nac, 1);
             for (long long i = sp.lo(t); i < sp.lo(t + 1); ++i) {
                 const int b = pptr[i], e = pptr[i + 1];
                 if (e == b) continue;
@@ -262,10 +383,16 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
                 if (hi < 0) pclass[i] = 2;
                 else if (dup || hi - lo + 1 > pp.tile_win || m > pp.chunk_obs) pclass[i] = 1;
                 else pclass[i] = 0;
+                for (int q = 0; q < m; ++q) {
+                    const int a = (int)(key[q] >> 32) - 1;
+                    if (a >= 0) f[a] = std::min(f[a], lo);
+                }
             }
         });
+        for (int t = 0; t < T; ++t)
+            for (int a = 0; a < nac; ++a) pl.fc[a] = std::min(pl.fc[a], floc[(size_t)t * nac + a]);
     }
-    tm.mark("point_sort_class");
+    tm.mark("point_sort_class_fc");
     // points by class; tiled and overflow points by first camera, ties in point order (a stable counting sort)
     std::vector<int> cls[3];
     {
@@ -286,41 +413,10 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
             else if (pclass[i] == 2) cls[2].push_back(i);
         }
     }
-    // tiles over the tiled points: window [base, base + span), span <= tile_win, <= tile_pts points; chunks of
-    // <= chunk_pts points and <= chunk_obs observations. tile_pts spreads the points over one wave of resident
-    // workgroups (no second, partly empty wave of tiles), grown until the tile count fits the resident slots.
-    const std::vector<int>& T0 = cls[0];
-    auto build_tiles = [&](int tile_pts) {
-        pl.tile_chunk.assign(1, 0); pl.tile_base.clear(); pl.tile_span.clear(); pl.chunk_ap.assign(1, 0);
-        const int n0 = (int)T0.size();
-        int i = 0;
-        while (i < n0) {
-            const int base = pl.pmin[T0[i]];
-            int j = i, hi = base;
-            while (j < n0 && j - i < tile_pts && pl.pmax[T0[j]] - base < pp.tile_win) { hi = std::max(hi, pl.pmax[T0[j]]); ++j; }
-            int c0 = i;
-            while (c0 < j) {
-                int c1 = c0, nob = 0;
-                while (c1 < j && c1 - c0 < pp.chunk_pts && nob + pl.pt_cnt[T0[c1]] <= pp.chunk_obs) { nob += pl.pt_cnt[T0[c1]]; ++c1; }
-                pl.chunk_ap.push_back(c1);
-                c0 = c1;
-            }
-            pl.tile_chunk.push_back((int)pl.chunk_ap.size() - 1);
-            pl.tile_base.push_back(base);
-            pl.tile_span.push_back(hi - base + 1);
-            i = j;
-        }
-    };
     {
-        const int slots = pp.tile_slots - 1;  // one resident slot for the intrinsics-term workgroup
-        int tile_pts = 128;
-        if (slots > 0) tile_pts = std::max(pp.chunk_pts, (int)((T0.size() + slots - 1) / slots));
-        if (pp.tile_pts_env > 0) tile_pts = pp.tile_pts_env;
-        build_tiles(tile_pts);
-        for (int grow = 0; pp.tile_pts_env <= 0 && slots > 0 && (int)pl.tile_base.size() > slots && grow < 16; ++grow) {
-            tile_pts += std::max(1, tile_pts / 8);
-            build_tiles(tile_pts);
-        }
+        const std::vector<int>& T0 = cls[0];
+        build_tiles((int)T0.size(), [&](int i) { return pl.pmin[T0[i]]; }, [&](int i) { return pl.pmax[T0[i]]; },
+                    [&](int i) { return pl.pt_cnt[T0[i]]; }, pp, pl);
     }
     tm.mark("class_sort_tiles");
     // active point order: tiled (tile order), overflow, gauge-only; point-major obs in that order
@@ -332,7 +428,6 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
     pl.pt_ptr.assign(n_ap + 1, 0);
     for (int a = 0; a < n_ap; ++a) pl.pt_ptr[a + 1] = pl.pt_ptr[a] + pl.pt_cnt[pl.pt_idx[a]];
     pl.po_orig.resize(n_adm);
-    pl.po_dest.resize(no);  // admissible entries here, the others (-1) in the camera-major pass below
     {
         const int T = n_tasks(n_ap, 8192);
         const Split sp{n_ap, T};
@@ -350,90 +445,40 @@ void plan_order(const PlanInput& in, const std::vector<int>& cam_seen, const Pla
     pl.ovf_obs.clear();
     for (int q = pl.pt_ptr[pl.n_tiled]; q < pl.pt_ptr[n_ap]; ++q)
         if (cam_ac[in.obs_cam[pl.po_orig[q]]] >= 0) pl.ovf_obs.push_back(q);
-    // back-substitution chunks over all active points: <= bs_pts points and <= bs_obs observations
-    pl.bs_chunk.assign(1, 0);
-    for (int a = 0; a < n_ap;) {
-        int b = a + 1;
-        while (b < n_ap && b - a < pp.bs_pts && pl.pt_ptr[b + 1] - pl.pt_ptr[a] <= pp.bs_obs) ++b;
-        pl.bs_chunk.push_back(b);
-        a = b;
-    }
+    build_bs_chunks(n_ap, pp, pl);
     tm.mark("ovf_bs");
-    // camera-major obs (one segment per camera with admissible obs, gauge included; each camera's in index
-    // order): a two-pass counting scatter over ranges of the observations
+    build_segments(nc, cstart, pp, pl);
+    tm.mark("segments");
+}
+
+// ---------------------------------------------------------------- stage 2 from the device plan
+void plan_from_device(const int* sum, int nc, int np, int fixed_cam, const PlanParams& pp, Plan& pl) {
+    PhaseTimer tm("device");
+    pl.dev = true;
+    pl.cam_cnt.assign(sum + DP_HDR, sum + DP_HDR + nc);
+    pl.pt_cnt.clear(); pl.adm.clear(); pl.pmin.clear(); pl.pmax.clear(); pl.task_cam.clear();
+    pl.pt_idx.clear(); pl.po_orig.clear(); pl.po_dest.clear(); pl.co_orig.clear(); pl.co_dest.clear();
+    pl.ovf_obs.clear();
+    std::vector<int> cam_seen(nc);
+    for (int i = 0; i < nc; ++i) cam_seen[i] = pl.cam_cnt[i] > 0;
+    build_active_cameras(nc, cam_seen, fixed_cam, pl);
+    const int nac = pl.nac;
+    const int* fc = sum + DP_HDR + nc;
+    const int* ptp = fc + nc;
+    const int* pmm = ptp + np + 1;
+    pl.fc.assign(fc, fc + nac);
+    const int n_ap = pl.dev_nap = sum[DP_NAP];
+    pl.n_tiled = sum[DP_NTILED];
+    pl.dev_novf = sum[DP_NOVF];
+    pl.pt_ptr.assign(ptp, ptp + n_ap + 1);
+    build_tiles(pl.n_tiled, [&](int i) { return (int)((unsigned)pmm[i] >> 16); },
+                [&](int i) { return (int)((unsigned)pmm[i] & 0xffffu); }, [&](int i) { return ptp[i + 1] - ptp[i]; },
+                pp, pl);
+    build_bs_chunks(n_ap, pp, pl);
     std::vector<int> cstart(nc + 1, 0);
     for (int i = 0; i < nc; ++i) cstart[i + 1] = cstart[i] + pl.cam_cnt[i];
-    pl.co_orig.resize(n_adm);
-    pl.co_dest.resize(no);
-    {
-        const int T = n_tasks(no, 65536);
-        const Split sp{no, T};
-        std::vector<std::vector<int>> off(T);
-        host_parallel(T, [&](int t) {
-            std::vector<int>& c = off[t];
-            c.assign(nc, 0);
-            for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k)
-                if (pl.adm[k]) ++c[in.obs_cam[k]];
-        });
-        std::vector<int> run(cstart.begin(), cstart.end() - 1);
-        for (int t = 0; t < T; ++t)
-            for (int i = 0; i < nc; ++i) {
-                const int v = off[t][i];
-                off[t][i] = run[i];
-                run[i] += v;
-            }
-        host_parallel(T, [&](int t) {
-            std::vector<int>& c = off[t];
-            for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k)
-                if (pl.adm[k]) {
-                    const int q = c[in.obs_cam[k]]++;
-                    pl.co_orig[q] = (int)k;
-                    pl.co_dest[k] = q;
-                } else {
-                    pl.co_dest[k] = -1;
-                    pl.po_dest[k] = -1;
-                }
-        });
-    }
-    tm.mark("camera_major");
-    // sub-segments of <= subseg observations (one workgroup each), equal-sized within a camera; ac_seg[ac] = the
-    // sub-segment range of active camera ac (empty when this shard has no observation of it)
-    pl.seg_ptr.assign(1, 0); pl.seg_cam.clear(); pl.seg_ac.clear();
-    pl.ac_seg.assign(2 * (size_t)std::max(nac, 1), 0);
-    for (int i = 0; i < nc; ++i)
-        if (pl.cam_cnt[i] > 0) {
-            const int first = (int)pl.seg_cam.size();
-            const int cnt = pl.cam_cnt[i], nseg = (cnt + pp.subseg - 1) / pp.subseg;
-            for (int k = 1; k <= nseg; ++k) {
-                pl.seg_cam.push_back(i);
-                pl.seg_ac.push_back(cam_ac[i]);
-                pl.seg_ptr.push_back(cstart[i] + (int)(((long long)cnt * k) / nseg));
-            }
-            if (cam_ac[i] >= 0) {
-                pl.ac_seg[2 * cam_ac[i]] = first;
-                pl.ac_seg[2 * cam_ac[i] + 1] = (int)pl.seg_cam.size();
-            }
-        }
-    // envelope of S: first co-visible active camera of each active camera (min over the points' first cameras)
-    pl.fc.resize(nac);
-    for (int a = 0; a < nac; ++a) pl.fc[a] = a;
-    {
-        const int T = n_tasks(no, 65536);
-        const Split sp{no, T};
-        std::vector<std::vector<int>> loc(T);
-        host_parallel(T, [&](int t) {
-            std::vector<int>& f = loc[t];
-            f.assign(nac, INT_MAX);
-            for (long long k = sp.lo(t); k < sp.lo(t + 1); ++k) {
-                if (!pl.adm[k]) continue;
-                const int a = cam_ac[in.obs_cam[k]];
-                if (a >= 0) f[a] = std::min(f[a], pl.pmin[in.obs_pt[k]]);
-            }
-        });
-        for (int t = 0; t < T; ++t)
-            for (int a = 0; a < nac; ++a) pl.fc[a] = std::min(pl.fc[a], loc[t][a]);
-    }
-    tm.mark("segments_fc");
+    build_segments(nc, cstart, pp, pl);
+    tm.mark("tiles_chunks_segments");
 }
 
 // ---------------------------------------------------------------- stage 3

@@ -48,6 +48,8 @@ struct Plan {
     std::vector<unsigned char> adm;  // observation k admissible (depth > 1e-15)
     int n_adm = 0;
     bool obs32 = false;              // every admissible pixel and depth is exactly an f32 (DevProblem::obs32)
+    int obs_tasks = 0;               // ranges of the observation passes (the same split in plan_order)
+    std::vector<int> task_cam;       // [obs_tasks * nc] admissible observations per (range, camera)
     // ---- stage 2 (plan_order): given the active cameras (cam_seen, all shards)
     std::vector<int> cam_ac;         // camera -> active index or -1 (fixed / unobserved)
     std::vector<int> ac_cam;         // active camera -> camera
@@ -69,8 +71,33 @@ struct Plan {
     int n = 0, npad = 0, nb = 0, cam_band = 0, band_w = 0;
     std::vector<int> fcol, rptr, rows;
     std::vector<int> env_tile;       // (block row, block col) pairs, flattened
-    int n_ap() const { return (int)pt_idx.size(); }
+    // ---- device plan (plan_from_device): pt_idx, po_*, co_*, ovf_obs and cam_ac live in HBM only
+    bool dev = false;
+    int dev_nap = 0, dev_novf = 0;
+    int n_ap() const { return dev ? dev_nap : (int)pt_idx.size(); }
+    int n_ovf() const { return dev ? dev_novf : (int)ovf_obs.size(); }
 };
+
+// The device plan's read-back summary (ba_dplan.hip): a header, then cam_cnt [nc] | fc [nc] | pt_ptr [np + 1] (the
+// point-major ranges of the active points, zeros past them) | per active point in the point order: first active
+// camera << 16 | last active camera (16 bits each) [np].
+enum {
+    DP_BAD = 0,    // first out-of-range observation index (INT_MAX: none)
+    DP_NOTF32,     // (unused: the host checks obs32 while it stages the pixels)
+    DP_NADM,       // admissible observations
+    DP_NAC,        // active cameras
+    DP_NAP,        // active points (observed by an admissible observation)
+    DP_NTILED,     // tiled points (class 0)
+    DP_NOVF,       // point-major slots of overflow points on an active camera (ovf_obs)
+    DP_TOOLONG,    // a point has more than DP_LONG_MAX admissible observations (the host plan takes over)
+    DP_NLONG,      // points of more than 16 observations (sorted by one workgroup each)
+    DP_HDR = 16
+};
+inline size_t dplan_sum_ints(int nc, int np) { return (size_t)DP_HDR + 2 * (size_t)nc + 2 * (size_t)np + 1; }
+
+// the host plan's stage 2 from the device plan's summary (counts, fc, the point order's columns): active cameras,
+// pt_ptr, Schur tiles, back-substitution chunks, camera sub-segments. n_adm / obs32 / err are the caller's.
+void plan_from_device(const int* sum, int nc, int np, int fixed_cam, const PlanParams& pp, Plan& pl);
 
 // stage 1: index validation + admissibility + per-camera / per-point admissible counts
 void plan_count(const PlanInput& in, Plan& pl);

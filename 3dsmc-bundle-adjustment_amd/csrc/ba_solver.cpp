@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <climits>
 #include <cstdint>
 #include <chrono>
 #include <cmath>
@@ -24,6 +25,7 @@
 #include "../../include/ba.h"
 #include "ba_host.h"
 #include "ba_kernels.h"
+#include "ba_dplan.h"
 #include "ba_plan.h"
 
 using namespace miba;
@@ -63,6 +65,7 @@ enum BufId {
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
     B_BCR, B_CAMDATA_LOC, B_ENV_LOC, B_RED, B_PREP, B_CAMPART, B_STATE, B_LOG, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_PO_REC, B_CO_REC,
+    B_RAW_ADM, B_DP_SCRATCH, B_DP_PO_DEST, B_DP_CO_DEST, B_DP_CAM_AC, B_DP_PT_IDX, B_DP_OVF, B_DP_SUM,
     B_COUNT
 };
 
@@ -87,6 +90,13 @@ struct ba_context {
     size_t stage_cap = 0;
     char* pstage = nullptr;  // pinned staging of the parameter uploads (cameras | points | intrinsics | prior)
     size_t pstage_cap = 0;
+    hipStream_t copy_stream = nullptr;  // the device plan's pixel DMA, beside the plan passes on `stream`
+    hipEvent_t ev_idx = nullptr, ev_uv = nullptr;  // indices / depths DMA'd; pixels DMA'd
+    bool uv_pending = false;  // the pixel DMA of the last prepare has not been waited for on `stream`
+    int* rsum = nullptr;     // the device plan's summary (ba_plan.h), in mapped host memory the last pass writes
+    int* rsum_dev = nullptr; // its device address
+    size_t rsum_cap = 0;     // in ints
+    std::vector<std::pair<size_t, size_t>> plan_parts;  // (offset, ints) of each array in B_PLAN (digest)
     // plan cache (ba_options.rebuild_plan = 0): the structure key of the last full prepare; while plan_ok the
     // staging buffer's raw region holds that window's observations (the reuse check compares against it) and
     // `raw` the device gather inputs (B_RAW_* + the plan's orderings in B_PLAN)
@@ -245,6 +255,9 @@ ba_context* ba_create(const ba_options* opts) {
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_idx, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_uv, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->hprog, PROG_BYTES, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->dprog, ctx->hprog, 0);
     if (ctx->opts.profile_kernels) {
@@ -276,6 +289,13 @@ void ba_destroy(ba_context* ctx) {
     if (ctx->hres) hipHostFree(ctx->hres);
     if (ctx->stage) hipHostFree(ctx->stage);
     if (ctx->pstage) hipHostFree(ctx->pstage);
+    if (ctx->rsum) hipHostFree(ctx->rsum);
+    if (ctx->copy_stream) {
+        hipStreamSynchronize(ctx->copy_stream);
+        hipStreamDestroy(ctx->copy_stream);
+    }
+    if (ctx->ev_idx) hipEventDestroy(ctx->ev_idx);
+    if (ctx->ev_uv) hipEventDestroy(ctx->ev_uv);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -522,18 +542,52 @@ static void stage_copy(const std::vector<StageCopy>& v) {
     });
 }
 
+// The pixels into the staging buffer (host pool), checking on the way that every admissible pixel and depth is
+// exactly an f32 (the obs32 layout, DevProblem::obs32; plan_count's check for the device plan). Returns true when
+// one is not.
+static bool stage_values_f32check(double* dst_uv, double* dst_dep, const double* uv, const double* dep, size_t no) {
+    const int T = (int)std::max<size_t>(1, std::min<size_t>(4 * (size_t)host_threads(), no >> 15));
+    std::vector<unsigned char> bad(T, 0);
+    auto f32_exact = [](double v) { return (double)(float)v == v; };
+    host_parallel(T, [&](int t) {
+        const size_t lo = no * t / T, hi = no * (t + 1) / T;
+        std::memcpy(dst_uv + 2 * lo, uv + 2 * lo, 16 * (hi - lo));
+        std::memcpy(dst_dep + lo, dep + lo, 8 * (hi - lo));
+        bool ok = true;
+        for (size_t k = lo; k < hi; ++k)
+            if (dep[k] > 1e-15) ok = ok && f32_exact(uv[2 * k]) && f32_exact(uv[2 * k + 1]) && f32_exact(dep[k]);
+        bad[t] = ok ? 0 : 1;
+    });
+    for (int t = 0; t < T; ++t)
+        if (bad[t]) return true;
+    return false;
+}
+
 // The staging layout of the raw observations: obs_uv | obs_depth | obs_cam | obs_pt.
+// (+ the admissibility bytes the device plan reads instead of the depths)
 struct RawStage {
-    double* uv; double* dep; int* cam; int* pt;
+    double* uv; double* dep; int* cam; int* pt; unsigned char* adm;
     RawStage(char* sg, size_t no)
-        : uv(reinterpret_cast<double*>(sg)), dep(uv + 2 * no), cam(reinterpret_cast<int*>(dep + no)), pt(cam + no) {}
+        : uv(reinterpret_cast<double*>(sg)), dep(uv + 2 * no), cam(reinterpret_cast<int*>(dep + no)), pt(cam + no),
+          adm(reinterpret_cast<unsigned char*>(pt + no)) {}
 };
-static size_t raw_stage_bytes(size_t no) { return no * (16 + 8 + 4 + 4); }
+static size_t raw_stage_bytes(size_t no) { return no * (16 + 8 + 4 + 4 + 1); }
+
+// The device plan's inputs into the staging buffer (host pool): the indices and one admissibility byte per
+// observation (depth > 1e-15, countConstraints / the skip at OptimizationUtils.cpp:265-268).
+static void stage_indices_adm(const RawStage& rs, const ba_problem* p, size_t no) {
+    const int T = (int)std::max<size_t>(1, std::min<size_t>(4 * (size_t)host_threads(), no >> 15));
+    host_parallel(T, [&](int t) {
+        const size_t lo = no * t / T, hi = no * (t + 1) / T;
+        std::memcpy(rs.cam + lo, p->obs_cam + lo, 4 * (hi - lo));
+        std::memcpy(rs.pt + lo, p->obs_pt + lo, 4 * (hi - lo));
+        for (size_t k = lo; k < hi; ++k) rs.adm[k] = p->obs_depth[k] > 1e-15 ? 1 : 0;
+    });
+}
 
 // The window's parameters (cameras, points, intrinsics, prior) -> pinned staging -> HBM slot 0, then copied on the
 // device into the candidate and initial slots (k_reset starts every solve from the initial ones).
-static int upload_params(ba_context* ctx, const ba_problem* p) {
-    hipStream_t s = ctx->stream;
+static int upload_params(ba_context* ctx, const ba_problem* p, hipStream_t s) {
     const size_t nc = p->n_cams, np = p->n_points;
     const size_t bytes = 56 * nc + 24 * np + 64;
     if (ctx->pstage_cap < bytes) {
@@ -570,7 +624,7 @@ static int upload_params(ba_context* ctx, const ba_problem* p) {
 static unsigned long long env_key() {
     static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
                                         "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED", "MIBA_SW", "MIBA_FPL",
-                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES"};
+                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES", "MIBA_DEVICE_PLAN"};
     unsigned long long h = 1469598103934665603ull;
     for (const char* n : names) {
         const char* v = std::getenv(n);
@@ -670,7 +724,7 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
         HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
         HIPCHECK(ctx, launch_prep_gather(ctx->P, ctx->raw, s));
     }
-    if (int rc = upload_params(ctx, p)) return rc;
+    if (int rc = upload_params(ctx, p, s)) return rc;
     // the same device state as after a full prepare: S, rhs and the partial slots cleared
     const DevProblem& P = ctx->P;
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
@@ -690,6 +744,99 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     ctx->prepared = true;
     ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;
     return 1;
+}
+
+// MIBA_DEVICE_PLAN: 0 = the host plan; 1 = the device plan whenever the window fits it; unset = the device plan on
+// windows of >= DPLAN_MIN_OBS observations (below, the host plan's passes cost less than the device plan's launches)
+static constexpr int DPLAN_MIN_OBS = 100000;
+static bool want_dplan(int nc, int np, int no) {
+    const char* e = std::getenv("MIBA_DEVICE_PLAN");
+    if (e && e[0] == '0') return false;
+    if (!dplan_fits(no, np, nc)) return false;
+    return (e && e[0] == '1') || no >= DPLAN_MIN_OBS;
+}
+
+// The device plan's prepare: the indices and admissibility bytes staged and DMA'd first; the plan's passes
+// enqueued behind them (the last one writes the summary into mapped host memory, no DMA engine involved); the
+// depths, pixels (obs32 checked on the way) and parameters staged meanwhile and DMA'd on the copy stream; then one
+// wait for the passes. ok = false: a point list longer than the device sort takes, or a scan that did not settle
+// (the host plan builds the window instead; the staged upload stands).
+static int run_dplan(ba_context* ctx, const ba_problem* p, int nc, int np, int no, bool& notf32, bool& ok) {
+    hipStream_t s = ctx->stream;
+    if (ctx->uv_pending) {  // a prepare that failed after its value DMA: the staging buffer is still read
+        HIPCHECK(ctx, hipEventSynchronize(ctx->ev_uv));
+        ctx->uv_pending = false;
+    }
+    if (int rc = stage_ensure(ctx, raw_stage_bytes((size_t)no), 0)) return rc;
+    RawStage rs(ctx->stage, (size_t)no);
+    HIPCHECK(ctx, ctx->buf[B_RAW_UV].ensure(16 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_RAW_DEP].ensure(8 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_RAW_CAM].ensure(4 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_RAW_PT].ensure(4 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_RAW_ADM].ensure((size_t)no));
+    const bool times = std::getenv("MIBA_PLAN_TIMES") != nullptr;  // diagnostic: host phases of the device plan
+    double tm = now_ms();
+    auto mark = [&](const char* what) {
+        if (!times) return;
+        const double t = now_ms();
+        std::fprintf(stderr, "dplan %s %.3f ms\n", what, t - tm);
+        tm = t;
+    };
+    stage_indices_adm(rs, p, (size_t)no);
+    mark("stage_indices");
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, rs.cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_PT].p, rs.pt, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_ADM].p, rs.adm, (size_t)no, hipMemcpyHostToDevice, s));
+    HIPCHECK(ctx, hipEventRecord(ctx->ev_idx, s));
+    const size_t nsum = dplan_sum_ints(nc, np);
+    HIPCHECK(ctx, ctx->buf[B_DP_SCRATCH].ensure(4 * dplan_scratch_ints(no, np, nc)));
+    HIPCHECK(ctx, ctx->buf[B_DP_PO_DEST].ensure(4 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_DP_CO_DEST].ensure(4 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_DP_CAM_AC].ensure(4 * (size_t)nc));
+    HIPCHECK(ctx, ctx->buf[B_DP_PT_IDX].ensure(4 * (size_t)np));
+    HIPCHECK(ctx, ctx->buf[B_DP_OVF].ensure(4 * (size_t)no));
+    HIPCHECK(ctx, ctx->buf[B_DP_SUM].ensure(4 * nsum));
+    if (ctx->rsum_cap < nsum) {
+        if (ctx->rsum) HIPCHECK(ctx, hipHostFree(ctx->rsum));
+        ctx->rsum = nullptr;
+        ctx->rsum_dev = nullptr;
+        ctx->rsum_cap = 0;
+        const size_t want = nsum + nsum / 8 + 64;
+        HIPCHECK(ctx, hipHostMalloc((void**)&ctx->rsum, 4 * want, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHECK(ctx, hipHostGetDevicePointer((void**)&ctx->rsum_dev, ctx->rsum, 0));
+        ctx->rsum_cap = want;
+    }
+    DPlanArgs a{};
+    a.cam = ctx->buf[B_RAW_CAM].as<int>();
+    a.pt = ctx->buf[B_RAW_PT].as<int>();
+    a.adm = ctx->buf[B_RAW_ADM].as<unsigned char>();
+    a.no = no; a.np = np; a.nc = nc; a.fixed_cam = p->fixed_cam;
+    a.tile_win = TILE_WIN; a.chunk_obs = CHUNK_OBS;
+    a.po_dest = ctx->buf[B_DP_PO_DEST].as<int>();
+    a.co_dest = ctx->buf[B_DP_CO_DEST].as<int>();
+    a.cam_ac = ctx->buf[B_DP_CAM_AC].as<int>();
+    a.pt_idx = ctx->buf[B_DP_PT_IDX].as<int>();
+    a.ovf_obs = ctx->buf[B_DP_OVF].as<int>();
+    a.sum = ctx->buf[B_DP_SUM].as<int>();
+    a.sum_host = ctx->rsum_dev;
+    a.scratch = ctx->buf[B_DP_SCRATCH].as<int>();
+    HIPCHECK(ctx, dplan_enqueue(a, s));
+    mark("enqueue");
+    // host work while the passes run: the values (behind the index DMA on the copy stream) and the parameters
+    notf32 = stage_values_f32check(rs.uv, rs.dep, p->obs_uv, p->obs_depth, (size_t)no);
+    mark("stage_values");
+    hipStream_t cs = ctx->copy_stream;
+    HIPCHECK(ctx, hipStreamWaitEvent(cs, ctx->ev_idx, 0));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, cs));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, rs.uv, 16 * (size_t)no, hipMemcpyHostToDevice, cs));
+    if (int rc = upload_params(ctx, p, cs)) return rc;
+    HIPCHECK(ctx, hipEventRecord(ctx->ev_uv, cs));
+    ctx->uv_pending = true;
+    mark("params");
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    mark("sync");
+    ok = ctx->rsum[DP_TOOLONG] == 0;
+    return BA_OK;
 }
 
 static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
@@ -730,23 +877,33 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     // the raw observations -> pinned staging -> HBM, in flight while the host builds the plan (landmark shards:
     // after the local count, its errors into the verdict)
     const size_t raw_bytes = raw_stage_bytes((size_t)no);
+    // the device plan (unsharded windows that fit it)
+    bool dplan = !shard && !verdict[0] && want_dplan(nc, np, no);
+    bool notf32 = false;
     auto stage_raw = [&]() -> int {
         if (no <= 0) return BA_OK;
+        if (ctx->uv_pending) {  // a prepare that failed after its pixel DMA: the staging buffer is still read
+            HIPCHECK(ctx, hipEventSynchronize(ctx->ev_uv));
+            ctx->uv_pending = false;
+        }
         if (int rc = stage_ensure(ctx, raw_bytes, 0)) return rc;
         RawStage rs(ctx->stage, (size_t)no);
-        stage_copy({{rs.uv, p->obs_uv, 16 * (size_t)no}, {rs.dep, p->obs_depth, 8 * (size_t)no},
-                    {rs.cam, p->obs_cam, 4 * (size_t)no}, {rs.pt, p->obs_pt, 4 * (size_t)no}});
         HIPCHECK(ctx, ctx->buf[B_RAW_UV].ensure(16 * (size_t)no));
         HIPCHECK(ctx, ctx->buf[B_RAW_DEP].ensure(8 * (size_t)no));
         HIPCHECK(ctx, ctx->buf[B_RAW_CAM].ensure(4 * (size_t)no));
         HIPCHECK(ctx, ctx->buf[B_RAW_PT].ensure(4 * (size_t)no));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, rs.uv, 16 * (size_t)no, hipMemcpyHostToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, rs.cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_PT].p, rs.pt, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+        {
+            stage_copy({{rs.uv, p->obs_uv, 16 * (size_t)no}, {rs.dep, p->obs_depth, 8 * (size_t)no},
+                        {rs.cam, p->obs_cam, 4 * (size_t)no}, {rs.pt, p->obs_pt, 4 * (size_t)no}});
+            HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, rs.uv, 16 * (size_t)no, hipMemcpyHostToDevice, s));
+            HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, s));
+            HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, rs.cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+            HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_PT].p, rs.pt, 4 * (size_t)no, hipMemcpyHostToDevice, s));
+        }
         return BA_OK;
     };
-    if (!shard && !verdict[0])
+    // the device plan stages and uploads the window itself (run_dplan, below)
+    if (!shard && !verdict[0] && !dplan)
         if (int rc = stage_raw()) return rc;
     const double tp_raw = now_ms();
     Plan& pl = ctx->plan;
@@ -759,7 +916,23 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         const char* e = std::getenv("MIBA_OBS32");
         if (!(e && e[0] == '0')) in.obs_uv = p->obs_uv;
     }
-    plan_count(in, pl);
+    // the device plan: its passes run behind the index / depth upload, the parameters are staged meanwhile, one
+    // read-back (the window's values are valid: a malformed window fails below, before any of them is used)
+    bool params_up = false;
+    if (dplan) {
+        if (int rc = run_dplan(ctx, p, nc, np, no, notf32, dplan)) return rc;
+        params_up = true;
+    }
+    ctx->pinfo.plan_device = dplan ? 1 : 0;
+    if (dplan) {
+        const int* sm = ctx->rsum;
+        pl.err = sm[DP_BAD] != INT_MAX ? "observation index out of range" : "";
+        pl.n_adm = sm[DP_NADM];
+        pl.obs32 = in.obs_uv != nullptr && !notf32;
+        pl.cam_cnt.assign(sm + DP_HDR, sm + DP_HDR + nc);
+    } else {
+        plan_count(in, pl);
+    }
     if (!verdict[0] && !pl.err.empty()) { local_err = pl.err; verdict[0] = 1; }
     int local_rc = BA_OK;
     if (shard) {
@@ -803,7 +976,8 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     // 34.2 us at 1700 vs 36.1 at 1024, 42.7 at 512, 34.7 at 2500); MIBA_SUBSEG overrides (tuning)
     pp.subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : SUBSEG_OBS;
     if (const char* e = std::getenv("MIBA_SUBSEG")) pp.subseg = std::max(64, std::atoi(e));
-    plan_order(in, cam_seen, pp, pl);
+    if (dplan) plan_from_device(ctx->rsum, nc, np, in.fixed_cam, pp, pl);
+    else plan_order(in, cam_seen, pp, pl);
     const int nac = pl.nac;
     if (shard) {  // envelope / band of the summed S: union over the shards
         const int rc = host_allreduce_i32(ctx, pl.fc.data(), nac, COMM_MIN);
@@ -833,16 +1007,19 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             }
         }
         // ---- uploads: the plan's index arrays in one staged DMA (each array 256-byte aligned in B_PLAN)
-        struct Part { const int* src; size_t n; size_t off; };
+        // (device plan: po_dest, co_dest, pt_idx and ovf_obs are copied on the device into their slots)
+        struct Part { const int* src; size_t n; size_t off; const int* dev; };
+        auto dv = [&](int id) -> const int* { return pl.dev ? ctx->buf[id].as<int>() : nullptr; };
         std::vector<Part> parts = {
-            {pl.po_dest.data(), (size_t)no, 0}, {pl.co_dest.data(), (size_t)no, 0}, {pl.cam_ac.data(), (size_t)nc, 0},
-            {pl.pt_ptr.data(), (size_t)n_ap + 1, 0}, {pl.pt_idx.data(), (size_t)n_ap, 0},
+            {pl.po_dest.data(), (size_t)no, 0, dv(B_DP_PO_DEST)}, {pl.co_dest.data(), (size_t)no, 0, dv(B_DP_CO_DEST)},
+            {pl.cam_ac.data(), (size_t)nc, 0, nullptr},
+            {pl.pt_ptr.data(), (size_t)n_ap + 1, 0, nullptr}, {pl.pt_idx.data(), (size_t)n_ap, 0, dv(B_DP_PT_IDX)},
             {pl.seg_ptr.data(), pl.seg_ptr.size(), 0}, {pl.seg_cam.data(), pl.seg_cam.size(), 0},
             {pl.seg_ac.data(), pl.seg_ac.size(), 0}, {pl.ac_seg.data(), pl.ac_seg.size(), 0},
             {pl.ac_cam.data(), (size_t)nac, 0}, {pl.fcol.data(), (size_t)nb, 0},
             {pl.tile_chunk.data(), pl.tile_chunk.size(), 0}, {pl.tile_base.data(), pl.tile_base.size(), 0},
             {pl.tile_span.data(), pl.tile_span.size(), 0}, {pl.chunk_ap.data(), pl.chunk_ap.size(), 0},
-            {pl.bs_chunk.data(), pl.bs_chunk.size(), 0}, {pl.ovf_obs.data(), pl.ovf_obs.size(), 0},
+            {pl.bs_chunk.data(), pl.bs_chunk.size(), 0}, {pl.ovf_obs.data(), (size_t)pl.n_ovf(), 0, dv(B_DP_OVF)},
             {pl.rptr.data(), (size_t)nb + 1, 0}, {pl.rows.data(), pl.rows.size(), 0},
             {pl.env_tile.data(), pl.env_tile.size(), 0}, {trange.data(), trange.size(), 0}};
         enum { PO_DEST, CO_DEST, CAM_AC, PT_PTR, PT_IDX, SEG_PTR, SEG_CAM, SEG_AC, AC_SEG, AC_CAM, FCOL, TILE_CHUNK,
@@ -861,14 +1038,23 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         {
             std::vector<StageCopy> cp;
             for (const Part& q : parts)
-                if (q.n) cp.push_back({sp + q.off, q.src, 4 * q.n});
+                if (q.n && !q.dev) cp.push_back({sp + q.off, q.src, 4 * q.n});
             stage_copy(cp);
         }
         HIPCHECK(ctx, ctx->buf[B_PLAN].ensure(4 * plan_ints));
-        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_PLAN].p, sp, 4 * plan_ints, hipMemcpyHostToDevice, s));
         int* dp = ctx->buf[B_PLAN].as<int>();
+        {  // device plan: from the first host part on (po_dest / co_dest lead and come device-to-device)
+            const size_t lo = pl.dev ? parts[CAM_AC].off : 0;
+            HIPCHECK(ctx, hipMemcpyAsync(dp + lo, sp + lo, 4 * (plan_ints - lo), hipMemcpyHostToDevice, s));
+        }
+        ctx->plan_parts.clear();
+        for (const Part& q : parts) {
+            ctx->plan_parts.emplace_back(q.off, q.n);
+            if (q.n && q.dev) HIPCHECK(ctx, hipMemcpyAsync(dp + q.off, q.dev, 4 * q.n, hipMemcpyDeviceToDevice, s));
+        }
         auto dptr = [&](int k) { return dp + parts[k].off; };
-        if (int rc = upload_params(ctx, p)) return rc;
+        if (!params_up)
+            if (int rc = upload_params(ctx, p, s)) return rc;
         // the observation layouts, gathered on the device from the raw window and the plan's orderings
         // ... in ONE layout: the 16-byte records on obs32 windows, the f64 arrays otherwise (the index arrays always)
         HIPCHECK(ctx, ctx->buf[B_PO_AC].ensure(4 * std::max<size_t>(n_adm, 1)));
@@ -888,7 +1074,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->ac_cam = pl.ac_cam;
         ctx->pt_idx = pl.pt_idx;
         const std::vector<int>& tile_base = pl.tile_base;
-        const std::vector<int>& ovf_obs = pl.ovf_obs;
+
         const int nblk_pt = pp_blocks(n_ap, PP_LANES_MAX);  // part slots sized for the widest lane grouping
         // (+ the small-window launch's per-tile and non-tiled point partials, §3 of DESIGN)
         const int part_stride = std::max({nblk_pt, (nac + 1 + 255) / 256, n_bs_chunks, (nac + BCR_CAMS - 1) / BCR_CAMS,
@@ -949,7 +1135,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         P.ovf_obs = dptr(OVF_OBS);
         P.bs_chunk = dptr(BS_CHUNK);
         P.n_bs_chunks = n_bs_chunks;
-        P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = (int)ovf_obs.size();
+        P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = pl.n_ovf();
         P.n_tiled_pts = n_tiled;
         ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
         P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
@@ -966,6 +1152,10 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             R.co_dest = dptr(CO_DEST);
             R.n_obs = no;
             ctx->raw = R;
+            if (ctx->uv_pending) {  // the device plan's pixel DMA (copy stream)
+                HIPCHECK(ctx, hipStreamWaitEvent(s, ctx->ev_uv, 0));
+                ctx->uv_pending = false;
+            }
             HIPCHECK(ctx, launch_prep_gather(P, R, s));
         }
         P.part_stride = part_stride;
@@ -1538,8 +1728,12 @@ extern "C" int32_t ba_debug_linearize(ba_context* ctx, const ba_problem* p, doub
     if (jcam) std::memset(jcam, 0, sizeof(double) * 18 * no);
     if (jpt) std::memset(jpt, 0, sizeof(double) * 9 * no);
     if (jint) std::memset(jint, 0, sizeof(double) * 8 * no);
-    for (size_t q = 0; q < na; ++q) {
-        const size_t k = ctx->plan.po_orig[q];
+    // original index -> point-major slot (the plan's po_dest, on the device for both plans)
+    std::vector<int> pdest(no);
+    if (no) HIPCHECK(ctx, hipMemcpy(pdest.data(), ctx->raw.po_dest, sizeof(int) * no, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < no; ++k) {
+        if (pdest[k] < 0) continue;
+        const size_t q = pdest[k];
         if (res) std::memcpy(res + 3 * k, &r[3 * q], sizeof(double) * 3);
         if (jcam) std::memcpy(jcam + 18 * k, &jc[18 * q], sizeof(double) * 18);
         if (jpt) std::memcpy(jpt + 9 * k, &jp[9 * q], sizeof(double) * 9);
@@ -1621,4 +1815,24 @@ extern "C" int32_t ba_kernel_stats(const ba_context* ctx, ba_kernel_stat* out, i
 extern "C" void ba_reset_kernel_stats(ba_context* ctx) {
     if (!ctx) return;
     for (int k = 0; k < K_COUNT; ++k) { ctx->k_launches[k] = 0; ctx->k_ms[k] = 0; }
+}
+
+extern "C" int32_t ba_debug_plan_digest(ba_context* ctx, uint64_t* out, int32_t max_n) {
+    if (!ctx || !ctx->prepared) return BA_E_INVALID;
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    const int n = (int)ctx->plan_parts.size();
+    for (int k = 0; k < n && k < max_n; ++k) {
+        const auto [off, len] = ctx->plan_parts[k];
+        std::vector<int32_t> v(len);
+        if (len)
+            HIPCHECK(ctx, hipMemcpy(v.data(), ctx->buf[B_PLAN].as<int>() + off, sizeof(int32_t) * len,
+                                    hipMemcpyDeviceToHost));
+        uint64_t h = 1469598103934665603ull;
+        for (int32_t x : v)
+            for (int b = 0; b < 4; ++b) h = (h ^ ((uint32_t)x >> (8 * b) & 0xffu)) * 1099511628211ull;
+        h = (h ^ (uint64_t)len) * 1099511628211ull;
+        out[k] = h;
+    }
+    return n;
 }

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MIBA_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libm
 EXPORTS = (
     "ba_api_version", "ba_build_info", "ba_default_options", "ba_create", "ba_destroy", "ba_last_error", "ba_set_options",
     "ba_solve", "ba_prepare", "ba_solve_prepared", "ba_kernel_stats", "ba_reset_kernel_stats",
-    "ba_debug_linearize", "ba_debug_reduced_system", "ba_debug_camera_sums", "ba_comm_unique_id", "ba_comm_init", "ba_comm_init_host",
+    "ba_debug_linearize", "ba_debug_reduced_system", "ba_debug_camera_sums", "ba_debug_plan_digest", "ba_comm_unique_id", "ba_comm_init", "ba_comm_init_host",
     "ba_iteration_log", "ba_last_prepare",
     "ba_problem_write", "ba_problem_read_dims", "ba_problem_read", "ba_bal_read_dims", "ba_bal_read", "ba_bal_write",
 )
@@ -71,6 +71,8 @@ def lib():
     L.ba_debug_camera_sums.argtypes = [C.c_void_p, C.POINTER(BaProblem), C.POINTER(C.c_int32), dp, dp,
                                        C.POINTER(C.c_int32)]
     L.ba_debug_camera_sums.restype = C.c_int32
+    L.ba_debug_plan_digest.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
+    L.ba_debug_plan_digest.restype = C.c_int32
     L.ba_comm_unique_id.argtypes = [C.c_char_p]
     L.ba_comm_unique_id.restype = C.c_int32
     L.ba_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]

@@ -139,6 +139,7 @@ class BaPrepareInfo(C.Structure):
         ("upload_ms", C.c_double),
         ("total_ms", C.c_double),
         ("lin_path", C.c_int32),
+        ("plan_device", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

@@ -137,6 +137,14 @@ class Solver:
         self._check(self._L.ba_solve_prepared(self._h, C.byref(ps), C.byref(s)), "ba_solve_prepared")
         return s.as_dict()
 
+    def plan_digest(self) -> list:
+        """ba_debug_plan_digest(): one FNV-1a digest per plan array of the last prepared window (as in HBM)."""
+        buf = (C.c_uint64 * 64)()
+        n = self._L.ba_debug_plan_digest(self._h, buf, 64)
+        if n < 0:
+            self._check(n, "ba_debug_plan_digest")
+        return [int(buf[k]) for k in range(min(n, 64))]
+
     def last_prepare(self) -> dict:
         """ba_last_prepare(): whether the last prepare reused the plan, uploaded observations, its phase times and
         the reduced-solve path (bcr_path)."""

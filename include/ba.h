@@ -198,6 +198,7 @@ typedef struct ba_prepare_info {
     int32_t lin_path;        /* linearisation of the LM loop: 1 = small window, the point side inside the Schur
                                 tiles and the camera side in the Schur launch (no separate linearisation launch);
                                 0 = a linearisation launch before the Schur launch */
+    int32_t plan_device;     /* 1: the window's plan passes ran on the device (MIBA_DEVICE_PLAN; 0 on a reuse) */
 } ba_prepare_info;
 int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info);
 
@@ -276,6 +277,11 @@ int32_t ba_debug_reduced_system(ba_context* ctx, const ba_problem* prob, double 
  * + prior); ac_cam[nac]: the camera index of each active camera. With NULL outputs only *nac is set. */
 int32_t ba_debug_camera_sums(ba_context* ctx, const ba_problem* prob, int32_t* nac, double* camdata,
                              double* lin, int32_t* ac_cam);
+
+/* Test hook: FNV-1a digests of the last prepared window's plan arrays as the kernels read them from HBM (the
+ * observation orderings, point order, tiles, chunks, segments, envelope), one per array, into out[max_n].
+ * Returns the number of arrays. The host plan and the device plan (MIBA_DEVICE_PLAN) give the same digests. */
+int32_t ba_debug_plan_digest(ba_context* ctx, uint64_t* out, int32_t max_n);
 
 #ifdef __cplusplus
 }
