@@ -546,7 +546,7 @@ static void stage_copy(const std::vector<StageCopy>& v) {
 // exactly an f32 (the obs32 layout, DevProblem::obs32; plan_count's check for the device plan). Returns true when
 // one is not.
 static bool stage_values_f32check(double* dst_uv, double* dst_dep, const double* uv, const double* dep, size_t no) {
-    const int T = (int)std::max<size_t>(1, std::min<size_t>(4 * (size_t)host_threads(), no >> 15));
+    const int T = (int)std::max<size_t>(1, std::min<size_t>(4 * (size_t)host_threads(), no >> 12));
     std::vector<unsigned char> bad(T, 0);
     auto f32_exact = [](double v) { return (double)(float)v == v; };
     host_parallel(T, [&](int t) {
@@ -746,9 +746,30 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     return 1;
 }
 
+// The plan's tiling / chunking parameters (n_adm: this shard's admissible observations).
+static PlanParams plan_params(int n_adm) {
+    PlanParams pp;
+    pp.tile_win = TILE_WIN;
+    pp.chunk_pts = CHUNK_PTS;
+    pp.chunk_obs = CHUNK_OBS;
+    pp.tile_slots = schur_tile_slots();
+    if (const char* e = std::getenv("MIBA_TILE_PTS")) pp.tile_pts_env = std::max(1, std::atoi(e));
+    pp.bs_pts = BS_PTS;
+    pp.bs_obs = BS_OBS;
+    // sub-segment size: ~6.5 observations per thread on large windows (C4 rocprof, fused linearisation:
+    // 34.2 us at 1700 vs 36.1 at 1024, 42.7 at 512, 34.7 at 2500); MIBA_SUBSEG overrides (tuning)
+    pp.subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : SUBSEG_OBS;
+    if (const char* e = std::getenv("MIBA_SUBSEG")) pp.subseg = std::max(64, std::atoi(e));
+    return pp;
+}
+
 // MIBA_DEVICE_PLAN: 0 = the host plan; 1 = the device plan whenever the window fits it; unset = the device plan on
-// windows of >= DPLAN_MIN_OBS observations (below, the host plan's passes cost less than the device plan's launches)
-static constexpr int DPLAN_MIN_OBS = 100000;
+// windows of >= DPLAN_MIN_OBS observations (prepare, host vs device plan: C1, 1.6k observations, 0.15 vs 0.21 ms;
+// C3, 8k, 0.26 vs 0.23-0.37; C2, 50k, 0.87 vs 0.31-0.34; C4, 1M, 2.8 vs 1.3-1.5)
+static constexpr int DPLAN_MIN_OBS = 16384;
+// windows from which a helper thread builds the host side of the plan while the values are staged (below, the
+// thread costs more than the overlap saves)
+static constexpr int DPLAN_HELPER_OBS = 262144;
 static bool want_dplan(int nc, int np, int no) {
     const char* e = std::getenv("MIBA_DEVICE_PLAN");
     if (e && e[0] == '0') return false;
@@ -761,8 +782,18 @@ static bool want_dplan(int nc, int np, int no) {
 // depths, pixels (obs32 checked on the way) and parameters staged meanwhile and DMA'd on the copy stream; then one
 // wait for the passes. ok = false: a point list longer than the device sort takes, or a scan that did not settle
 // (the host plan builds the window instead; the staged upload stands).
-static int run_dplan(ba_context* ctx, const ba_problem* p, int nc, int np, int no, bool& notf32, bool& ok) {
+static int run_dplan(ba_context* ctx, const ba_problem* p, int nc, int np, int no, bool& notf32, bool& ok,
+                     bool& built) {
     hipStream_t s = ctx->stream;
+    built = false;
+    const bool times = std::getenv("MIBA_PLAN_TIMES") != nullptr;  // diagnostic: host phases of the device plan
+    double tm = now_ms();
+    auto mark = [&](const char* what) {
+        if (!times) return;
+        const double t = now_ms();
+        std::fprintf(stderr, "dplan %s %.3f ms\n", what, t - tm);
+        tm = t;
+    };
     if (ctx->uv_pending) {  // a prepare that failed after its value DMA: the staging buffer is still read
         HIPCHECK(ctx, hipEventSynchronize(ctx->ev_uv));
         ctx->uv_pending = false;
@@ -774,14 +805,7 @@ static int run_dplan(ba_context* ctx, const ba_problem* p, int nc, int np, int n
     HIPCHECK(ctx, ctx->buf[B_RAW_CAM].ensure(4 * (size_t)no));
     HIPCHECK(ctx, ctx->buf[B_RAW_PT].ensure(4 * (size_t)no));
     HIPCHECK(ctx, ctx->buf[B_RAW_ADM].ensure((size_t)no));
-    const bool times = std::getenv("MIBA_PLAN_TIMES") != nullptr;  // diagnostic: host phases of the device plan
-    double tm = now_ms();
-    auto mark = [&](const char* what) {
-        if (!times) return;
-        const double t = now_ms();
-        std::fprintf(stderr, "dplan %s %.3f ms\n", what, t - tm);
-        tm = t;
-    };
+    mark("buffers");
     stage_indices_adm(rs, p, (size_t)no);
     mark("stage_indices");
     HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_CAM].p, rs.cam, 4 * (size_t)no, hipMemcpyHostToDevice, s));
@@ -822,19 +846,50 @@ static int run_dplan(ba_context* ctx, const ba_problem* p, int nc, int np, int n
     a.scratch = ctx->buf[B_DP_SCRATCH].as<int>();
     HIPCHECK(ctx, dplan_enqueue(a, s));
     mark("enqueue");
+    // a helper thread waits for the passes and builds the host side of the plan (tiles, chunks, segments) from the
+    // summary while this thread stages the values and parameters
+    hipError_t helper_err = hipSuccess;
+    auto build_host_side = [&]() {
+        helper_err = hipStreamSynchronize(s);
+        const int* sm = ctx->rsum;
+        if (helper_err == hipSuccess && sm[DP_TOOLONG] == 0 && sm[DP_BAD] == INT_MAX) {
+            plan_from_device(sm, nc, np, p->fixed_cam, plan_params(sm[DP_NADM]), ctx->plan);
+            built = true;
+        }
+    };
+    std::thread helper;
+    if (no >= DPLAN_HELPER_OBS) helper = std::thread(build_host_side);
+    struct Join {
+        std::thread& t;
+        ~Join() { if (t.joinable()) t.join(); }
+    } join{helper};
     // host work while the passes run: the values (behind the index DMA on the copy stream) and the parameters
-    notf32 = stage_values_f32check(rs.uv, rs.dep, p->obs_uv, p->obs_depth, (size_t)no);
-    mark("stage_values");
     hipStream_t cs = ctx->copy_stream;
     HIPCHECK(ctx, hipStreamWaitEvent(cs, ctx->ev_idx, 0));
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].p, rs.dep, 8 * (size_t)no, hipMemcpyHostToDevice, cs));
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].p, rs.uv, 16 * (size_t)no, hipMemcpyHostToDevice, cs));
+    // the values in pieces, each DMA'd while the next is staged (the copies and the DMA share the host's memory
+    // bandwidth: same-box A/B, prepare ms at 1 / 2 / 4 / 8 pieces: C4 1.28-1.59 / 1.29-1.37 / 1.26-1.28 /
+    // 1.36-1.42, C5 7.44 / 5.10 / 5.78 / 6.33); MIBA_VALUE_CHUNKS overrides
+    int nchunk = no >= (1 << 19) ? 2 : 1;
+    if (const char* e = std::getenv("MIBA_VALUE_CHUNKS")) nchunk = std::max(1, std::min(64, std::atoi(e)));
+    notf32 = false;
+    for (int c = 0; c < nchunk; ++c) {
+        const size_t lo = (size_t)no * c / nchunk, n = (size_t)no * (c + 1) / nchunk - lo;
+        if (!n) continue;
+        notf32 = stage_values_f32check(rs.uv + 2 * lo, rs.dep + lo, p->obs_uv + 2 * lo, p->obs_depth + lo, n) || notf32;
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_DEP].as<double>() + lo, rs.dep + lo, 8 * n, hipMemcpyHostToDevice,
+                                     cs));
+        HIPCHECK(ctx, hipMemcpyAsync(ctx->buf[B_RAW_UV].as<double>() + 2 * lo, rs.uv + 2 * lo, 16 * n,
+                                     hipMemcpyHostToDevice, cs));
+    }
+    mark("stage_values");
     if (int rc = upload_params(ctx, p, cs)) return rc;
     HIPCHECK(ctx, hipEventRecord(ctx->ev_uv, cs));
     ctx->uv_pending = true;
     mark("params");
-    HIPCHECK(ctx, hipStreamSynchronize(s));
-    mark("sync");
+    if (helper.joinable()) helper.join();
+    else build_host_side();
+    HIPCHECK(ctx, helper_err);
+    mark("helper");
     ok = ctx->rsum[DP_TOOLONG] == 0;
     return BA_OK;
 }
@@ -918,9 +973,9 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     }
     // the device plan: its passes run behind the index / depth upload, the parameters are staged meanwhile, one
     // read-back (the window's values are valid: a malformed window fails below, before any of them is used)
-    bool params_up = false;
+    bool params_up = false, dplan_built = false;
     if (dplan) {
-        if (int rc = run_dplan(ctx, p, nc, np, no, notf32, dplan)) return rc;
+        if (int rc = run_dplan(ctx, p, nc, np, no, notf32, dplan, dplan_built)) return rc;
         params_up = true;
     }
     ctx->pinfo.plan_device = dplan ? 1 : 0;
@@ -964,20 +1019,12 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         if (rc == BA_OK) rc = host_allreduce_i32(ctx, &n_adm_all, 1, COMM_SUM);
         if (rc != BA_OK) return rc;
     }
-    PlanParams pp;
-    pp.tile_win = TILE_WIN;
-    pp.chunk_pts = CHUNK_PTS;
-    pp.chunk_obs = CHUNK_OBS;
-    pp.tile_slots = schur_tile_slots();
-    if (const char* e = std::getenv("MIBA_TILE_PTS")) pp.tile_pts_env = std::max(1, std::atoi(e));
-    pp.bs_pts = BS_PTS;
-    pp.bs_obs = BS_OBS;
-    // sub-segment size: ~6.5 observations per thread on large windows (C4 rocprof, fused linearisation:
-    // 34.2 us at 1700 vs 36.1 at 1024, 42.7 at 512, 34.7 at 2500); MIBA_SUBSEG overrides (tuning)
-    pp.subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : SUBSEG_OBS;
-    if (const char* e = std::getenv("MIBA_SUBSEG")) pp.subseg = std::max(64, std::atoi(e));
-    if (dplan) plan_from_device(ctx->rsum, nc, np, in.fixed_cam, pp, pl);
-    else plan_order(in, cam_seen, pp, pl);
+    const PlanParams pp = plan_params(n_adm);
+    if (dplan) {
+        if (!dplan_built) plan_from_device(ctx->rsum, nc, np, in.fixed_cam, pp, pl);
+    } else {
+        plan_order(in, cam_seen, pp, pl);
+    }
     const int nac = pl.nac;
     if (shard) {  // envelope / band of the summed S: union over the shards
         const int rc = host_allreduce_i32(ctx, pl.fc.data(), nac, COMM_MIN);
@@ -989,6 +1036,14 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
     // other ranks to wait in the first LM iteration's collectives
     auto finish = [&]() -> int {
         const double tp_plan = now_ms();
+        const bool ftimes = std::getenv("MIBA_PLAN_TIMES") != nullptr;  // diagnostic: host phases of the finish
+        double ftm = tp_plan;
+        auto fmark = [&](const char* what) {
+            if (!ftimes) return;
+            const double t = now_ms();
+            std::fprintf(stderr, "finish %s %.3f ms\n", what, t - ftm);
+            ftm = t;
+        };
         const int n_ap = pl.n_ap(), n_tiled = pl.n_tiled;
         const int n = pl.n, npad = pl.npad, nb = pl.nb, band_w = pl.band_w, cam_band = pl.cam_band;
         const int n_bs_chunks = (int)pl.bs_chunk.size() - 1;
@@ -1041,6 +1096,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
                 if (q.n && !q.dev) cp.push_back({sp + q.off, q.src, 4 * q.n});
             stage_copy(cp);
         }
+        fmark("stage_plan");
         HIPCHECK(ctx, ctx->buf[B_PLAN].ensure(4 * plan_ints));
         int* dp = ctx->buf[B_PLAN].as<int>();
         {  // device plan: from the first host part on (po_dest / co_dest lead and come device-to-device)
@@ -1158,6 +1214,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             }
             HIPCHECK(ctx, launch_prep_gather(P, R, s));
         }
+        fmark("allocs_gather");
         P.part_stride = part_stride;
         P.band_w = (nb >= 2 && nb <= 2048 && band_w <= 6) ? std::max(band_w, 1) : 0;
         P.cam_band = cam_band;
@@ -1205,6 +1262,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             Bw.flags = reinterpret_cast<unsigned*>(Bw.bk + 16);  // zeroed with the workspace above
             if (int rc = bcr_setup(ctx)) return rc;
         }
+        fmark("solver_setup");
         DevWork& W = ctx->W;
         W.camdata = ctx->buf[B_CAMDATA].as<double>(); W.seg_intr = ctx->buf[B_SEGINTR].as<double>();
         W.camdata_loc = shard ? ctx->buf[B_CAMDATA_LOC].as<double>() : W.camdata;
@@ -1340,6 +1398,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             kb[K_LIN_POINT] = kb[K_CAM_SIDE] + kb[K_POINT_PREP];  // the whole linearisation pass of an accepted step
             kf[K_LIN_POINT] = kf[K_CAM_SIDE] + kf[K_POINT_PREP];
         }
+        fmark("work_accounting");
         if (std::getenv("MIBA_PREP_TIMES"))  // diagnostic: host phases of ba_prepare (the device work is still in flight)
             std::fprintf(stderr, "prepare: raw staging %.3f ms, plan %.3f ms, plan staging + enqueue %.3f ms (%d host threads)\n",
                          tp_raw - tp0, tp_plan - tp_raw, now_ms() - tp_plan, host_threads());

@@ -2,7 +2,7 @@
 
 ba_prepare's plan passes (admissibility, point lists sorted on (active camera + 1, observation index), the camera-
 major and active point orders, the Schur tiles, chunks, segments and envelope) run on the device for windows of
->= 100k observations; MIBA_DEVICE_PLAN=1 forces them on any window that fits, =0 keeps the host plan. Checked
+>= 16k observations; MIBA_DEVICE_PLAN=1 forces them on any window that fits, =0 keeps the host plan. Checked
 here, on windows that exercise every branch of the plan (shuffled and duplicate observations, inadmissible depths,
 non-f32 pixels, unobserved cameras and points, no gauge, long point lists that take the workgroup sort, a list too
 long for it that hands the window to the host plan, an out-of-range index): ba_debug_plan_digest — one FNV-1a
