@@ -32,6 +32,7 @@
 // No inter-workgroup wait anywhere: the kernel cannot time out.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -39,6 +40,7 @@
 #include "ba_device.h"
 #include "ba_kernels.h"
 #include "ba_solve_util.h"
+#include "ba_tail.h"
 
 namespace miba {
 
@@ -183,14 +185,12 @@ struct BandItem {
 };
 
 template <int BC, bool STAMP>
-__global__ __launch_bounds__(BAND_TPB) void k_bcr_band(const LmState* __restrict__ st, DevProblem P,
-                                                       const double* __restrict__ S, double* __restrict__ rhs,
-                                                       int* __restrict__ flag, BaConsts c,
-                                                       const double* __restrict__ scale,
-                                                       const double* __restrict__ camdata,
-                                                       const double* __restrict__ lin, double* __restrict__ delta,
-                                                       double* __restrict__ part, int nb,
-                                                       unsigned long long* __restrict__ tl) {
+__device__ __forceinline__ void band_body(const LmState* __restrict__ st, const DevProblem& P,
+                                          const double* __restrict__ S, double* __restrict__ rhs,
+                                          int* __restrict__ flag, const BaConsts& c, const double* __restrict__ scale,
+                                          const double* __restrict__ camdata, const double* __restrict__ lin,
+                                          double* __restrict__ delta, double* __restrict__ part, int nb,
+                                          unsigned long long* __restrict__ tl, double* __restrict__ lds) {
     constexpr int G = 6 * BC;
     constexpr int GG = G * G;
     constexpr int TPB = BAND_TPB, NW = BAND_TPB / 64;
@@ -201,7 +201,6 @@ __global__ __launch_bounds__(BAND_TPB) void k_bcr_band(const LmState* __restrict
     constexpr int NSI = ND + G + 4 * G + GG;      // output elements per survivor: D lower | b | B | fill
     constexpr int NQ = (NSI + TPB - 1) / TPB;     // elements per thread and survivor
     constexpr int GRP = NSI <= TPB ? TPB / NSI : 1;  // survivors per pass
-    extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool hi = lane >= 32;
     const int ul = lane & (U - 1);
@@ -670,16 +669,119 @@ __global__ __launch_bounds__(BAND_TPB) void k_bcr_band(const LmState* __restrict
             tl[k] = k < ts || k >= BAND_STAMPS - 1 ? stl[k] : 0ull;
 }
 
+template <int BC, bool STAMP>
+__global__ __launch_bounds__(BAND_TPB) void k_bcr_band(const LmState* __restrict__ st, DevProblem P,
+                                                       const double* __restrict__ S, double* __restrict__ rhs,
+                                                       int* __restrict__ flag, BaConsts c,
+                                                       const double* __restrict__ scale,
+                                                       const double* __restrict__ camdata,
+                                                       const double* __restrict__ lin, double* __restrict__ delta,
+                                                       double* __restrict__ part, int nb,
+                                                       unsigned long long* __restrict__ tl) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    band_body<BC, STAMP>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, tl, lds);
+}
+
+// ---- the band solve's tail in the same launch (DevWork::tail) -------------------------------------------------
+// Workgroup 0 runs the band solve; workgroups 1..nb_bs the point back-substitution chunks (backsub_body), each
+// waiting for the solve's launch number in tail_flags[0]; the last one the final reduction and LM decision
+// (final_body), waiting until tail_flags[1] counts every chunk of this launch. The chunks zero S's envelope tiles
+// only after the solve has read them. Two launches and their dependent-launch latency less per LM iteration, and
+// the chunks' prologue overlaps the solve. Every workgroup is resident at once (band_tail_blocks bounds the grid),
+// waits are bounded (a timeout raises FLAG_TIMEOUT: the decision then asks the host to re-run the iteration with
+// the separate launches). Roles past the solve use waves 0-3 (the bodies are written for 256 threads).
+__device__ unsigned g_tail_spin_limit = 1u << 20;
+
+__device__ __forceinline__ bool tail_wait(const unsigned* w, unsigned target, unsigned lim) {
+    for (unsigned n = 0;; ++n) {  // relaxed: the payload is read past the L2 (PUB bodies), no invalidate needed
+        if (__hip_atomic_load(const_cast<unsigned*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target)
+            return true;
+        if (n >= lim) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <int BC, bool O32>
+__global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restrict__ st_c, DevProblem P, BaConsts c,
+                                                        LmParams prm, double* __restrict__ S, double* __restrict__ rhs,
+                                                        int* __restrict__ flag, const double* __restrict__ scale,
+                                                        const double* __restrict__ camdata,
+                                                        const double* __restrict__ lin, double* __restrict__ delta,
+                                                        double* __restrict__ part, int nb, const double* __restrict__ pdata,
+                                                        const int2* __restrict__ ztiles, int n_ztiles, int nb_bs,
+                                                        int nb_pt, int nb_upd, double* __restrict__ scal,
+                                                        double* __restrict__ log, unsigned* __restrict__ tflags,
+                                                        unsigned seq) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ int ok_s;
+    LmState* const st = const_cast<LmState*>(st_c);
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (b == 0) {
+        band_body<BC, false>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, nullptr, lds);
+        __syncthreads();  // every thread's stores of y, the candidate cameras and the partials are issued
+        if (tid == 0) {
+            __threadfence();
+            __hip_atomic_store(tflags, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (tid >= 256) return;  // (the back-substitution and final bodies are written for 256 threads)
+    const bool skip = skip_step(st);
+    // A wait past the spin bound marks the iteration for a re-run (FLAG_TIMEOUT) and then still waits for its
+    // producer (which waits on nothing and runs ahead of its consumers in dispatch order) before this workgroup
+    // touches S or rhs, which the re-run assembles onto
+    constexpr unsigned BOUND = 1u << 26;
+    if (b <= nb_bs) {
+        if (tid == 0) {
+            ok_s = skip ? 1 : (tail_wait(tflags, seq, g_tail_spin_limit) ? 1 : 0);
+            if (!ok_s) {
+                raise_flag(flag, FLAG_TIMEOUT);
+                (void)tail_wait(tflags, seq, BOUND);
+            }
+        }
+        __syncthreads();
+        if (ok_s) {
+            backsub_body<O32, true>(P, c, st, scale, pdata, rhs, delta, part, ztiles, n_ztiles, S, b - 1, nb_bs,
+                                    *reinterpret_cast<BsLds*>(lds));
+        } else if (tid == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flag) drained before the count
+        }
+        // thread 0 stored and drained this chunk's partials (PUB): count the chunk, no fence
+        if (tid == 0) __hip_atomic_fetch_add(tflags + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // then this chunk's share of S's envelope tiles for the next iteration's assembly (the solve has read S;
+        // the next launch sees the stores)
+        if (!skip)
+            for (int t = (b - 1) * n_ztiles / nb_bs; t < b * n_ztiles / nb_bs; ++t) {
+                const int2 ij = ztiles[t];
+                S[(size_t)(16 * ij.x + (tid >> 4)) * P.npad + 16 * ij.y + (tid & 15)] = 0.0;
+            }
+        return;
+    }
+    // the final workgroup: every chunk of this launch has counted itself
+    if (tid == 0) {
+        ok_s = (skip || tail_wait(tflags + 1, seq * (unsigned)nb_bs, g_tail_spin_limit)) ? 1 : 0;
+        if (!ok_s) {
+            raise_flag(flag, FLAG_TIMEOUT);
+            (void)tail_wait(tflags + 1, seq * (unsigned)nb_bs, BOUND);  // every chunk done before rhs is zeroed
+        }
+    }
+    __syncthreads();
+    final_body<2, true>(P, st, nb_pt, nb_upd, nb_bs, part, flag, scal, prm, lin, log, rhs, nullptr,
+                        *reinterpret_cast<FinLds*>(lds));
+}
+
 static size_t band_lds_bytes(int bc, int nb, int nac) { return sizeof(double) * (size_t)band_layout(6 * bc, nb, nac).total; }
 
 // The band path for this window: cameras per block (1..3), 0 when it does not apply. mode: MIBA_BCR_BAND
 // (0 off, 2 also for one-block windows, else the default: windows of more than one 64-dof BCR block).
-int bcr_band_ok(int nac, int cam_band, int kb) {
+int bcr_band_ok(int nac, int cam_band, int kb, bool one_block) {
     if (nac < 2 || cam_band > 3 || std::getenv("MIBA_BCR")) return 0;
     const char* e = std::getenv("MIBA_BCR_BAND");
     const int mode = e ? std::atoi(e) : 1;
     if (mode == 0) return 0;
-    if (mode != 2 && nac <= BCR_CAMS && kb + 4 <= 64) return 0;  // one BCR block: k_bcr_dense1
+    // one BCR block: k_bcr_dense1, unless the band solve's tail launch will run (C1: 46.8-47.8 us per LM iteration
+    // against 48.0-48.9 with k_bcr_dense1, same box) or MIBA_BCR_BAND=2
+    if (mode != 2 && !one_block && nac <= BCR_CAMS && kb + 4 <= 64) return 0;
     const int bc = cam_band < 1 ? 1 : cam_band;
     const int nb = (nac + bc - 1) / bc;
     int dev = 0, lmax = 0;
@@ -749,6 +851,52 @@ static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork&
                        W.scale, W.camdata, W.lin, W.delta, W.part, nb, (unsigned long long*)nullptr);
     if (pf) pf->end(s);
     return hipGetLastError();
+}
+
+int band_tail_blocks(const DevProblem& P, int bc) {
+    if (bc < 1 || bc > 3) return 0;
+    const int n = P.n_bs_chunks + 2;
+    const size_t lds = std::max(band_lds_bytes(bc, (P.nac + bc - 1) / bc, P.nac), std::max(sizeof(BsLds), sizeof(FinLds)));
+    // one resident round with room to spare (>= 256 CUs), the dynamic LDS beside the launch's static word
+    return (P.n_ap > 0 && n <= 128 && lds <= 160 * 1024 - 256) ? n : 0;
+}
+
+hipError_t tail_set_spin_limit(unsigned limit) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_spin_limit), &limit, sizeof(limit));
+}
+
+template <int BC, bool O32>
+static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int nb,
+                                int nb_pt, int nb_upd, hipStream_t s, Prof* pf) {
+    static bool attr = false;
+    if (!attr) {
+        CKD(hipFuncSetAttribute((const void*)k_band_tail<BC, O32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024 - 256));
+        attr = true;
+    }
+    const size_t lds = std::max(band_lds_bytes(BC, nb, P.nac), std::max(sizeof(BsLds), sizeof(FinLds)));
+    const int nb_bs = P.n_bs_chunks;
+    ++W.tail_seq;
+    if (pf) pf->begin(K_BCR_PERSIST, s);
+    hipLaunchKernelGGL((k_band_tail<BC, O32>), dim3(nb_bs + 2), dim3(BAND_TPB), lds, s, W.st, P, c, prm, W.S, W.rhs,
+                       W.chol_flag, W.scale, W.camdata, W.lin, W.delta, W.part, nb, W.pdata, W.env_tile,
+                       W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq);
+    if (pf) pf->end(s);
+    return hipGetLastError();
+}
+
+hipError_t launch_band_tail(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int bc, int nb_pt,
+                            int nb_upd, hipStream_t s, Prof* pf) {
+    const int nb = (P.nac + bc - 1) / bc;
+    switch (bc * 2 + (P.obs32 ? 1 : 0)) {
+        case 2: return launch_tail_t<1, false>(P, c, prm, W, nb, nb_pt, nb_upd, s, pf);
+        case 3: return launch_tail_t<1, true>(P, c, prm, W, nb, nb_pt, nb_upd, s, pf);
+        case 4: return launch_tail_t<2, false>(P, c, prm, W, nb, nb_pt, nb_upd, s, pf);
+        case 5: return launch_tail_t<2, true>(P, c, prm, W, nb, nb_pt, nb_upd, s, pf);
+        case 6: return launch_tail_t<3, false>(P, c, prm, W, nb, nb_pt, nb_upd, s, pf);
+        case 7: return launch_tail_t<3, true>(P, c, prm, W, nb, nb_pt, nb_upd, s, pf);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_bcr_band(const DevProblem& P, const BaConsts& c, DevWork& W, int bc, hipStream_t s, Prof* pf) {

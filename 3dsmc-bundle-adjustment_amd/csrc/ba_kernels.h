@@ -337,6 +337,13 @@ struct DevWork {
     int fpl = 0;
     unsigned* sw_cnt = nullptr;
     unsigned sw_seq = 0;
+    // the band solve's tail (small unsharded windows, default mode): the back-substitution chunks and the final
+    // reduction + decision as workgroups of the band solve's launch (k_band_tail), behind two hand-off words
+    // tail_flags[0] (the solve's launch number) and [1] (back-substitution chunks done, monotonic within a solve;
+    // both reset by launch_reset); tail_seq: tail launches of this solve (host side)
+    int tail = 0;
+    unsigned* tail_flags = nullptr;
+    unsigned tail_seq = 0;
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)
@@ -405,8 +412,15 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
 int bcr_persist_ok(int nblk);
 int bcr_dense1_ok(int nblk, int kb);
 // cameras per block of the one-workgroup band solve for this window (0: not eligible; MIBA_BCR_BAND)
-int bcr_band_ok(int nac, int cam_band, int kb);
+// (one_block: also windows of one 64-dof block, where the band solve runs with its tail launch)
+int bcr_band_ok(int nac, int cam_band, int kb, bool one_block);
 hipError_t launch_bcr_band(const DevProblem& P, const BaConsts& c, DevWork& W, int bc, hipStream_t s, Prof* pf);
+// the band solve + back-substitution + final decision in one launch (W.tail): nb_pt / nb_upd / nb_bs as k_final's
+hipError_t launch_band_tail(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int bc, int nb_pt,
+                            int nb_upd, hipStream_t s, Prof* pf);
+// workgroups of the tail launch (0: the window does not fit one resident round)
+int band_tail_blocks(const DevProblem& P, int bc);
+hipError_t tail_set_spin_limit(unsigned limit);
 // k_bcr_split's pull slots: empty (split = true, Bw.persist >= 2) or zero (the per-level / persistent paths)
 hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s);
 // spin bound of the resident BCR kernels' inter-workgroup waits (default 1 << 22 polls; tests force a

@@ -30,95 +30,9 @@
 #include "ba_common.h"
 #include "ba_device.h"
 #include "ba_kernels.h"
+#include "ba_tail.h"
 
 namespace miba {
-
-static constexpr int TPB = 256;
-
-// Observation record as loaded (ObsRaw<O32>): O32 = the window's obs32 records (one 16-byte load), else the f64
-// arrays; u / v / depth widen to f64 exactly, so both paths run the same arithmetic.
-template <bool O32>
-struct ObsRaw;
-template <>
-struct ObsRaw<true> {
-    float4 r;
-    __device__ __forceinline__ double u() const { return (double)r.x; }
-    __device__ __forceinline__ double v() const { return (double)r.y; }
-    __device__ __forceinline__ double d() const { return (double)r.z; }
-    __device__ __forceinline__ int idx() const { return __float_as_int(r.w); }
-};
-template <>
-struct ObsRaw<false> {
-    double2 uv;
-    double dep;
-    int i;
-    __device__ __forceinline__ double u() const { return uv.x; }
-    __device__ __forceinline__ double v() const { return uv.y; }
-    __device__ __forceinline__ double d() const { return dep; }
-    __device__ __forceinline__ int idx() const { return i; }
-};
-// point-major observation o: pixel, depth, camera index
-template <bool O32>
-__device__ __forceinline__ ObsRaw<O32> po_obs(const DevProblem& P, int o) {
-    if constexpr (O32) return ObsRaw<true>{P.po_rec[o]};
-    else return ObsRaw<false>{P.po_uv[o], P.po_depth[o], P.po_cam[o]};
-}
-// camera-major observation o: pixel, depth, point index
-template <bool O32>
-__device__ __forceinline__ ObsRaw<O32> co_obs(const DevProblem& P, int o) {
-    if constexpr (O32) return ObsRaw<true>{P.co_rec[o]};
-    else return ObsRaw<false>{P.co_uv[o], P.co_depth[o], P.co_pt[o]};
-}
-template <bool O32>
-__device__ __forceinline__ ObsRaw<O32> obs_zero() {
-    if constexpr (O32) return ObsRaw<true>{float4{0.f, 0.f, 0.f, 0.f}};
-    else return ObsRaw<false>{double2{0.0, 0.0}, 0.0, 0};
-}
-
-
-// Block (256 threads) sum of NV values; result valid in out[0..NV) after return (LDS).
-template <int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double* lds /*4*NV*/, double* out /*NV*/) {
-    wave_sum<NV>(v);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0)
-#pragma unroll
-        for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
-    __syncthreads();
-    for (int i = threadIdx.x; i < NV; i += blockDim.x)
-        out[i] = lds[0 * NV + i] + lds[1 * NV + i] + lds[2 * NV + i] + lds[3 * NV + i];
-    __syncthreads();
-}
-
-
-// Block (256 threads) sum of NV values via the wave reduce-scatter; out[0..NV) valid after return.
-// lds must hold 4 * NV doubles. Fixed summation order (deterministic).
-template <int NV>
-__device__ __forceinline__ void block_sum_rs(double (&v)[NV], double* lds, double* out) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int base = 0, len = NV;
-    WaveHalve<NV, 32>::run(v, lane, base, len);
-    constexpr int R = HalveRemain<NV, 32>::value;
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-        if (j < len) lds[wave * NV + base + j] = v[j];
-    __syncthreads();
-    for (int i = threadIdx.x; i < NV; i += blockDim.x)
-        out[i] = lds[0 * NV + i] + lds[1 * NV + i] + lds[2 * NV + i] + lds[3 * NV + i];
-    __syncthreads();
-}
-
-
-__device__ __forceinline__ double block_max(double v, double* lds) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) lds[wave] = v;
-    __syncthreads();
-    const double r = fmax(fmax(lds[0], lds[1]), fmax(lds[2], lds[3]));
-    __syncthreads();
-    return r;
-}
 
 // ---------------------------------------------------------------- camera side
 // XCD-aware sub-segment order: workgroup b of a launch runs on XCD b % 8 (dispatch round-robin; a placement
@@ -2038,14 +1952,7 @@ __global__ void k_update_cams(DevProblem P, BaConsts c, const LmState* __restric
     }
 }
 
-// Back-substitution over a chunk of <= BS_PTS points / <= BS_OBS observations (one
-// workgroup; observation loads coalesced, one observation per thread):
-//   phase 1 (obs):   c_o = s_p (Jp^T (Jc (s_c y_c)))  -> LDS slot of the observation
-//   phase 2 (point): y_p = V~^-1 (e~ - Kt^T y_k - sum_o c_o) (fixed order), delta_p = -s_p y_p
-//   phase 3 (obs):   candidate cost at x + delta
-// The points' share of the model cost change, 0.5 (e~^T y_p + y_p^T D~_p y_p), is summed in phase 2
-// (k_update_cams states the identity).
-// A chunk holding a single point with more than BS_OBS observations sums c_o by block reduction.
+// Back-substitution over a chunk of points (backsub_body, ba_tail.h): one workgroup per chunk.
 template <bool O32>
 __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c, const LmState* __restrict__ st,
                                                        const double* __restrict__ scale,
@@ -2053,136 +1960,8 @@ __global__ __launch_bounds__(TPB) void k_backsub_chunk(DevProblem P, BaConsts c,
                                                        const double* __restrict__ delta, double* __restrict__ part,
                                                        const int2* __restrict__ ztiles, int n_ztiles,
                                                        double* __restrict__ Sz) {
-    __shared__ double co[BS_OBS][3];
-    __shared__ double dpl[BS_PTS][3];
-    __shared__ double lds[4 * 5];
-    __shared__ double out[5];
-    if (skip_step(st)) return;
-    // fused path: the reduced solve has consumed S; zero this chunk's share of its envelope tiles for the next
-    // iteration's atomic assembly (k_final zeroes rhs, which still holds y here)
-    for (int t = blockIdx.x * n_ztiles / gridDim.x; t < (blockIdx.x + 1) * n_ztiles / (int)gridDim.x; ++t) {
-        const int2 ij = ztiles[t];
-        Sz[(size_t)(16 * ij.x + (threadIdx.x >> 4)) * P.npad + 16 * ij.y + (threadIdx.x & 15)] = 0.0;
-    }
-    const int cur = st->cur;
-    const int ch = blockIdx.x, tid = threadIdx.x;
-    const int apb = P.bs_chunk[ch], ape = P.bs_chunk[ch + 1];
-    const int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
-    const int npts = ape - apb;
-    const bool big = oe - ob > BS_OBS;  // single point
-    const double* K = P.K[cur];
-    const double* Kn = P.K[cur ^ 1];
-    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cost, bad, |x_cand|^2
-    // each thread's observation records (<= BS_OBS / TPB of them) are read once, in phase 1, and kept in
-    // registers for phase 3 (a single point with more observations re-reads its records in phase 3)
-    constexpr int NR = BS_OBS / TPB;
-    int r_ap[NR];
-    ObsRaw<O32> r_o[NR];  // camera index, pixel, depth
-    // ---- phase 1
-    double bsum[3] = {0.0, 0.0, 0.0};
-    int it = 0;
-    for (int o = ob + tid; o < oe; o += TPB, ++it) {
-        const int ac = P.po_ac[o];
-        const int ap = P.po_ap[o];
-        const ObsRaw<O32> ro = po_obs<O32>(P, o);
-        const int cam = ro.idx();
-#pragma unroll
-        for (int k = 0; k < NR; ++k)  // register arrays: constant indices only
-            if (k == it) { r_ap[k] = ap; r_o[k] = ro; }
-        double v[3] = {0.0, 0.0, 0.0};
-        if (ac >= 0) {
-            ObsEval ev;
-            double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * cam, P.pts[cur] + 3 * P.pt_idx[ap], K, ro.u(), ro.v(), ro.d(), ev, jc, jp, jk);
-            const double* sc = scale + 6 * ac;
-            const double* yc = y + 6 * ac;
-            const double* sp = scale + P.off_pt + 3 * ap;
-            double jy[3], sy[6];
-#pragma unroll
-            for (int d = 0; d < 6; ++d) sy[d] = sc[d] * yc[d];
-            jc_times(jc, sy, jy);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) v[i] = sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
-        }
-        if (big) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) bsum[i] += v[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) co[o - ob][i] = v[i];
-        }
-    }
-    if (big) block_sum<3>(bsum, lds, out);  // out[0..3) valid for every thread after this
-    __syncthreads();
-    // ---- phase 2
-    if (tid < npts) {
-        const int ap = apb + tid;
-        const int pi = P.pt_idx[ap];
-        const double* X = P.pts[cur] + 3 * pi;
-        double* Xn = P.pts[cur ^ 1] + 3 * pi;
-        const double* pd = pdata + (size_t)ap * PDATA;
-        const double* sp = scale + P.off_pt + 3 * ap;
-        const double* yk = y + P.kb;
-        double t[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-            t[i] = pd[6 + i] - (pd[9 + 0 * 3 + i] * yk[0] + pd[9 + 1 * 3 + i] * yk[1] + pd[9 + 2 * 3 + i] * yk[2] +
-                                pd[9 + 3 * 3 + i] * yk[3]);
-        if (big) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) t[i] -= out[i];
-        } else {
-            for (int o = P.pt_ptr[ap]; o < P.pt_ptr[ap + 1]; ++o)
-#pragma unroll
-                for (int i = 0; i < 3; ++i) t[i] -= co[o - ob][i];
-        }
-        double Vf[9];
-        vinv_from_g(pd, Vf);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const double yp = Vf[i * 3 + 0] * t[0] + Vf[i * 3 + 1] * t[1] + Vf[i * 3 + 2] * t[2];
-            acc[1] += 0.5 * (pd[6 + i] * yp + pd[21 + i] * yp * yp);
-            const double dp = -sp[i] * yp;
-            const double xn = X[i] + dp;
-            Xn[i] = xn;
-            dpl[tid][i] = dp;
-            const double df = X[i] - xn;
-            acc[0] += df * df;
-            acc[4] += xn * xn;
-        }
-    }
-    __syncthreads();
-    // ---- phase 3
-    (void)delta;
-    it = 0;
-    for (int o = ob + tid; o < oe; o += TPB, ++it) {
-        int ap;
-        ObsRaw<O32> ro;
-        if (it < NR) {
-#pragma unroll
-            for (int k = 0; k < NR; ++k)  // register arrays: constant indices only
-                if (k == it) { ap = r_ap[k]; ro = r_o[k]; }
-        } else {
-            ap = P.po_ap[o];
-            ro = po_obs<O32>(P, o);
-        }
-        const int cam = ro.idx();
-        const int pl = ap - apb;
-        const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
-        const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
-        ObsEval en;
-        eval_obs(c, P.cams[cur ^ 1] + 7 * cam, xn, Kn, ro.u(), ro.v(), ro.d(), en);
-        if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
-    }
-    if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
-    block_sum<5>(acc, lds, out);
-    if (tid == 0) {
-        part[PART_BS_SN2 * P.part_stride + ch] = out[0];
-        part[PART_BS_MCC * P.part_stride + ch] = out[1];
-        part[PART_BS_COST * P.part_stride + ch] = out[2];
-        part[PART_BS_BAD * P.part_stride + ch] = out[3] > 0.0 ? 1.0 : 0.0;
-        part[PART_BS_XN2 * P.part_stride + ch] = out[4];
-    }
+    __shared__ BsLds L;
+    backsub_body<O32>(P, c, st, scale, pdata, y, delta, part, ztiles, n_ztiles, Sz, blockIdx.x, gridDim.x, L);
 }
 
 // Clear the envelope tiles of S (every solver reads only these; the rest stays zero).
@@ -2201,77 +1980,15 @@ __global__ __launch_bounds__(TPB) void k_env_zero(const LmState* __restrict__ st
 // k_assemble + the chol_flag memset (same values as k_assemble, element for element).
 
 // ---------------------------------------------------------------- final
-// scal[SC_MCC], [SC_CAND], [SC_SN2], [SC_GMAX_PT], [SC_BAD]; then the LM decision (k_lm_decide's
-// body, fused: one launch less per iteration)
-// 4 waves (16 measured 1 us slower at C4: more waves to start and to reduce than loads saved). UNR: unroll of
-// the partial-sum loops (C4 rocprof: k_final 9.2 / 6.9 / 7.5 us at 1 / 2 / 8; k_final_shard with twice the
-// accumulators 6.7 / 11.0 / 12.8 us at 1 / 4 / 8)
-static constexpr int TPB_F = 256, NW_F = TPB_F / 64;
+// The deterministic reduction of the per-block partials + the LM decision (final_body, ba_tail.h).
 template <int UNR>
 __global__ __launch_bounds__(TPB_F) void k_final(DevProblem P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                                int nblk_bs, const double* __restrict__ part,
                                                const int* __restrict__ chol_flag, double* __restrict__ scal,
                                                LmParams prm, const double* __restrict__ lin, double* __restrict__ log,
                                                double* __restrict__ rhs_z, unsigned* __restrict__ bcr_epoch) {
-    __shared__ double lds[NW_F * 4];
-    __shared__ double out[4];
-    __shared__ double red[NW_F];
-    // every load up front (the state, the flag, lin and all partials), so the reductions and the decision
-    // wait for one memory round trip instead of one per loop trip
-    LmState S0;
-    int cf = 0;
-    double lin0 = 0.0, lin1 = 0.0;
-    if (threadIdx.x == 0) {
-        S0 = *st;
-        cf = *chol_flag;
-        lin0 = lin[0];
-        lin1 = lin[1];
-    }
-    const int done = __builtin_amdgcn_readfirstlane(st->done);
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    double gm = 0.0, bad = 0.0;
-    const size_t stp = P.part_stride;
-#pragma unroll UNR
-    for (int i = threadIdx.x; i < nblk_upd; i += TPB_F) {
-        acc[0] += part[PART_UPD_SN2 * stp + i];
-        acc[1] += part[PART_UPD_MCC * stp + i];
-        acc[2] += part[PART_UPD_COST * stp + i];
-        acc[3] += part[PART_UPD_XN2 * stp + i];
-    }
-#pragma unroll UNR
-    for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
-        acc[0] += part[PART_BS_SN2 * stp + i];
-        acc[1] += part[PART_BS_MCC * stp + i];
-        acc[2] += part[PART_BS_COST * stp + i];
-        acc[3] += part[PART_BS_XN2 * stp + i];
-        bad = fmax(bad, part[PART_BS_BAD * stp + i]);
-    }
-#pragma unroll UNR
-    for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
-        gm = fmax(gm, part[PART_PT_GMAX * stp + i]);
-        bad = fmax(bad, 2.0 * part[PART_PT_BAD * stp + i]);
-    }
-    if (done) return;
-    // k_bcr_split ran this iteration (it skips exactly when done | stop_next): the next launch's epoch. Advanced
-    // here, in stream order behind it, so no workgroup of that launch can still be reading the current one.
-    if (bcr_epoch && threadIdx.x == 0 && !S0.stop_next) *bcr_epoch += 1;
-    if (rhs_z)  // fused path: y has been consumed; rhs is the next assembly's atomic target
-        for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
-    block_sum_nw<NW_F, 4>(acc, lds, out);
-    gm = block_max_nw<NW_F>(gm, red);
-    bad = block_max_nw<NW_F>(bad, red);
-    if (threadIdx.x == 0) {
-        double sc[SC_N] = {};
-        sc[SC_XN2] = out[3];
-        sc[SC_SN2] = out[0];
-        sc[SC_MCC] = out[1];
-        sc[SC_CAND] = out[2];
-        sc[SC_GMAX_PT] = gm;
-        sc[SC_BAD] = bad + ((cf & FLAG_NOT_PD) ? 4.0 : 0.0) + ((cf & FLAG_TIMEOUT) ? SC_BAD_TIMEOUT : 0.0);
-#pragma unroll
-        for (int k = 0; k < SC_N; ++k) scal[k] = sc[k];
-        lm_decide_pre(S0, st, prm, lin0, lin1, sc, log);
-    }
+    __shared__ FinLds L;
+    final_body<UNR>(P, st, nblk_pt, nblk_upd, nblk_bs, part, chol_flag, scal, prm, lin, log, rhs_z, bcr_epoch, L);
 }
 
 // ---------------------------------------------------------------- landmark sharding
@@ -2757,6 +2474,8 @@ hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, con
                         const double* K0, int n_cams, int n_points, hipStream_t s) {
     if (W.sw_cnt) CK(hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));  // the small-window launch's counter
     W.sw_seq = 0;
+    if (W.tail_flags) CK(hipMemsetAsync(W.tail_flags, 0, 2 * sizeof(unsigned), s));  // the band tail's hand-offs
+    W.tail_seq = 0;
     const int ncd = 7 * n_cams, npd = 3 * n_points;
     // fused path: S (npad^2, even: npad is a multiple of 16) and rhs are zeroed here too
     const size_t nS2 = W.fused ? (size_t)P.npad * P.npad / 2 : 0;
@@ -2962,6 +2681,7 @@ static hipError_t launch_band(const DevProblem& P, DevWork& W, hipStream_t s, Pr
 }
 
 hipError_t launch_factor(const DevProblem& P, const BaConsts& c, DevWork& W, hipStream_t s, Prof* pf) {
+    if (P.solver == 2 && W.tail) return hipSuccess;  // the band solve runs in launch_update's tail launch
     if (P.solver == 2) return launch_bcr(P, c, W, W.bcr, s, pf);  // k_bcr_border also applies the camera step
     if (P.solver == 1) switch (P.band_w) {
         case 1: return launch_band<1>(P, W, s, pf);
@@ -2988,6 +2708,10 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
         ndummy = e ? atoi(e) : 0;
     }
     for (int k = 0; k < ndummy; ++k) PL(K_DUMMY, k_dummy, dim3(1), dim3(64), 0, s, W.st);
+    if (W.tail) {  // band solve + back-substitution + decision in one launch (ba_band.hip k_band_tail)
+        const int nb_pt = W.sw ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts, 1) : pp_parts(P);
+        return launch_band_tail(P, c, prm, W, W.bcr.band, nb_pt, nb_upd, s, pf);
+    }
     if (!fused_upd)
         PL(K_UPDATE_CAMS, k_update_cams, dim3(nb_upd), dim3(TPB), 0, s, P, c, W.st, W.scale, W.camdata, W.lin, W.rhs,
            W.delta, W.part);

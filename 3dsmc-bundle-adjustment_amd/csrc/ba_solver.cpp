@@ -119,6 +119,8 @@ struct ba_context {
     int n_tiles = 0, n_ovf_obs = 0, n_tiled_pts = 0;
     int n_adm_all = 0;  // admissible observations over all landmark shards
     int sw_full = 0;    // DevWork::sw as the last full prepare chose it (a timeout re-run clears W.sw)
+    int tail_full = 0;  // DevWork::tail likewise
+    bool tail_possible = false;  // the window's LM loop can take the band tail launch (set before bcr_setup)
     int prep_nc = -1, prep_np = -1, prep_no = -1;
     int last_iter = -1;        // iterations of the last solve (ba_iteration_log rows - 1)
     // shard_min_obs: a window below the threshold is gathered onto every rank and solved there alone; the
@@ -624,7 +626,7 @@ static int upload_params(ba_context* ctx, const ba_problem* p, hipStream_t s) {
 static unsigned long long env_key() {
     static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
                                         "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED", "MIBA_SW", "MIBA_FPL",
-                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES", "MIBA_DEVICE_PLAN"};
+                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES", "MIBA_DEVICE_PLAN", "MIBA_TAIL"};
     unsigned long long h = 1469598103934665603ull;
     for (const char* n : names) {
         const char* v = std::getenv(n);
@@ -646,7 +648,7 @@ static int bcr_setup(ba_context* ctx) {
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_BCR].p, 0, ctx->buf[B_BCR].cap, ctx->stream));
     Bw.persist = bcr_persist_ok(Bw.nblk);
     Bw.dense1 = bcr_dense1_ok(Bw.nblk, ctx->P.kb);
-    Bw.band = bcr_band_ok(ctx->P.nac, ctx->P.cam_band, ctx->P.kb);
+    Bw.band = bcr_band_ok(ctx->P.nac, ctx->P.cam_band, ctx->P.kb, ctx->tail_possible);
     if (const char* e = std::getenv("MIBA_BCR")) {
         if (!std::strcmp(e, "launch")) Bw.persist = 0;
         else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
@@ -735,12 +737,14 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     // a hand-off timeout cleared the small-window launch for the rest of that solve: the next one takes the path
     // the full prepare chose again (no sticky fallback)
     ctx->W.sw = ctx->sw_full;
+    ctx->W.tail = ctx->tail_full;
     set_consts(ctx);
     ctx->pinfo.plan_reused = 1;
     ctx->pinfo.obs_uploaded = any_vals ? 1 : 0;
     ctx->pinfo.upload_ms = now_ms() - tu;
     ctx->pinfo.bcr_path = P.solver == 2 ? bcr_path_id(ctx->W.bcr) : -1;
     ctx->pinfo.lin_path = ctx->W.sw;
+    ctx->pinfo.tail = ctx->W.tail;
     ctx->prepared = true;
     ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;
     return 1;
@@ -1160,7 +1164,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         HIPCHECK(ctx, ctx->buf[B_DELTA].ensure(sizeof(double) * npad));
         HIPCHECK(ctx, ctx->buf[B_PART].ensure(sizeof(double) * PART_NSLOTS * part_stride));
         HIPCHECK(ctx, ctx->buf[B_SCAL].ensure(sizeof(double) * SC_N));
-        HIPCHECK(ctx, ctx->buf[B_FLAG].ensure(sizeof(int) * 4));
+        HIPCHECK(ctx, ctx->buf[B_FLAG].ensure(sizeof(int) * 8));
         HIPCHECK(ctx, ctx->buf[B_STATE].ensure(sizeof(LmState)));
         HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (std::max(o.max_num_iterations, 0) + 2)));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * part_stride, s));
@@ -1230,6 +1234,12 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             else if (!std::strcmp(e, "bcr") && cam_band < BCR_CAMS && bcr_nblk >= 1) P.solver = 2;
         }
         if (const char* e = std::getenv("MIBA_DENSE_CHOL")) if (e[0] == '1') P.solver = 0;
+        {
+            const char* ef = std::getenv("MIBA_FUSED");
+            const char* et = std::getenv("MIBA_TAIL");
+            ctx->tail_possible = !shard && !det && n_ap > 0 && n_seg > 0 && !(ef && ef[0] == '0') &&
+                                 !(et && et[0] == '0') && n_bs_chunks + 2 <= 128;
+        }
         if (P.solver == 2) {
             const size_t bytes = bcr_bytes(bcr_nblk);
             HIPCHECK(ctx, ctx->buf[B_BCR].ensure(bytes));
@@ -1318,9 +1328,18 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             W.sw_cnt = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 2);
             W.sw_seq = 0;
             HIPCHECK(ctx, hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));
+            // the band solve's tail (back-substitution chunks + decision) in its launch: unsharded default-mode band
+            // windows whose tail fits one resident round; MIBA_TAIL=0 keeps the separate launches
+            const char* e4 = std::getenv("MIBA_TAIL");
+            W.tail = (P.solver == 2 && W.bcr.band && W.fused && !shard && !W.det_tbuf && band_tail_blocks(P, W.bcr.band) > 0 &&
+                      !(e4 && e4[0] == '0')) ? 1 : 0;
+            W.tail_flags = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 4);
+            W.tail_seq = 0;
+            HIPCHECK(ctx, hipMemsetAsync(W.tail_flags, 0, 2 * sizeof(unsigned), s));
         }
         ctx->n_adm_all = n_adm_all;
         ctx->sw_full = W.sw;
+        ctx->tail_full = W.tail;
         set_consts(ctx);
         ctx->nblk_pt = nblk_pt;
         ctx->prepared = true;
@@ -1407,6 +1426,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->pinfo.obs_uploaded = 1;
         ctx->pinfo.bcr_path = P.solver == 2 ? bcr_path_id(ctx->W.bcr) : -1;
         ctx->pinfo.lin_path = ctx->W.sw;
+    ctx->pinfo.tail = ctx->W.tail;
         return BA_OK;
     };
     int rc = finish();
@@ -1481,6 +1501,7 @@ static int apply_spin_limit(ba_context* ctx) {
     if (applied[ctx->device] != want) {
         HIPCHECK(ctx, bcr_set_spin_limit(want));
         HIPCHECK(ctx, sw_set_spin_limit(want_sw));
+        HIPCHECK(ctx, tail_set_spin_limit(want_sw));
         applied[ctx->device] = want;
     }
     return BA_OK;
@@ -1498,6 +1519,7 @@ static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     Bw.persist = 0;
     Bw.dense1 = 0;  // (k_bcr_dense1 waits only inside its workgroup: a forced spin bound can still time it out)
     ctx->W.sw = 0;  // the small-window Schur launch's envelope tiles wait for its camera side
+    ctx->W.tail = 0;  // the band tail's chunks and decision wait for the solve / the chunks
     ctx->bcr_fallback = true;
     if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
     HIPCHECK(ctx, bcr_reset_pull_slots(Bw, false, s));

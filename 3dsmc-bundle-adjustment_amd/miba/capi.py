@@ -140,6 +140,7 @@ class BaPrepareInfo(C.Structure):
         ("total_ms", C.c_double),
         ("lin_path", C.c_int32),
         ("plan_device", C.c_int32),
+        ("tail", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

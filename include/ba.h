@@ -199,6 +199,8 @@ typedef struct ba_prepare_info {
                                 tiles and the camera side in the Schur launch (no separate linearisation launch);
                                 0 = a linearisation launch before the Schur launch */
     int32_t plan_device;     /* 1: the window's plan passes ran on the device (MIBA_DEVICE_PLAN; 0 on a reuse) */
+    int32_t tail;            /* 1: the band solve's launch also runs the point back-substitution and the LM
+                                decision (bcr_path 5, small unsharded windows; MIBA_TAIL=0: separate launches) */
 } ba_prepare_info;
 int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info);
 

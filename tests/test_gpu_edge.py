@@ -104,6 +104,7 @@ def test_one_block_window_timeout_reruns_and_restores_the_small_window_path(monk
     solve (BA_OK, oracle parity); the next solve of the same window (plan cache) takes the one-block path again."""
     p = synthetic.make_config("C1")
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=8))
+    monkeypatch.setenv("MIBA_BCR_BAND", "0")  # (the default one-block path is the band solve with its tail launch)
     with _solver(max_num_iterations=8) as s:
         s.solve(p.copy())
         info0 = s.last_prepare()
@@ -119,6 +120,37 @@ def test_one_block_window_timeout_reruns_and_restores_the_small_window_path(monk
         note2 = s.last_error()
     assert "re-run with the per-level BCR launches" in note, note
     assert info2["plan_reused"] == 1 and info2["bcr_path"] == 4 and info2["lin_path"] == 1, info2
+    assert note2 == "", note2
+    for g in (sg, sg2):
+        assert g["termination"] == so["termination"], (g, so)
+        assert g["num_iterations"] == so["num_iterations"]
+        assert g["num_successful_steps"] == so["num_successful_steps"]
+        assert abs(g["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (g, so)
+    np.testing.assert_allclose(q.cams, q2.cams, rtol=0, atol=1e-10)
+
+
+def test_band_tail_timeout_reruns_with_the_separate_launches(monkeypatch):
+    """The band solve's tail launch (C3: the back-substitution chunks wait for the solve, the decision for the
+    chunks) under a forced one-poll spin bound: the waits time out, the decision asks for a re-run, the iteration
+    re-runs with the separate launches inside the same solve (BA_OK, oracle parity), and the next solve of the
+    window (plan cache) takes the tail launch again."""
+    p = synthetic.make_config("C3")
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=8))
+    with _solver(max_num_iterations=8) as s:
+        s.solve(p.copy())
+        info0 = s.last_prepare()
+        assert info0["bcr_path"] == 5 and info0["tail"] == 1, info0
+        monkeypatch.setenv("MIBA_BCR_SPIN_LIMIT", "1")
+        q = p.copy()
+        sg = s.solve(q)
+        note = s.last_error()
+        monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
+        q2 = p.copy()
+        sg2 = s.solve(q2)
+        info2 = s.last_prepare()
+        note2 = s.last_error()
+    assert "re-run with the per-level BCR launches" in note, note
+    assert info2["plan_reused"] == 1 and info2["tail"] == 1, info2
     assert note2 == "", note2
     for g in (sg, sg2):
         assert g["termination"] == so["termination"], (g, so)

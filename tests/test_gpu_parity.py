@@ -234,6 +234,7 @@ def test_bcr_dense1_one_block_windows(n_cams, fixed, monkeypatch):
                                fixed_cam=fixed, sensor_f32=True)
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
+    monkeypatch.setenv("MIBA_BCR_BAND", "0")  # (narrow one-block windows default to the band solve + tail)
     res = {}
     for mode, path in (("dense1", 4), ("split", 3)):
         monkeypatch.setenv("MIBA_BCR_DENSE1", "1" if mode == "dense1" else "0")
@@ -406,22 +407,52 @@ def test_band_one_workgroup_solve(case, monkeypatch):
     np.testing.assert_array_equal(outs[0][1].cams, outs[1][1].cams)
 
 
+@pytest.mark.parametrize("case", sorted(BAND_CASES))
+def test_band_tail_launch_is_the_separate_launches(case, monkeypatch):
+    """The band solve's tail (ba_band.hip k_band_tail: the back-substitution chunks and the final decision as
+    workgroups of the solve's launch, ba_prepare_info.tail) computes what the three launches compute: the same
+    bodies, partials in the same slots (to rounding: the default mode's Schur atomics); and oracle parity."""
+    from miba.solver import Solver
+    make, _ = BAND_CASES[case]
+    p = make()
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
+    monkeypatch.setenv("MIBA_BCR_BAND", "1")
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MIBA_TAIL", mode)
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
+            res[mode] = (s.solve(q), q, s.iteration_log())
+            info = s.last_prepare()
+        assert info["bcr_path"] == 5 and info["tail"] == (mode == "1"), (mode, info)
+    (sa, qa, la), (sb, qb, lb) = res["1"], res["0"]
+    # (the Schur tiles' f64 atomics make the default mode reproducible to rounding only)
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] and sa["num_iterations"] == sb["num_iterations"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-12 * sb["final_cost"], (sa, sb)
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(la, lb, rtol=1e-6, atol=1e-14)  # (cost change and rho cancel)
+    assert sa["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sa, so)
+
+
 def test_band_solve_on_one_block_windows(monkeypatch):
-    """MIBA_BCR_BAND=2: the band solve also on a one-block window (C1, beside the small-window Schur launch)
-    against k_bcr_dense1 and the oracle."""
+    """The band solve (with its tail launch, the default) also on a one-block window (C1, beside the
+    small-window Schur launch) against k_bcr_dense1 (MIBA_BCR_BAND=0) and the oracle."""
     from miba.solver import Solver
     p = synthetic.make_config("C1")
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
     res = {}
-    for mode, path in (("2", 5), ("1", 4)):
+    for mode, path in (("1", 5), ("0", 4)):
         monkeypatch.setenv("MIBA_BCR_BAND", mode)
         q = p.copy()
         with Solver(minimizer_progress_to_stdout=0, max_num_iterations=6, **no_tol) as s:
             res[mode] = (s.solve(q), q)
             info = s.last_prepare()
         assert info["bcr_path"] == path and info["lin_path"] == 1, (mode, info)
-    (sa, qa), (sb, qb) = res["2"], res["1"]
+    (sa, qa), (sb, qb) = res["1"], res["0"]
     assert sa["num_successful_steps"] == sb["num_successful_steps"] == so["num_successful_steps"]
     assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-10 * sb["final_cost"]
     assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
