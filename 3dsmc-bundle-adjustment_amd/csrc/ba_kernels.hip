@@ -59,10 +59,14 @@ __device__ __forceinline__ int xcd_seg(int b, int first, int n) {
 template <bool O32>
 __device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                                int gated, double* __restrict__ camdata, double* __restrict__ seg_intr,
-                                               double* __restrict__ gmax_word, const int s) {
+                                               double* __restrict__ gmax_word, const int s, bool pub = false) {
     // lin[1] is max-accumulated by the envelope tiles / k_cam_finalize (read only after a linearisation):
     // clear it here, one kernel boundary ahead, whether or not this iteration linearises
-    if (s == 0 && threadIdx.x == 0) *gmax_word = 0.0;
+    // (pub: the small-window launch's envelope tiles read the outputs in the same launch, past the L2; stores
+    // likewise, drained by the caller)
+    if (s == 0 && threadIdx.x == 0) {
+        if (pub) tail_st(gmax_word, 0.0); else *gmax_word = 0.0;
+    }
     if (st->done || (gated && !st->need_lin)) return;
     const int cur = st->cur;
     __shared__ double lds[4 * CAM_NZ];
@@ -104,8 +108,14 @@ __device__ __forceinline__ void cam_side_block(const DevProblem& P, const BaCons
     }
     block_sum_rs<CAM_NZ>(acc, lds, out);
     if (ac >= 0)
-        for (int i = threadIdx.x; i < CAMDATA; i += TPB) camdata[(size_t)s * CAMDATA + i] = cam_unpack(out, i);
-    for (int i = threadIdx.x; i < SEGINTR; i += TPB) seg_intr[(size_t)s * SEGINTR + i] = cam_unpack(out, CAMDATA + i);
+        for (int i = threadIdx.x; i < CAMDATA; i += TPB) {
+            double* q = camdata + (size_t)s * CAMDATA + i;
+            if (pub) tail_st(q, cam_unpack(out, i)); else *q = cam_unpack(out, i);
+        }
+    for (int i = threadIdx.x; i < SEGINTR; i += TPB) {
+        double* q = seg_intr + (size_t)s * SEGINTR + i;
+        if (pub) tail_st(q, cam_unpack(out, CAMDATA + i)); else *q = cam_unpack(out, CAMDATA + i);
+    }
 }
 template <bool O32>
 __global__ __launch_bounds__(TPB) void k_cam_side(DevProblem P, BaConsts c, const LmState* __restrict__ st, int gated,
@@ -268,13 +278,17 @@ __device__ __forceinline__ void group_sum(double (&v)[NV]) {
         for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
 }
 // Camera ac's value v (of CAMDATA) summed over its sub-segment partials, in sub-segment order.
-__device__ __forceinline__ double cam_sum(const DevProblem& P, const double* __restrict__ cpart, int ac, int v) {
+__device__ __forceinline__ double cam_sum(const DevProblem& P, const double* __restrict__ cpart, int ac, int v,
+                                          bool pub = false) {
     const int2 r = P.ac_seg[ac];
     double acc = 0.0;
     for (int sg0 = r.x; sg0 < r.y; sg0 += 4) {  // 4 loads in flight, added in segment order
         double t[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = sg0 + k < r.y ? cpart[(size_t)(sg0 + k) * CAMDATA + v] : 0.0;
+        for (int k = 0; k < 4; ++k) {
+            const double* q = cpart + (size_t)(sg0 + k) * CAMDATA + v;
+            t[k] = sg0 + k < r.y ? (pub ? tail_ld(q) : *q) : 0.0;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (sg0 + k < r.y) acc += t[k];
@@ -282,13 +296,17 @@ __device__ __forceinline__ double cam_sum(const DevProblem& P, const double* __r
     return acc;
 }
 // The intrinsics partials of all sub-segments in a fixed order (strided per thread, then block_sum).
-__device__ void intr_sums(const DevProblem& P, const double* __restrict__ seg_intr, double* lds, double* out) {
+__device__ void intr_sums(const DevProblem& P, const double* __restrict__ seg_intr, double* lds, double* out,
+                          bool pub = false) {
     double acc[SEGINTR];
 #pragma unroll
     for (int i = 0; i < SEGINTR; ++i) acc[i] = 0.0;
     for (int sg = threadIdx.x; sg < P.n_seg; sg += TPB)
 #pragma unroll
-        for (int i = 0; i < SEGINTR; ++i) acc[i] += seg_intr[(size_t)sg * SEGINTR + i];
+        for (int i = 0; i < SEGINTR; ++i) {
+            const double* q = seg_intr + (size_t)sg * SEGINTR + i;
+            acc[i] += pub ? tail_ld(q) : *q;
+        }
     block_sum<SEGINTR>(acc, lds, out);
 }
 
@@ -308,7 +326,7 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
                          const double* __restrict__ lin, const double* __restrict__ scale, double* __restrict__ S,
                          double* __restrict__ rhs, int* __restrict__ chol_flag, int fin,
                          const double* __restrict__ cpart, const double* __restrict__ seg_intr, double* camdata_w,
-                         double* lin_w, bool accumulate = false) {
+                         double* lin_w, bool accumulate = false, bool pub = false) {
     __shared__ double cds[4 * CAMDATA];
     __shared__ double l16[LIN_N];
     __shared__ double ilds[4 * SEGINTR];
@@ -335,9 +353,9 @@ __device__ void env_tile(const DevProblem& P, const BaConsts& c, const LmState* 
         else { lo = max(rlo, clo); hi = min(rhi, chi); }
         if (hi < lo) { lo = 0; hi = -1; }
         const int ncam = hi - lo + 1;
-        for (int e = tid; e < ncam * CAMDATA; e += TPB) cds[e] = cam_sum(P, cpart, lo + e / CAMDATA, e % CAMDATA);
+        for (int e = tid; e < ncam * CAMDATA; e += TPB) cds[e] = cam_sum(P, cpart, lo + e / CAMDATA, e % CAMDATA, pub);
         const bool kk_any = brd && c0 + 15 >= kb && c0 < kb + 4;
-        if (kk_any) intr_sums(P, seg_intr, ilds, io);  // (barriers inside; uniform per tile)
+        if (kk_any) intr_sums(P, seg_intr, ilds, io, pub);  // (barriers inside; uniform per tile)
         __syncthreads();
         const int cur = st->cur;
         if (diag) {  // cameras whose first dof lies in this tile's rows
@@ -841,7 +859,8 @@ __device__ unsigned g_sw_spin_limit = 1u << 20;
 __device__ __forceinline__ bool sw_wait(const unsigned* cnt, unsigned target) {
     const unsigned lim = g_sw_spin_limit;
     for (unsigned i = 0; i < lim; ++i) {
-        if (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        // relaxed: the camera side's outputs are read past the L2 (env_tile pub), no invalidate needed
+        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
         __builtin_amdgcn_s_sleep(1);
     }
     return false;
@@ -866,12 +885,12 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
     if constexpr (SW) {
         const int b = (int)blockIdx.x - P.n_tiles - 1;
         if (b >= 0 && b < E.n_cs) {  // camera side (gated on an accepted step), counted whatever it did
-            cam_side_block<O32>(P, c, st, 1, E.cpart_w, E.seg_intr_w, E.lin_w + 1, b);
+            // outputs stored past the L2 and drained by every thread, then counted: no release fence (an L2
+            // write-back) between the camera side and the envelope tiles
+            cam_side_block<O32>(P, c, st, 1, E.cpart_w, E.seg_intr_w, E.lin_w + 1, b, true);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (threadIdx.x == 0) {
-                __threadfence();
-                atomicAdd(E.sw_cnt, 1u);
-            }
+            if (threadIdx.x == 0) __hip_atomic_fetch_add(E.sw_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
         if (b >= E.n_cs && b < E.n_cs + E.n_gb) {  // non-tiled points (intrinsics terms into S unless stop_next)
@@ -886,7 +905,7 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
             if (threadIdx.x == 0) sw_ok = sw_wait(E.sw_cnt, E.sw_target) ? 1 : 0;
             __syncthreads();
             env_tile(P, c, st, b - E.n_cs - E.n_gb, E.tiles, E.camdata, E.lin, scale, S, rhs, E.chol_flag, E.fin,
-                     E.cpart, E.seg_intr, E.camdata_w, E.lin_w, true);
+                     E.cpart, E.seg_intr, E.camdata_w, E.lin_w, true, true);
             if (!sw_ok && threadIdx.x == 0) atomicOr(E.chol_flag, FLAG_TIMEOUT);
             return;
         }

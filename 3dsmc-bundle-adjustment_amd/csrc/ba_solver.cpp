@@ -1313,21 +1313,6 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             // small windows: the point side inside the Schur tiles, the camera side and the non-tiled points as
             // extra workgroups of the Schur launch (no k_lin_point in the LM loop) when the whole launch is one
             // resident round (its envelope tiles wait for its camera side); MIBA_SW=0 keeps the two launches
-            const char* e2 = std::getenv("MIBA_SW");
-            const int n_sw = P.n_tiles + 1 + n_seg + pp_blocks(n_ap - n_tiled, 1) + n_env;
-            // one-block windows only (<= BCR_CAMS active cameras): on C3 (50 cameras, 5 blocks) the fused launch
-            // measured 3 us per LM iteration slower, on C1 1.3 us faster
-            W.sw = (W.fused && !shard && P.n_tiles > 0 && n_sw <= 256 && nac <= BCR_CAMS && !(e2 && e2[0] == '0')) ? 1
-                                                                                                                : 0;
-            if (e2 && e2[0] == '2') W.sw = (W.fused && !shard && P.n_tiles > 0 && n_sw <= 256) ? 1 : 0;  // A/B
-            // larger windows, opt-in (MIBA_FPL=1): the tiled points' point side in the Schur tiles. k_lin_point
-            // 48 -> 25 us at C4 but the tiles 76 -> 133 us (their per-chunk point reduction and tail run on one
-            // wave between two barriers, and the registers spill), 4140 -> 3650 LM it/s (DESIGN §4.3)
-            const char* e3 = std::getenv("MIBA_FPL");
-            W.fpl = (W.fused && !shard && !W.det_tbuf && P.n_tiles > 0 && !W.sw && e3 && e3[0] == '1') ? 1 : 0;
-            W.sw_cnt = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 2);
-            W.sw_seq = 0;
-            HIPCHECK(ctx, hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));
             // the band solve's tail (back-substitution chunks + decision) in its launch: unsharded default-mode band
             // windows whose tail fits one resident round; MIBA_TAIL=0 keeps the separate launches
             const char* e4 = std::getenv("MIBA_TAIL");
@@ -1336,6 +1321,23 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             W.tail_flags = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 4);
             W.tail_seq = 0;
             HIPCHECK(ctx, hipMemsetAsync(W.tail_flags, 0, 2 * sizeof(unsigned), s));
+            const char* e2 = std::getenv("MIBA_SW");
+            const int n_sw = P.n_tiles + 1 + n_seg + pp_blocks(n_ap - n_tiled, 1) + n_env;
+            // one-block windows (<= BCR_CAMS active cameras) and the band tail's windows. The camera side hands
+            // its sums to the envelope tiles without a release fence (round 5): C3 with the tail launch 58.8-58.9 us
+            // per LM iteration against 62.1-62.3 with k_lin_point (same box); round 4's fenced hand-off measured
+            // 3 us slower than k_lin_point there. MIBA_SW=0: off; 2: every window that fits
+            const bool sw_fit = W.fused && !shard && P.n_tiles > 0 && n_sw <= 256;
+            W.sw = (sw_fit && (nac <= BCR_CAMS || W.tail) && !(e2 && e2[0] == '0')) ? 1 : 0;
+            if (e2 && e2[0] == '2') W.sw = sw_fit ? 1 : 0;  // A/B
+            // larger windows, opt-in (MIBA_FPL=1): the tiled points' point side in the Schur tiles. k_lin_point
+            // 48 -> 25 us at C4 but the tiles 76 -> 133 us (their per-chunk point reduction and tail run on one
+            // wave between two barriers, and the registers spill), 4140 -> 3650 LM it/s (DESIGN §4.3)
+            const char* e3 = std::getenv("MIBA_FPL");
+            W.fpl = (W.fused && !shard && !W.det_tbuf && P.n_tiles > 0 && !W.sw && e3 && e3[0] == '1') ? 1 : 0;
+            W.sw_cnt = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 2);
+            W.sw_seq = 0;
+            HIPCHECK(ctx, hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));
         }
         ctx->n_adm_all = n_adm_all;
         ctx->sw_full = W.sw;

@@ -297,8 +297,9 @@ def test_small_window_fused_schur(case, monkeypatch):
         p = synthetic.make_problem(24, 1500, obs_per_point=(1, 8), seed=72, fixed_cam=3, dup_frac=0.01)
     no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
     so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=6, **no_tol))
-    # the default takes it for one-block windows (<= 10 active cameras); MIBA_SW=2 forces it on larger ones
-    on = "1" if p.n_cams <= 11 else "2"
+    # the default takes it for one-block windows (<= 10 active cameras) and the band tail's windows (C3); MIBA_SW=2
+    # forces it on the others that fit one resident round
+    on = "1" if p.n_cams <= 11 or case == "C3" else "2"
     res = {}
     for sw in (on, "0"):
         monkeypatch.setenv("MIBA_SW", sw)
