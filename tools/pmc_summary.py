@@ -18,7 +18,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     n = re.sub(r"<.*>", "", n)
     n = n.replace("void ", "").replace("miba::", "")
     return n[2:] if n.startswith("k_") else n

@@ -16,6 +16,11 @@ import statistics
 import sys
 
 
+def kname(n):
+    """Kernel symbol without its argument list ('(anonymous namespace)::' dropped first)."""
+    return n.replace("(anonymous namespace)::", "").split("(")[0]
+
+
 def rows_from_csv(path):
     out = []
     for r in csv.DictReader(open(path)):
@@ -59,7 +64,7 @@ def main(argv):
         f.write(f"# {title}\n\nSource: `rocprofv3 --kernel-trace --stats` ({src.split('/')[-1]}).\n\n")
         f.write("| kernel | calls | avg us | min us | max us | total ms | % |\n|---|---|---|---|---|---|---|\n")
         for r in rows:
-            name = r["name"].split("(")[0]
+            name = kname(r["name"])
             f.write(f"| `{name}` | {r['calls']} | {r['avg'] / 1e3:.2f} | {r['mn'] / 1e3:.2f} | "
                     f"{r['mx'] / 1e3:.2f} | {r['tot'] / 1e6:.3f} | {100.0 * r['tot'] / total:.2f} |\n")
         trace = src.replace("_kernel_stats.csv", "_kernel_trace.csv")
@@ -72,7 +77,7 @@ def main(argv):
             for name, k in order:
                 if not k["d"] or name.startswith("__amd"):
                     continue
-                f.write(f"| `{name.split('(')[0]}` | {len(k['d'])} | {statistics.median(k['d']):.2f} | {k['grid']} | "
+                f.write(f"| `{kname(name)}` | {len(k['d'])} | {statistics.median(k['d']):.2f} | {k['grid']} | "
                         f"{k['wg']} | {k['vgpr']} | {k['agpr']} | {k['lds']} | {k['scratch']} |\n")
 
 
