@@ -626,7 +626,8 @@ static int upload_params(ba_context* ctx, const ba_problem* p, hipStream_t s) {
 static unsigned long long env_key() {
     static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
                                         "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED", "MIBA_SW", "MIBA_FPL",
-                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES", "MIBA_DEVICE_PLAN", "MIBA_TAIL"};
+                                        "MIBA_BCR_DENSE1", "MIBA_PP_LANES", "MIBA_DEVICE_PLAN", "MIBA_TAIL",
+                                        "MIBA_BCR_BAND"};
     unsigned long long h = 1469598103934665603ull;
     for (const char* n : names) {
         const char* v = std::getenv(n);
