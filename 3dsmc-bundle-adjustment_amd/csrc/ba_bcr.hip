@@ -1404,8 +1404,15 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                                                      double* __restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nblk = Bw.nblk;
-    const int i = blockIdx.x / (NH + 1);
-    const int role = blockIdx.x % (NH + 1);  // 0 factor, 1 helper (A), 2 helper B
+    // workgroup id (xmap: launch workgroup b on XCD b mod 8; only XCDs 0-3 take a role, densely numbered)
+    int bid = blockIdx.x;
+    if (Bw.xmap) {
+        if ((bid & 7) >= 4) return;
+        bid = (bid >> 3) * 4 + (bid & 7);
+        if (bid >= (NH + 1) * nblk) return;
+    }
+    const int i = bid / (NH + 1);
+    const int role = bid % (NH + 1);  // 0 factor, 1 helper (A), 2 helper B
     // elimination tree on virtual indices v = i + voff (balanced: the root is the middle block, depth
     // floor(log2 nblk) + 1 instead of ceil(log2 nblk) + 1 with block 0 as the root)
     const bool root = i == Bw.vroot;
@@ -1591,7 +1598,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                 double dn = bcast_b(a[0], 0);
                 // shader-clock stamps around the first and last chains' pivots (slots 28-31): cycles per pivot in
                 // the kernel, beside the micro-benchmark's (tools/pivot_chain_bench.hip)
-                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 28 + (kb ? 2 : 0)] = bcr_stamp();
+                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * bid + 28 + (kb ? 2 : 0)] = bcr_stamp();
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     // d = current pivot; y ~ d^-1/2 (v_rsq_f64), one Newton step folded into l = a y (1 + e/2)
@@ -1609,7 +1616,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                         for (int k = j + 1; k < 16; ++k) a[k] = __builtin_fma(-l, bcast_b(l, k), a[k]);
                     }
                 }
-                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * blockIdx.x + 29 + (kb ? 2 : 0)] = bcr_stamp();
+                if constexpr (STAMP) if (lane == 0 && (kb == 0 || kb == 3)) tl[32 * bid + 29 + (kb ? 2 : 0)] = bcr_stamp();
                 if (live)
 #pragma unroll
                     for (int c = 0; c < 16; ++c) T[row * BLD + 16 * kb + c] = (r >= 16 || c <= r) ? a[c] : 0.0;
@@ -1670,7 +1677,7 @@ __global__ __launch_bounds__(TPB_E) void k_bcr_split(const LmState* __restrict__
                     for (int m = 0; m < 16; ++m) st_pub(pg + BB * BB + kb * 256 + m * 16 + lane, v[m]);
                     st_pub(pg + BB * BB + 4 * 256 + 16 * kb + lane, rd[lane]);
                 }
-                if constexpr (STAMP) if (lane == 0) tl[32 * blockIdx.x + 2 + kb] = realtime_now();
+                if constexpr (STAMP) if (lane == 0) tl[32 * bid + 2 + kb] = realtime_now();
             }
         }
         if (!ok) raise_flag(flag, FLAG_TIMEOUT);
@@ -2415,7 +2422,8 @@ static bool bcr_coop() {
 template <bool STAMP, int NH>
 static hipError_t launch_split(const DevProblem& P, const BaConsts& c, DevWork& W, const BcrWork& Bw, hipStream_t s,
                                unsigned long long* stamps, Prof* pf) {
-    const dim3 grid((NH + 1) * Bw.nblk), block(TPB_E);
+    const int nwg = (NH + 1) * Bw.nblk;
+    const dim3 grid(Bw.xmap ? 8 * ((nwg + 3) / 4) : nwg), block(TPB_E);
     if (!bcr_coop()) {
         BPL(K_BCR_PERSIST, (k_bcr_split<STAMP, NH>), grid, block, sizeof(HLds), s, W.st, P, W.S, W.rhs, Bw, W.chol_flag,
             stamps, c, W.scale, W.camdata, W.lin, W.delta, W.part);
@@ -2548,6 +2556,20 @@ int bcr_persist_ok(int nblk) {
         hipSuccess)
         return 0;
     return per_cu >= 1 && nblk <= per_cu * ncu ? 1 : 0;
+}
+
+// MIBA_BCR_XMAP=1 (opt-in): k_bcr_split's workgroups on XCDs 0-3 only, when they all fit there at once (every
+// workgroup of the split kernel waits on others: a launch that does not fit would time out)
+int bcr_xmap_ok(int nblk, int persist) {
+    const char* e = std::getenv("MIBA_BCR_XMAP");
+    if (!(e && e[0] == '1') || persist < 2) return 0;
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    const hipError_t r = persist == 3
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_split<false, 2>, TPB_E, sizeof(HLds))
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bcr_split<false, 1>, TPB_E, sizeof(HLds));
+    return r == hipSuccess && persist * nblk <= per_cu * (ncu / 2) ? 1 : 0;
 }
 
 hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s, Prof* pf) {

@@ -141,6 +141,8 @@ struct BcrWork {
     int dense1;   // one-block window solved by k_bcr_dense1 (bcr_dense1_ok)
     int band;     // narrow-band window solved in one workgroup by k_bcr_band (ba_band.hip): cameras per block
                   // (1..3 = max(camera band, 1)), 0 = off (bcr_band_ok)
+    int xmap;     // k_bcr_split on XCDs 0-3 only (one I/O die: 385 vs 510-580 ns per cross-workgroup hop,
+                  // tools/handoff_probe.hip): launch workgroup b runs on XCD b mod 8, those on XCDs 4-7 exit
 };
 // k_bcr_split's flag-free back-substitution hand-off: y rows double-buffered by epoch parity (Y even,
 // Racc odd — Racc belongs to the per-level path only); an empty slot holds this signalling-NaN pattern,
@@ -410,6 +412,7 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
 // 2 when the 2 * nblk workgroups of k_bcr_split can all be resident on the current device, else 1
 // when the nblk workgroups of k_bcr_persist can, else 0
 int bcr_persist_ok(int nblk);
+int bcr_xmap_ok(int nblk, int persist);
 int bcr_dense1_ok(int nblk, int kb);
 // cameras per block of the one-workgroup band solve for this window (0: not eligible; MIBA_BCR_BAND)
 // (one_block: also windows of one 64-dof block, where the band solve runs with its tail launch)

@@ -627,7 +627,7 @@ static unsigned long long env_key() {
     static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
                                         "MIBA_BCR", "MIBA_XCD_MAP", "MIBA_FUSED", "MIBA_SW", "MIBA_FPL",
                                         "MIBA_BCR_DENSE1", "MIBA_PP_LANES", "MIBA_DEVICE_PLAN", "MIBA_TAIL",
-                                        "MIBA_BCR_BAND"};
+                                        "MIBA_BCR_BAND", "MIBA_BCR_XMAP"};
     unsigned long long h = 1469598103934665603ull;
     for (const char* n : names) {
         const char* v = std::getenv(n);
@@ -655,6 +655,7 @@ static int bcr_setup(ba_context* ctx) {
         else if (!std::strcmp(e, "persist") && Bw.persist >= 2) Bw.persist = 1;
         else if (!std::strcmp(e, "split") && Bw.persist == 3) Bw.persist = 2;  // "split3" or unset: default
     }
+    Bw.xmap = bcr_xmap_ok(Bw.nblk, Bw.persist);
     ctx->bcr_fallback = false;
     return bcr_init_handoffs(ctx);
 }

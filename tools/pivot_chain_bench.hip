@@ -6,6 +6,8 @@
 //      step (rcp + 3 dependent ops + readlane on the chain instead of rsq + 4); l and the trailing updates as 0
 //   2  variant 0 without the trailing updates (the chain alone: a lower bound)
 //   3  variant 0 with the trailing updates of columns j + 2.. fed by an LDS broadcast of the multipliers
+//   4  variant 0 with pivot j - 1's trailing updates issued inside pivot j's chain (sched_barrier fences; same L)
+//   5  variant 4 without the fences
 // Reports ns and shader cycles per pivot and the max |L L^T - A| of the last repetition.
 // build: hipcc --offload-arch=gfx950 -O3 tools/pivot_chain_bench.hip -o /tmp/pcb && /tmp/pcb
 #include <hip/hip_runtime.h>
@@ -113,6 +115,51 @@ __device__ __forceinline__ void chain(double (&a)[16], double& my_inv, double* l
     }
 }
 
+
+template <int V>
+__device__ __forceinline__ void chain_pipe(double (&a)[16], double& my_inv) {
+    // variant 4 / 5: the trailing updates of pivot j - 1 (columns j + 1..15) issue inside pivot j's chain, which
+    // does not read them (column j + 1 first: the next pivot needs it). Every element still receives its updates
+    // in pivot order, so L is bitwise the kernel's. 5: the same code order without scheduling fences.
+    const int r = threadIdx.x & 63;
+    double dn = bcast(a[0], 0);
+    double lp = 0.0;  // this lane's multiplier of the previous pivot
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const double d = dn;
+        const double y = __builtin_amdgcn_rsq(d);
+        if (j >= 1 && j + 1 < 16) a[j + 1] = __builtin_fma(-lp, bcast(lp, j + 1), a[j + 1]);
+        if constexpr (V == 4) __builtin_amdgcn_sched_barrier(0);
+        const double dy = d * y;
+        constexpr int dummy = 0; (void)dummy;
+        // the deferred trailing updates, split over the chain's dependent steps
+        const int k0 = j + 2, n = 16 - k0 > 0 ? 16 - k0 : 0;
+        const int c1 = k0 + n / 3, c2 = k0 + (2 * n) / 3;
+        if (j >= 1)
+#pragma unroll
+            for (int k = k0; k < c1; ++k) a[k] = __builtin_fma(-lp, bcast(lp, k), a[k]);
+        if constexpr (V == 4) __builtin_amdgcn_sched_barrier(0);
+        const double e = __builtin_fma(-dy, y, 1.0);
+        const double ay = a[j] * y;
+        if (j >= 1)
+#pragma unroll
+            for (int k = c1; k < c2; ++k) a[k] = __builtin_fma(-lp, bcast(lp, k), a[k]);
+        if constexpr (V == 4) __builtin_amdgcn_sched_barrier(0);
+        const double l = __builtin_fma(0.5 * ay, e, ay);
+        my_inv = (r == j) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+        a[j] = l;
+        if (j >= 1)
+#pragma unroll
+            for (int k = c2; k < 16; ++k) a[k] = __builtin_fma(-lp, bcast(lp, k), a[k]);
+        if constexpr (V == 4) __builtin_amdgcn_sched_barrier(0);
+        if (j < 15) {
+            dn = bcast(__builtin_fma(-l, l, a[j + 1]), j + 1);
+            a[j + 1] = __builtin_fma(-l, bcast(l, j + 1), a[j + 1]);
+        }
+        lp = l;
+    }
+}
+
 template <int V>
 __global__ __launch_bounds__(64) void k_bench(const double* __restrict__ A, double* __restrict__ L,
                                               unsigned long long* __restrict__ t, int reps) {
@@ -126,7 +173,7 @@ __global__ __launch_bounds__(64) void k_bench(const double* __restrict__ A, doub
     for (int it = 0; it < reps; ++it) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) a[c] = a0[c] + sink * 1e-300;  // depends on the previous repetition
-        chain<V>(a, my_inv, lb);
+        if constexpr (V >= 4) chain_pipe<V>(a, my_inv); else chain<V>(a, my_inv, lb);
         sink = bcast(a[15], 63);
     }
     const unsigned long long c1 = clk(), t1 = rt();
@@ -154,14 +201,16 @@ int main() {
     (void)hipMalloc(&dA, 8 * A.size()); (void)hipMalloc(&dL, 8 * A.size()); (void)hipMalloc(&dt, 16);
     (void)hipMemcpy(dA, A.data(), 8 * A.size(), hipMemcpyHostToDevice);
     const int reps = 2000;
-    const char* names[4] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)",
-                            "LDS-broadcast trailing"};
+    const char* names[6] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)",
+                            "LDS-broadcast trailing", "deferred trailing, fenced", "deferred trailing, unfenced"};
     for (int round = 0; round < 2; ++round)
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < 6; ++v) {
             if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 2) hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 3) hipLaunchKernelGGL(k_bench<3>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 4) hipLaunchKernelGGL(k_bench<4>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 5) hipLaunchKernelGGL(k_bench<5>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             unsigned long long t[2];
             std::vector<double> L(64 * 16);
             (void)hipMemcpy(t, dt, 16, hipMemcpyDeviceToHost);
