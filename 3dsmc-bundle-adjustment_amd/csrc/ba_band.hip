@@ -184,7 +184,7 @@ struct BandItem {
     int ok, r, b1_arr, b2_arr, boff, bs, dst_arr, doff, mirror, two, keep;
 };
 
-template <int BC, bool STAMP>
+template <int BC, bool STAMP, bool PUB = false>
 __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const DevProblem& P,
                                           const double* __restrict__ S, double* __restrict__ rhs,
                                           int* __restrict__ flag, const BaConsts& c, const double* __restrict__ scale,
@@ -613,7 +613,7 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
     stamp();  // 2K + 4: back-substitution
     // ---- y to rhs (the points' back-substitution reads it); the step (block_step's arithmetic and grouping: wave w =
     // cameras [10 w, 10 w + 10), w = 0 also the intrinsics; part slot w)
-    for (int d = tid; d < ncd + 4; d += TPB) rhs[d] = d < ncd ? YV[d] : yk[d - ncd];
+    for (int d = tid; d < ncd + 4; d += TPB) st_opt<PUB>(rhs + d, d < ncd ? YV[d] : yk[d - ncd]);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int e = tid + q * TPB;
@@ -636,7 +636,7 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
             }
 #pragma unroll
             for (int k = 0; k < 7; ++k) o.x[k] = op[18 + k];
-            cam_step(P, c, cur, radius, o, t, YV + 6 * t, delta, acc);
+            cam_step<PUB>(P, c, cur, radius, o, t, YV + 6 * t, delta, acc);
         } else if (w == 0 && lane == BCR_CAMS) {
             IntrStepOps o;
             const double* op = lds + Ly.IOPS;
@@ -648,7 +648,7 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
                 o.gk[k] = op[12 + k];
                 o.prior[k] = op[16 + k];
             }
-            intr_step(P, c, cur, radius, o, yk, delta, acc);
+            intr_step<PUB>(P, c, cur, radius, o, yk, delta, acc);
         }
         // (lanes >= 16 hold no term: a 16-lane butterfly in a fixed order)
         static_assert(BCR_CAMS + 1 <= 16, "the step's terms sit on lanes < 16");
@@ -657,10 +657,10 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
 #pragma unroll
             for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off, 16);
         if (lane == 0) {
-            part[PART_UPD_SN2 * P.part_stride + w] = acc[0];
-            part[PART_UPD_MCC * P.part_stride + w] = acc[1];
-            part[PART_UPD_COST * P.part_stride + w] = acc[2];
-            part[PART_UPD_XN2 * P.part_stride + w] = acc[3];
+            st_opt<PUB>(part + PART_UPD_SN2 * P.part_stride + w, acc[0]);
+            st_opt<PUB>(part + PART_UPD_MCC * P.part_stride + w, acc[1]);
+            st_opt<PUB>(part + PART_UPD_COST * P.part_stride + w, acc[2]);
+            st_opt<PUB>(part + PART_UPD_XN2 * P.part_stride + w, acc[3]);
         }
     }
     stamp();  // 2K + 5: step
@@ -717,12 +717,13 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
     LmState* const st = const_cast<LmState*>(st_c);
     const int b = blockIdx.x, tid = threadIdx.x;
     if (b == 0) {
-        band_body<BC, false>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, nullptr, lds);
-        __syncthreads();  // every thread's stores of y, the candidate cameras and the partials are issued
-        if (tid == 0) {
-            __threadfence();
-            __hip_atomic_store(tflags, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        // y, the candidate cameras and intrinsics, the step and the partials are stored past the L2 (PUB) and
+        // drained by every thread before the count: no L2 write-back fence on the critical path (the consumers
+        // read them with agent-scope loads)
+        band_body<BC, false, true>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, nullptr, lds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(tflags, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     if (tid >= 256) return;  // (the back-substitution and final bodies are written for 256 threads)

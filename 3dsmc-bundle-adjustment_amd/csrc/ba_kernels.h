@@ -191,6 +191,17 @@ __device__ __forceinline__ void load_cam_step_ops(const DevProblem& P, int cur, 
 #pragma unroll
     for (int j = 0; j < 7; ++j) o.x[j] = x[j];
 }
+// PUB: a store past the L2 (agent-scope relaxed 8-byte atomic store), for a consumer of the same launch on another
+// XCD that reads with agent-scope loads once the producer has drained its stores (the band tail launch)
+template <bool PUB>
+__device__ __forceinline__ void st_opt(double* p, double v) {
+    if constexpr (PUB)
+        __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+template <bool PUB = false>
 __device__ __forceinline__ void cam_step(const DevProblem& P, const BaConsts& c, int cur, double radius,
                                          const CamStepOps& o, int t, const double* yv, double* __restrict__ delta,
                                          double acc[4]) {
@@ -199,7 +210,7 @@ __device__ __forceinline__ void cam_step(const DevProblem& P, const BaConsts& c,
     for (int k = 0; k < 6; ++k) {
         const double sc = o.sc[k], yk = yv[k];
         d[k] = -yk * sc;
-        delta[6 * t + k] = d[k];
+        st_opt<PUB>(delta + 6 * t + k, d[k]);
         const double u = sc * o.ud[k] * sc;  // diag of s U s (k_env_assemble)
         const double dd = fmin(fmax(u, c.min_diag), c.max_diag) / radius;
         acc[1] += 0.5 * ((sc * o.g[k]) * yk + dd * yk * yk);
@@ -209,7 +220,7 @@ __device__ __forceinline__ void cam_step(const DevProblem& P, const BaConsts& c,
     se3_plus(o.x, d, tp);
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
-        xn[j] = tp[j];
+        st_opt<PUB>(xn + j, tp[j]);
         const double df = o.x[j] - tp[j];
         acc[0] += df * df;
         acc[3] += tp[j] * tp[j];
@@ -237,6 +248,7 @@ __device__ __forceinline__ void load_intr_step_ops(const DevProblem& P, int cur,
         o.prior[m] = P.prior[m];
     }
 }
+template <bool PUB = false>
 __device__ __forceinline__ void intr_step(const DevProblem& P, const BaConsts& c, int cur, double radius,
                                           const IntrStepOps& o, const double* yk4, double* __restrict__ delta,
                                           double acc[4]) {
@@ -244,9 +256,9 @@ __device__ __forceinline__ void intr_step(const DevProblem& P, const BaConsts& c
     for (int m = 0; m < 4; ++m) {
         const double sk = o.sk[m], ym = yk4[m];
         const double dk = -ym * sk;
-        delta[P.kb + m] = dk;
+        st_opt<PUB>(delta + P.kb + m, dk);
         const double kn = o.K[m] + dk;
-        Kn[m] = kn;
+        st_opt<PUB>(Kn + m, kn);
         const double df = o.K[m] - kn;
         acc[0] += df * df;
         const double u = sk * o.uk[m] * sk;  // Ukk incl. the prior block

@@ -947,7 +947,7 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
         }
         return;
     }
-    unsigned long long t_prev = 0, st_acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long t_prev = 0, st_acc[5] = {0, 0, 0, 0, 0}, sub_st[5] = {0, 0, 0, 0, 0};
 #define SCH_STAMP(k)                                          \
     do {                                                      \
         if constexpr (STAMP) {                                \
@@ -988,6 +988,9 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
     }
     // the valid slots are a prefix; their count is wave-uniform (empty slots issue no MFMA)
     const int ntok = __builtin_amdgcn_readfirstlane((int)tok[0] + (int)tok[1] + (int)tok[2] + (int)tok[3]);
+    // waves of the rhs-aside dot product: all four when the product has at most 4 tiles (one MFMA tile per wave at
+    // most), else wave 3 alone (spread over the 2-tile waves 2-3 of the 10-tile shape it measured slower at C4)
+    const int dw0 = ntl <= 4 ? 0 : 3;
     d4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
@@ -1081,7 +1084,9 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
 #pragma unroll
                 for (int i = 0; i < 21; ++i) psum[i * CHUNK_OBS + tid] = a[i];
             }
+            if constexpr (STAMP) if (tid == 0) sub_st[2] += stamp_now() - t_prev;
             __syncthreads();
+            if constexpr (STAMP) if (tid == 0) sub_st[3] += stamp_now() - t_prev;
             if (tid < npts) {
                 const int ap = apb + tid;
                 const int q0 = P.pt_ptr[ap] - ob, q1 = P.pt_ptr[ap + 1] - ob;
@@ -1102,6 +1107,7 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
 #pragma unroll
                 for (int k = 0; k < 6; ++k) gL[6 * tid + k] = rec[k];
             }
+            if constexpr (STAMP) if (tid == 0) sub_st[4] += stamp_now() - t_prev;
             __syncthreads();  // (psum is M': read before the clear)
         }
         {
@@ -1167,9 +1173,10 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
             load_rec(oe + tid);
             load_pq(ape, ape_n);
         }
-        // ---- rhs row aside: rhs_acc(r) += sum_k M'[r][k] ze[k] (wave 3, lane = camera row r): four
-        // interleaved partial chains (k mod 4; f64 FMA dependent latency is 32 cycles), summed in a fixed order
-        if (rhs_aside && wave == 3 && lane < kr) {
+        // ---- rhs row aside: rhs_acc(r) += sum_k M'[r][k] ze[k] (lane = camera row r), the chunk's k-steps split
+        // over the dot waves (waves dw0..3: all four when the product has few tiles, the two 2-tile waves of the
+        // 10-tile shape); each wave four interleaved partial chains (k mod 4), its k-steps' loads issued together
+        if (rhs_aside && dw0 == 3 && wave == 3 && lane < kr) {  // (the large tiles: wave 3 alone, k in order)
             const int nk = 3 * npts;
             double ra[4] = {0.0, 0.0, 0.0, 0.0};
             int k = 0;
@@ -1178,7 +1185,30 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
                 for (int u = 0; u < 4; ++u) ra[u] = __builtin_fma(Mt[(k + u) * SCH_LDM + lane], zeL[k + u], ra[u]);
             for (; k < nk; ++k) ra[0] = __builtin_fma(Mt[k * SCH_LDM + lane], zeL[k], ra[0]);
             rhs_acc += (ra[0] + ra[1]) + (ra[2] + ra[3]);
+        } else if (rhs_aside && dw0 < 3 && lane < kr) {
+            const int nk = 3 * npts, ns = (nk + 3) >> 2, nw = 4 - dw0, wi = wave - dw0;
+            const int s0 = ns * wi / nw, s1 = ns * (wi + 1) / nw;
+            double ra[4] = {0.0, 0.0, 0.0, 0.0};
+            constexpr int UNR = 4;
+            for (int sb = s0; sb < s1; sb += UNR) {
+                double mv[UNR][4], zv[UNR][4];
+#pragma unroll
+                for (int q = 0; q < UNR; ++q)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = 4 * (sb + q) + u;
+                        const bool in = sb + q < s1 && k < nk;  // (zeL past the chunk's columns is stale)
+                        mv[q][u] = in ? Mt[k * SCH_LDM + lane] : 0.0;
+                        zv[q][u] = in ? zeL[k] : 0.0;
+                    }
+#pragma unroll
+                for (int q = 0; q < UNR; ++q)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) ra[u] = __builtin_fma(mv[q][u], zv[q][u], ra[u]);
+            }
+            rhs_acc += (ra[0] + ra[1]) + (ra[2] + ra[3]);
         }
+        if constexpr (STAMP && FP) if (tid == 0) sub_st[0] += stamp_now() - t_prev;
         // ---- phase B: acc[t] += M'[16 ib..][k] M'[16 jb..][k]^T over the chunk's K
         const int ksteps = (3 * npts + 3) >> 2;
         if ((rhs_aside && nrt == 4) || (!rhs_aside && nrt == 5)) {
@@ -1239,6 +1269,21 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
                     default: run(std::integral_constant<int, 5>{}, I3{}); break;
                 }
             }
+        } else if (ntl == 1) {
+            // one 16 x 16 tile (span <= 2: the TUM windows' tiles), M'_0 M'_0^T: the chunk's k-steps split over the
+            // four waves (a quarter each, partial products summed in wave order at the flush), each wave's operand
+            // rows loaded in one block ahead of its MFMA chain (a wave alone on its SIMD waits out every LDS round
+            // trip a one-step-ahead prefetch leaves exposed)
+            const double* row = Mt + kq * SCH_LDM + rr;
+            const int s0 = ksteps * wave / 4, s1 = ksteps * (wave + 1) / 4;
+            constexpr int KB = 8;
+            static_assert(KB * 4 >= SCH_K / 4, "a quarter of a chunk's k-steps in one block");
+            double av[KB];
+#pragma unroll
+            for (int q = 0; q < KB; ++q) av[q] = s0 + q < s1 ? row[(s0 + q) * 4 * SCH_LDM] : 0.0;
+#pragma unroll
+            for (int q = 0; q < KB; ++q)
+                if (s0 + q < s1) acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], av[q], acc[0], 0, 0, 0);
         } else {
             const double* row = Mt + kq * SCH_LDM + rr;
             double a[4], b[4];
@@ -1257,6 +1302,7 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
                 row = nrow;
             }
         }
+        if constexpr (STAMP && FP) if (tid == 0) sub_st[1] += stamp_now() - t_prev;
         if (!more) break;
         // ---- prefetch: level-2 operands of the next chunk
         const int oe_n = P.pt_ptr[ape_n];
@@ -1269,6 +1315,24 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
     }
     __syncthreads();
     SCH_STAMP(2);
+    if ((rhs_aside && dw0 < 3) || ntl == 1) {  // (tile-uniform) partials summed in wave order, before any global
+        // store of the flush (a barrier after them would wait for their acknowledgement): the dot waves' rhs rows on
+        // wave 3; the one-tile product's k-quarters on wave 0
+        if (rhs_aside && wave >= dw0 && wave < 3 && lane < kr) Mt[wave * 64 + lane] = rhs_acc;
+        if (ntl == 1 && wave > 0)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Mt[256 + (wave - 1) * 256 + g * 64 + lane] = acc[0][g];
+        __syncthreads();
+        if (rhs_aside && wave == 3 && lane < kr) {
+            double v = 0.0;
+            for (int w = dw0; w < 3; ++w) v += Mt[w * 64 + lane];
+            rhs_acc += v;
+        }
+        if (ntl == 1 && wave == 0)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                acc[0][g] += (Mt[256 + g * 64 + lane] + Mt[512 + g * 64 + lane]) + Mt[768 + g * 64 + lane];
+    }
     // ---- flush (lower triangle of S, row-major npad); C/D layout row = kq + 4g, col = rr
     const size_t ld = P.npad;
 #pragma unroll
@@ -1325,6 +1389,9 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
         SCH_STAMP(3);
         if (threadIdx.x == 0)
             for (int k = 0; k < 5; ++k) stamps[(size_t)blockIdx.x * 5 + k] = st_acc[k];
+        if constexpr (FP) if (threadIdx.x == 0) {  // phase B on wave 0: after the rhs dot, after the MFMA loop
+            for (int k = 0; k < 5; ++k) stamps[(size_t)5 * 256 + 5 * blockIdx.x + k] = sub_st[k];
+        }
     }
 #undef SCH_STAMP
 }
@@ -2529,7 +2596,7 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             fp_stamps = (e && e[0] == '1') ? 1 : 0;
         }
         if (fp_stamps == 1 && P.obs32) {  // diagnostic: per-tile phase cycles (zero, A incl. the point side, B, flush)
-            if (!fst) CK(hipMalloc(&fst, sizeof(unsigned long long) * 5 * 256));
+            if (!fst) CK(hipMalloc(&fst, sizeof(unsigned long long) * 10 * 256));
             PL(K_SCHUR_TILE, (k_schur_tile<true, true, true, true, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale,
                W.pdata, W.S, W.rhs, fst, 0, W.part, (double*)nullptr, E);
             std::vector<unsigned long long> h5((size_t)5 * P.n_tiles);
@@ -2538,9 +2605,17 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
             double sum[5] = {0, 0, 0, 0, 0};
             for (int t = 0; t < P.n_tiles; ++t)
                 for (int k = 0; k < 5; ++k) sum[k] += (double)h5[5 * t + k];
+            std::vector<unsigned long long> hs((size_t)5 * P.n_tiles);
+            CK(hipMemcpy(hs.data(), fst + 5 * 256, sizeof(hs[0]) * hs.size(), hipMemcpyDeviceToHost));
+            double sb[5] = {0, 0, 0, 0, 0};
+            for (int t = 0; t < P.n_tiles; ++t)
+                for (int k = 0; k < 5; ++k) sb[k] += (double)hs[5 * t + k];
+            fprintf(stderr, "  point side (thread 0, from the tile start): evaluated %.0f, barrier passed %.0f, point tail "
+                    "done %.0f\n", sb[2] / P.n_tiles, sb[3] / P.n_tiles, sb[4] / P.n_tiles);
             fprintf(stderr, "schur_tile FP %d tiles, mean cycles/tile: point side + zero stores %.0f, barrier %.0f, phaseA %.0f, "
-                    "phaseB %.0f, flush %.0f\n", P.n_tiles, sum[4] / P.n_tiles, sum[0] / P.n_tiles, sum[1] / P.n_tiles,
-                    sum[2] / P.n_tiles, sum[3] / P.n_tiles);
+                    "phaseB %.0f (wave 0: rhs dot done %.0f, MFMA done %.0f), flush %.0f\n", P.n_tiles, sum[4] / P.n_tiles,
+                    sum[0] / P.n_tiles, sum[1] / P.n_tiles, sum[2] / P.n_tiles, sb[0] / P.n_tiles, sb[1] / P.n_tiles,
+                    sum[3] / P.n_tiles);
         } else
         OPL(K_SCHUR_TILE, (k_schur_tile<false, true, true, true, true>), (k_schur_tile<false, false, true, true, true>), dim3(n_sch),
             dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, (unsigned long long*)nullptr, 0, W.part,
