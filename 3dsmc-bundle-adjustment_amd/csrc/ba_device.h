@@ -242,7 +242,31 @@ __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const dou
         imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * t4;
         real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * t4;
     } else {
-        sincos(0.5 * theta, &sh, &ch);
+        const double h = 0.5 * theta;
+        if (h < 0.5) {
+            // |h| < 1/2 (every LM step short of a 1 rad rotation): the Taylor series to h^13 / h^14, truncation below
+            // 3e-17 absolute, in Horner form — a short FMA chain on the camera step's critical path instead of the
+            // library sincos' argument reduction and branches
+            const double h2 = h * h;
+            double ps = 1.0 / 6227020800.0;  // 1/13!
+            ps = __builtin_fma(ps, -h2, 1.0 / 39916800.0);
+            ps = __builtin_fma(ps, -h2, 1.0 / 362880.0);
+            ps = __builtin_fma(ps, -h2, 1.0 / 5040.0);
+            ps = __builtin_fma(ps, -h2, 1.0 / 120.0);
+            ps = __builtin_fma(ps, -h2, 1.0 / 6.0);
+            ps = __builtin_fma(ps, -h2, 1.0);
+            sh = h * ps;
+            double pc = 1.0 / 87178291200.0;  // 1/14!
+            pc = __builtin_fma(pc, -h2, 1.0 / 479001600.0);
+            pc = __builtin_fma(pc, -h2, 1.0 / 3628800.0);
+            pc = __builtin_fma(pc, -h2, 1.0 / 40320.0);
+            pc = __builtin_fma(pc, -h2, 1.0 / 720.0);
+            pc = __builtin_fma(pc, -h2, 1.0 / 24.0);
+            pc = __builtin_fma(pc, -h2, 0.5);
+            ch = __builtin_fma(pc, -h2, 1.0);
+        } else {
+            sincos(h, &sh, &ch);
+        }
         imag = sh / theta;
         real = ch;
     }
