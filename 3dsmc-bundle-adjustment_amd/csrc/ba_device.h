@@ -235,19 +235,22 @@ __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const dou
                                          double* __restrict__ out) {
     const double ox = d[3], oy = d[4], oz = d[5];
     const double theta_sq = ox * ox + oy * oy + oz * oz;
-    const double theta = sqrt(theta_sq);
-    double imag, real, sh = 0.0, ch = 1.0;
-    if (theta < 1e-10) {
+    double imag, real;
+    double V[9];
+    if (theta_sq < 1e-20) {  // theta < 1e-10: Sophus' small-angle branch (V = the rotation itself)
         const double t4 = theta_sq * theta_sq;
         imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * t4;
         real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * t4;
+        const double qd0[4] = {imag * ox, imag * oy, imag * oz, real};
+        quat_R(qd0, V);
     } else {
-        const double h = 0.5 * theta;
-        if (h < 0.5) {
-            // |h| < 1/2 (every LM step short of a 1 rad rotation): the Taylor series to h^13 / h^14, truncation below
-            // 3e-17 absolute, in Horner form — a short FMA chain on the camera step's critical path instead of the
-            // library sincos' argument reduction and branches
-            const double h2 = h * h;
+        double a, b;
+        if (theta_sq < 1.0) {
+            // theta < 1 (every LM step short of a 1 rad rotation): sin(theta / 2) = h ps(h^2), cos(theta / 2) =
+            // pc(h^2), (theta - sin theta) / theta^3 = pb(theta^2) by their Taylor series (truncated below 3e-17) in
+            // FMA form: imag = sin(h) / theta = ps / 2, a = 2 sin^2(h) / theta^2 = ps^2 / 2 — no square root,
+            // division or library sincos on the camera step's critical path
+            const double h2 = 0.25 * theta_sq;
             double ps = 1.0 / 6227020800.0;  // 1/13!
             ps = __builtin_fma(ps, -h2, 1.0 / 39916800.0);
             ps = __builtin_fma(ps, -h2, 1.0 / 362880.0);
@@ -255,7 +258,6 @@ __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const dou
             ps = __builtin_fma(ps, -h2, 1.0 / 120.0);
             ps = __builtin_fma(ps, -h2, 1.0 / 6.0);
             ps = __builtin_fma(ps, -h2, 1.0);
-            sh = h * ps;
             double pc = 1.0 / 87178291200.0;  // 1/14!
             pc = __builtin_fma(pc, -h2, 1.0 / 479001600.0);
             pc = __builtin_fma(pc, -h2, 1.0 / 3628800.0);
@@ -263,24 +265,28 @@ __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const dou
             pc = __builtin_fma(pc, -h2, 1.0 / 720.0);
             pc = __builtin_fma(pc, -h2, 1.0 / 24.0);
             pc = __builtin_fma(pc, -h2, 0.5);
-            ch = __builtin_fma(pc, -h2, 1.0);
+            real = __builtin_fma(pc, -h2, 1.0);
+            imag = 0.5 * ps;
+            a = 0.5 * ps * ps;
+            double pb = 1.0 / 355687428096000.0;  // 1/17!
+            pb = __builtin_fma(pb, -theta_sq, 1.0 / 1307674368000.0);
+            pb = __builtin_fma(pb, -theta_sq, 1.0 / 6227020800.0);
+            pb = __builtin_fma(pb, -theta_sq, 1.0 / 39916800.0);
+            pb = __builtin_fma(pb, -theta_sq, 1.0 / 362880.0);
+            pb = __builtin_fma(pb, -theta_sq, 1.0 / 5040.0);
+            pb = __builtin_fma(pb, -theta_sq, 1.0 / 120.0);
+            b = __builtin_fma(pb, -theta_sq, 1.0 / 6.0);
         } else {
-            sincos(h, &sh, &ch);
+            const double theta = sqrt(theta_sq);
+            double sh, ch;
+            sincos(0.5 * theta, &sh, &ch);
+            imag = sh / theta;
+            real = ch;
+            // sin(theta) and 1 - cos(theta) from the half-angle pair (2 sin^2(theta / 2) avoids the cancellation)
+            a = (2.0 * sh * sh) / theta_sq;
+            b = (theta - 2.0 * sh * ch) / (theta_sq * theta);
         }
-        imag = sh / theta;
-        real = ch;
-    }
-    const double qd[4] = {imag * ox, imag * oy, imag * oz, real};
-    double V[9];
-    if (theta < 1e-10) {
-        quat_R(qd, V);
-    } else {
-        // sin(theta) and 1 - cos(theta) from the half-angle pair already evaluated for the quaternion (one f64 sincos
-        // instead of two on the camera step's chain; 2 sin^2(theta / 2) also avoids the cancellation of 1 - cos)
         const double Om[9] = {0, -oz, oy, oz, 0, -ox, -oy, ox, 0};
-        const double s = 2.0 * sh * ch;
-        const double a = (2.0 * sh * sh) / theta_sq;
-        const double b = (theta - s) / (theta_sq * theta);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -289,6 +295,7 @@ __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const dou
                 V[i * 3 + j] = (i == j ? 1.0 : 0.0) + a * Om[i * 3 + j] + b * o2;
             }
     }
+    const double qd[4] = {imag * ox, imag * oy, imag * oz, real};
     double td[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) td[i] = V[i * 3 + 0] * d[0] + V[i * 3 + 1] * d[1] + V[i * 3 + 2] * d[2];
@@ -306,7 +313,10 @@ __device__ __forceinline__ void se3_plus(const double* __restrict__ T, const dou
     double nz = qw * bz + qz * bw + qx * by - qy * bx;
     const double sq = nx * nx + ny * ny + nz * nz + nw * nw;
     if (sq != 1.0) {
-        const double f = 2.0 / (1.0 + sq);
+        // 2 / (1 + sq) = 1 / (1 + e / 2), e = sq - 1: 1 - e / 2 + e^2 / 4 is exact to double for |e| < 1e-6 (a unit
+        // quaternion times a unit quaternion: e is a few ulp), a division otherwise
+        const double e = sq - 1.0;
+        const double f = fabs(e) < 1e-6 ? __builtin_fma(e, __builtin_fma(e, 0.25, -0.5), 1.0) : 2.0 / (1.0 + sq);
         nx *= f; ny *= f; nz *= f; nw *= f;
     }
     out[0] = nx; out[1] = ny; out[2] = nz; out[3] = nw;
