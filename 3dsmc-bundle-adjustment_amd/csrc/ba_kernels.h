@@ -21,6 +21,7 @@ static constexpr int CHUNK_OBS = 256;
 static constexpr int SCH_TBUF_LD = 6 * TILE_WIN;
 static constexpr int SCH_TBUF = 80 * SCH_TBUF_LD;
 static constexpr int SUBSEG_OBS = 1024;  // observations per camera-side sub-segment (one workgroup)
+static constexpr int SUBSEG_OBS_SMALL = 256;  // ... on windows of < 4096 observations
 static constexpr int SUBSEG_OBS_LARGE = 1700;  // the same on windows of >= 200k observations
 static constexpr int BS_PTS = 128;    // points per back-substitution chunk (C4: 64 / 512 29.4 us, 128 / 1024 27.6, 256 / 2048 33.1)
 static constexpr int BS_OBS = 1024;   // observations per back-substitution chunk (a single point may exceed)

@@ -161,7 +161,10 @@ void build_tiles(int n0, Fmin pmin, Fmax pmax, Fcnt cnt, const PlanParams& pp, P
     };
     const int slots = pp.tile_slots - 1;  // one resident slot for the intrinsics-term workgroup
     int tile_pts = 128;
-    if (slots > 0) tile_pts = std::max(pp.chunk_pts, (n0 + slots - 1) / slots);
+    // small windows (<= 64 chunks of points: the TUM windows) take half-chunk tiles — twice the tiles, each a
+    // shorter chain, in a launch that is far from filling the chip (C1 -1 to -2 % per LM iteration)
+    const int min_pts = n0 <= 64 * pp.chunk_pts ? std::max(1, pp.chunk_pts / 2) : pp.chunk_pts;
+    if (slots > 0) tile_pts = std::max(min_pts, (n0 + slots - 1) / slots);
     if (pp.tile_pts_env > 0) tile_pts = pp.tile_pts_env;
     for (int grow = 0; pp.tile_pts_env <= 0 && slots > 0 && grow < 16 && count(tile_pts) > slots; ++grow)
         tile_pts += std::max(1, tile_pts / 8);

@@ -764,7 +764,9 @@ static PlanParams plan_params(int n_adm) {
     pp.bs_obs = BS_OBS;
     // sub-segment size: ~6.5 observations per thread on large windows (C4 rocprof, fused linearisation:
     // 34.2 us at 1700 vs 36.1 at 1024, 42.7 at 512, 34.7 at 2500); MIBA_SUBSEG overrides (tuning)
-    pp.subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : SUBSEG_OBS;
+    // and 256 on windows of a few thousand observations (C1's camera side in its Schur launch: shorter per-thread
+    // chains, with the half-chunk tiles -2.4 % per LM iteration; neutral at C3's 8k, which keeps 1024)
+    pp.subseg = n_adm >= 200000 ? SUBSEG_OBS_LARGE : n_adm < 4096 ? SUBSEG_OBS_SMALL : SUBSEG_OBS;
     if (const char* e = std::getenv("MIBA_SUBSEG")) pp.subseg = std::max(64, std::atoi(e));
     return pp;
 }
