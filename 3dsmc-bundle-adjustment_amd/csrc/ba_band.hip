@@ -728,6 +728,10 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
     }
     if (tid >= 256) return;  // (the back-substitution and final bodies are written for 256 threads)
     const bool skip = skip_step(st);
+    // a back-substitution chunk loads its records and point data and evaluates its y-free products before it waits
+    BsPre<O32> pre;
+    BsPreLds* const pl = reinterpret_cast<BsPreLds*>(reinterpret_cast<char*>(lds) + sizeof(BsLds));
+    if (b <= nb_bs) backsub_pre<O32>(P, c, st, scale, pdata, b - 1, *pl, pre);
     // A wait past the spin bound marks the iteration for a re-run (FLAG_TIMEOUT) and then still waits for its
     // producer (which waits on nothing and runs ahead of its consumers in dispatch order) before this workgroup
     // touches S or rhs, which the re-run assembles onto
@@ -743,7 +747,7 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
         __syncthreads();
         if (ok_s) {
             backsub_body<O32, true>(P, c, st, scale, pdata, rhs, delta, part, ztiles, n_ztiles, S, b - 1, nb_bs,
-                                    *reinterpret_cast<BsLds*>(lds));
+                                    *reinterpret_cast<BsLds*>(lds), pre, pl);
         } else if (tid == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flag) drained before the count
         }
@@ -857,7 +861,8 @@ static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork&
 int band_tail_blocks(const DevProblem& P, int bc) {
     if (bc < 1 || bc > 3) return 0;
     const int n = P.n_bs_chunks + 2;
-    const size_t lds = std::max(band_lds_bytes(bc, (P.nac + bc - 1) / bc, P.nac), std::max(sizeof(BsLds), sizeof(FinLds)));
+    const size_t lds = std::max(band_lds_bytes(bc, (P.nac + bc - 1) / bc, P.nac),
+                                std::max(sizeof(BsLds) + sizeof(BsPreLds), sizeof(FinLds)));
     // one resident round with room to spare (>= 256 CUs), the dynamic LDS beside the launch's static word
     return (P.n_ap > 0 && n <= 128 && lds <= 160 * 1024 - 256) ? n : 0;
 }
@@ -875,7 +880,7 @@ static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const Lm
                                 160 * 1024 - 256));
         attr = true;
     }
-    const size_t lds = std::max(band_lds_bytes(BC, nb, P.nac), std::max(sizeof(BsLds), sizeof(FinLds)));
+    const size_t lds = std::max(band_lds_bytes(BC, nb, P.nac), std::max(sizeof(BsLds) + sizeof(BsPreLds), sizeof(FinLds)));
     const int nb_bs = P.n_bs_chunks;
     ++W.tail_seq;
     if (pf) pf->begin(K_BCR_PERSIST, s);

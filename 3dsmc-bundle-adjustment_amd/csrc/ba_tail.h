@@ -123,12 +123,79 @@ struct BsLds {
     double lds[4 * 5];
     double out[5];
 };
+// the band tail (BsPre): the chunk's point records, point scales and current points, loaded before the wait (in the
+// tail launch's dynamic LDS after BsLds; k_backsub_chunk's static BsLds stays as it was)
+struct BsPreLds {
+    double pt[BS_PTS][PDATA + 6];
+};
+// Band tail (PUB): what a back-substitution chunk can compute before the band solve's y exists — its observation
+// records, each thread's first observation's y-free product A = diag(s_p) Jp^T Jc diag(s_c) (3 x 6; v = A y_c
+// after the wait) and the chunk's point data in LDS — so only the y / candidate loads and short products follow it
+template <bool O32>
+struct BsPre {
+    bool on;            // the chunk is not a single big point and the window's state says step
+    int ac0;            // active camera of this thread's first observation (< 0: none / gauge)
+    double A[18];
+    int r_ap[BS_OBS / TPB];
+    ObsRaw<O32> r_o[BS_OBS / TPB];
+};
+template <bool O32>
+__device__ __forceinline__ void backsub_pre(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
+                                            const double* __restrict__ scale, const double* __restrict__ pdata, int ch,
+                                            BsPreLds& L, BsPre<O32>& B) {
+    B.on = false;
+    B.ac0 = -1;
+    if (skip_step(st)) return;
+    const int cur = st->cur;
+    const int tid = threadIdx.x;
+    const int apb = P.bs_chunk[ch], ape = P.bs_chunk[ch + 1];
+    const int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
+    if (oe - ob > BS_OBS) return;  // a single big point: the plain path after the wait
+    B.on = true;
+    constexpr int NR = BS_OBS / TPB;
+    int it = 0;
+    for (int o = ob + tid; o < oe; o += TPB, ++it) {
+        const int ap = P.po_ap[o];
+        const ObsRaw<O32> ro = po_obs<O32>(P, o);
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (k == it) { B.r_ap[k] = ap; B.r_o[k] = ro; }
+        if (it == 0) {
+            const int ac = P.po_ac[o];
+            B.ac0 = ac;
+            if (ac >= 0) {
+                ObsEval ev;
+                double jc[18], jp[9], jk[8];
+                lin_obs(c, P.cams[cur] + 7 * ro.idx(), P.pts[cur] + 3 * P.pt_idx[ap], P.K[cur], ro.u(), ro.v(), ro.d(),
+                        ev, jc, jp, jk);
+                const double* sc = scale + 6 * ac;
+                const double* sp = scale + P.off_pt + 3 * ap;
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int d = 0; d < 6; ++d)
+                        B.A[i * 6 + d] = sp[i] * ((jp[i] * jc[d] + jp[3 + i] * jc[6 + d]) + jp[6 + i] * jc[12 + d]) * sc[d];
+            }
+        }
+    }
+    for (int e = tid; e < (ape - apb) * (PDATA + 6); e += TPB) {  // point data, coalesced by element
+        const int pl = e / (PDATA + 6), q = e - pl * (PDATA + 6), ap = apb + pl;
+        double v;
+        if (q < PDATA) v = pdata[(size_t)ap * PDATA + q];
+        else if (q < PDATA + 3) v = scale[P.off_pt + 3 * (size_t)ap + q - PDATA];
+        else v = P.pts[cur][3 * (size_t)P.pt_idx[ap] + q - PDATA - 3];
+        L.pt[pl][q] = v;
+    }
+}
 template <bool O32, bool PUB = false>
 __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                              const double* __restrict__ scale, const double* __restrict__ pdata,
                                              const double* __restrict__ y, const double* __restrict__ delta,
                                              double* __restrict__ part, const int2* __restrict__ ztiles, int n_ztiles,
-                                             double* __restrict__ Sz, int ch, int nch, BsLds& L) {
+                                             double* __restrict__ Sz, int ch, int nch, BsLds& L,
+                                             const BsPre<O32>& pre = BsPre<O32>{}, BsPreLds* PL = nullptr) {
+    const bool use_pre = PL != nullptr;
+    const bool PRE = use_pre && pre.on;  // (block-uniform)
     auto& co = L.co;
     auto& dpl = L.dpl;
     double* const lds = L.lds;
@@ -158,6 +225,27 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     double bsum[3] = {0.0, 0.0, 0.0};
     int it = 0;
     for (int o = ob + tid; o < oe; o += TPB, ++it) {
+        if (PRE && it == 0) {  // the y-free product computed before the wait: v = A y_c
+#pragma unroll
+            for (int k = 0; k < NR; ++k) { r_ap[k] = pre.r_ap[k]; r_o[k] = pre.r_o[k]; }
+            double v[3] = {0.0, 0.0, 0.0};
+            const int ac = pre.ac0;
+            if (ac >= 0) {
+                double yv[6];
+#pragma unroll
+                for (int d = 0; d < 6; ++d) yv[d] = tail_ld(y + 6 * ac + d);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    double a = 0.0;
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) a = __builtin_fma(pre.A[i * 6 + d], yv[d], a);
+                    v[i] = a;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) co[o - ob][i] = v[i];
+            continue;
+        }
         const int ac = P.po_ac[o];
         const int ap = P.po_ap[o];
         const ObsRaw<O32> ro = po_obs<O32>(P, o);
@@ -194,10 +282,10 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     if (tid < npts) {
         const int ap = apb + tid;
         const int pi = P.pt_idx[ap];
-        const double* X = P.pts[cur] + 3 * pi;
+        const double* X = PRE ? &PL->pt[tid][PDATA + 3] : P.pts[cur] + 3 * pi;
         double* Xn = P.pts[cur ^ 1] + 3 * pi;
-        const double* pd = pdata + (size_t)ap * PDATA;
-        const double* sp = scale + P.off_pt + 3 * ap;
+        const double* pd = PRE ? &PL->pt[tid][0] : pdata + (size_t)ap * PDATA;
+        const double* sp = PRE ? &PL->pt[tid][PDATA] : scale + P.off_pt + 3 * ap;
         double yk[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) yk[m] = PUB ? tail_ld(y + P.kb + m) : y[P.kb + m];
@@ -246,7 +334,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         }
         const int cam = ro.idx();
         const int pl = ap - apb;
-        const double* X = P.pts[cur] + 3 * P.pt_idx[ap];
+        const double* X = PRE ? &PL->pt[pl][PDATA + 3] : P.pts[cur] + 3 * P.pt_idx[ap];
         const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
         ObsEval en;
         if constexpr (PUB) {
