@@ -805,21 +805,19 @@ int bcr_band_ok(int nac, int cam_band, int kb, bool one_block) {
 
 template <int BC>
 static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork& W, int nb, hipStream_t s, Prof* pf) {
-    static bool attr = false;
-    static int smode = -1;
-    static unsigned long long* dst = nullptr;
-    if (!attr) {
+    static DeviceOnce attr;
+    static DeviceScratch stamp_buf;
+    static const int smode = env_on("MIBA_BCR_STAMPS");
+    CKD(attr([] {
         CKD(hipFuncSetAttribute((const void*)k_bcr_band<BC, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024));
-        CKD(hipFuncSetAttribute((const void*)k_bcr_band<BC, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
-        const char* e = std::getenv("MIBA_BCR_STAMPS");
-        smode = (e && e[0] == '1') ? 1 : 0;
-        attr = true;
-    }
+        return hipFuncSetAttribute((const void*)k_bcr_band<BC, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+    }));
     const size_t lds = band_lds_bytes(BC, nb, P.nac);
     if (smode) {
-        if (!dst) CKD(hipMalloc(&dst, (BAND_STAMPS + BAND_FSTAMPS) * sizeof(unsigned long long)));
+        unsigned long long* dst = stamp_buf.get<unsigned long long>((BAND_STAMPS + BAND_FSTAMPS) * sizeof(unsigned long long));
+        if (!dst) return hipErrorOutOfMemory;
         CKD(hipMemsetAsync(dst, 0, (BAND_STAMPS + BAND_FSTAMPS) * sizeof(unsigned long long), s));
         if (pf) pf->begin(K_BCR_PERSIST, s);
         hipLaunchKernelGGL((k_bcr_band<BC, true>), dim3(1), dim3(BAND_TPB), lds, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
@@ -874,12 +872,11 @@ hipError_t tail_set_spin_limit(unsigned limit) {
 template <int BC, bool O32>
 static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int nb,
                                 int nb_pt, int nb_upd, hipStream_t s, Prof* pf) {
-    static bool attr = false;
-    if (!attr) {
-        CKD(hipFuncSetAttribute((const void*)k_band_tail<BC, O32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024 - 256));
-        attr = true;
-    }
+    static DeviceOnce attr;
+    CKD(attr([] {
+        return hipFuncSetAttribute((const void*)k_band_tail<BC, O32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024 - 256);
+    }));
     const size_t lds = std::max(band_lds_bytes(BC, nb, P.nac), std::max(sizeof(BsLds) + sizeof(BsPreLds), sizeof(FinLds)));
     const int nb_bs = P.n_bs_chunks;
     ++W.tail_seq;

@@ -29,6 +29,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "ba_device.h"
 #include "ba_kernels.h"
@@ -2503,8 +2504,8 @@ static hipError_t launch_per_level(const DevProblem& P, const BaConsts& c, DevWo
 }
 
 static hipError_t bcr_persist_attr() {
-    static bool done = false;
-    if (!done) {
+    static DeviceOnce once;
+    return once([]() -> hipError_t {
         CKB(hipFuncSetAttribute((const void*)k_bcr_persist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(PersistLds)));
         CKB(hipFuncSetAttribute((const void*)k_bcr_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2512,10 +2513,8 @@ static hipError_t bcr_persist_attr() {
         const void* fns[] = {(const void*)k_bcr_split<false, 1>, (const void*)k_bcr_split<true, 1>,
                              (const void*)k_bcr_split<false, 2>, (const void*)k_bcr_split<true, 2>};
         for (const void* f : fns) CKB(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(HLds)));
-
-        done = true;
-    }
-    return hipSuccess;
+        return hipSuccess;
+    });
 }
 
 // k_bcr_split's pull slots (published XL / XR / x rows, two epochs: UL | UR | F, rL | rR, F2) start empty;
@@ -2575,14 +2574,11 @@ int bcr_xmap_ok(int nblk, int persist) {
 hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWork& Bw, hipStream_t s, Prof* pf) {
     if (Bw.band) return launch_bcr_band(P, c, W, Bw.band, s, pf);  // narrow band: one workgroup (ba_band.hip)
     if (Bw.dense1) {  // one-block window: the dense single-workgroup solve (bcr_dense1_ok)
-        static unsigned long long* dst = nullptr;
-        static int dmode = -1;
-        if (dmode < 0) {
-            const char* e = getenv("MIBA_BCR_STAMPS");
-            dmode = (e && e[0] == '1') ? 1 : 0;
-            if (dmode) CKB(hipMalloc(&dst, 16 * sizeof(unsigned long long)));
-        }
+        static DeviceScratch stamp_buf;
+        static const int dmode = env_on("MIBA_BCR_STAMPS");
         if (dmode) {
+            unsigned long long* dst = stamp_buf.get<unsigned long long>(16 * sizeof(unsigned long long));
+            if (!dst) return hipErrorOutOfMemory;
             CKB(hipMemsetAsync(dst, 0, 16 * sizeof(unsigned long long), s));
             BPL(K_BCR_PERSIST, k_bcr_dense1<true>, dim3(1), dim3(TPB_D1), 0, s, W.st, P, W.S, W.rhs, W.chol_flag, c,
                 W.scale, W.camdata, W.lin, W.delta, W.part, dst);
@@ -2600,23 +2596,25 @@ hipError_t launch_bcr(const DevProblem& P, const BaConsts& c, DevWork& W, BcrWor
             W.scale, W.camdata, W.lin, W.delta, W.part, (unsigned long long*)nullptr);
         return hipSuccess;
     }
-    static bool attr = false;
-    static unsigned long long* stamps = nullptr;
-    if (!attr) {
+    static DeviceOnce attr;
+    static DeviceScratch stamp_buf;
+    static const int smode = env_on("MIBA_BCR_STAMPS");
+    CKB(attr([]() -> hipError_t {
         const int le = (int)sizeof(ElimLds), lb = (int)sizeof(BackLds);
         CKB(hipFuncSetAttribute((const void*)k_bcr_elim<false>, hipFuncAttributeMaxDynamicSharedMemorySize, le));
         CKB(hipFuncSetAttribute((const void*)k_bcr_elim<true>, hipFuncAttributeMaxDynamicSharedMemorySize, le));
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
         CKB(hipFuncSetAttribute((const void*)k_bcr_back<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
-        const char* e = getenv("MIBA_BCR_STAMPS");
-        if (e && e[0] == '1') CKB(hipMalloc(&stamps, sizeof(unsigned long long) * NSTAMP));
-        attr = true;
-    }
-    if (stamps) {
+        return hipSuccess;
+    }));
+    if (smode) {
+        unsigned long long* stamps = stamp_buf.get<unsigned long long>(sizeof(unsigned long long) * NSTAMP);
+        if (!stamps) return hipErrorOutOfMemory;
         CKB(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * NSTAMP, s));
         CKB(launch_bcr_t<true>(P, c, W, Bw, s, stamps, nullptr));
-        static unsigned long long h[NSTAMP];
-        CKB(hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s));
+        std::vector<unsigned long long> hv(NSTAMP);
+        unsigned long long* h = hv.data();
+        CKB(hipMemcpyAsync(h, stamps, sizeof(unsigned long long) * NSTAMP, hipMemcpyDeviceToHost, s));
         CKB(hipStreamSynchronize(s));
         if (Bw.persist >= 2) {
             const int nr = Bw.persist;  // workgroups per block

@@ -2,6 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+
 #include "ba_comm.h"
 #include "ba_device.h"
 
@@ -393,6 +397,57 @@ struct Prof {
 
 // All kernels read cur / radius / done from W.st (device), so an LM iteration is a
 // fixed launch sequence the host can enqueue without reading anything back.
+// ---------------------------------------------------------------- per-device launch setup (host)
+// hipFuncSetAttribute (the 160 KB dynamic LDS opt-in) applies to the CURRENT device only, and the API allows one
+// context per host thread on any device (include/ba.h): the one-time setup of a launch path runs once per device,
+// under a lock, and is retried if it failed. Diagnostic stamp buffers are kept per device the same way.
+struct DeviceOnce {
+    static constexpr int MAXDEV = 64;
+    std::atomic<unsigned long long> done{0};
+    std::mutex mu;
+    template <class F>
+    hipError_t operator()(F&& setup) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= MAXDEV) return hipErrorInvalidDevice;
+        const unsigned long long bit = 1ull << dev;
+        if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+        std::lock_guard<std::mutex> lock(mu);
+        if (done.load(std::memory_order_relaxed) & bit) return hipSuccess;
+        e = setup();
+        if (e == hipSuccess) done.fetch_or(bit, std::memory_order_release);
+        return e;
+    }
+};
+
+// A device buffer per device (stamp diagnostics), grown to `bytes` on first use; nullptr on failure.
+struct DeviceScratch {
+    std::mutex mu;
+    void* p[DeviceOnce::MAXDEV] = {};
+    size_t cap[DeviceOnce::MAXDEV] = {};
+    template <class T>
+    T* get(size_t bytes) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= DeviceOnce::MAXDEV) return nullptr;
+        std::lock_guard<std::mutex> lock(mu);
+        if (cap[dev] < bytes) {
+            if (p[dev]) (void)hipFree(p[dev]);
+            p[dev] = nullptr;
+            cap[dev] = 0;
+            if (hipMalloc(&p[dev], bytes) != hipSuccess) return nullptr;
+            cap[dev] = bytes;
+        }
+        return static_cast<T*>(p[dev]);
+    }
+};
+
+// "1" in a MIBA_* diagnostic switch (read once per process: thread-safe function-local statics at the call sites)
+inline int env_on(const char* name) {
+    const char* e = std::getenv(name);
+    return (e && e[0] == '1') ? 1 : 0;
+}
+
 hipError_t launch_linearize(const DevProblem& P, const BaConsts& c, int gated, DevWork& W, hipStream_t s, Prof* pf);
 hipError_t launch_scale(const DevProblem& P, const BaConsts& c, int jacobi, DevWork& W, hipStream_t s, Prof* pf);
 // progress: the host-mapped LM progress word (LmParams::progress), published with the done bit when the

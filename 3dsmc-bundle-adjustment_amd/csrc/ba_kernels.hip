@@ -2382,14 +2382,14 @@ static inline int nblocks(int n, int t) { return (n + t - 1) / t; }
     } while (0)
 
 int pp_lanes() {
-    static int lanes = 0;
-    if (!lanes) {
-        lanes = 1;  // measured at C4: 1 lane per point beats 2 and 4 (the per-point tail dominates)
+    static const int lanes = [] {
+        int l = 1;  // measured at C4: 1 lane per point beats 2 and 4 (the per-point tail dominates)
         if (const char* e = getenv("MIBA_PP_LANES")) {
             const int v = atoi(e);
-            if (v == 1 || v == 2 || v == 4) lanes = v;
+            if (v == 1 || v == 2 || v == 4) l = v;
         }
-    }
+        return l;
+    }();
     return lanes;
 }
 
@@ -2589,14 +2589,11 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
                     W.pdata, W.part, W.camdata_part, W.seg_intr, W.sw_cnt, (++W.sw_seq) * (unsigned)P.n_seg, P.n_seg,
                     pp_blocks(P.n_ap - P.n_tiled_pts, 1)};
         const int n_sch = P.n_tiles + 1 + E.n_cs + E.n_gb + E.n_env;
-        static int fp_stamps = -1;
-        static unsigned long long* fst = nullptr;
-        if (fp_stamps < 0) {
-            const char* e = getenv("MIBA_SCHUR_STAMPS");
-            fp_stamps = (e && e[0] == '1') ? 1 : 0;
-        }
+        static const int fp_stamps = env_on("MIBA_SCHUR_STAMPS");
+        static DeviceScratch fst_buf;
         if (fp_stamps == 1 && P.obs32) {  // diagnostic: per-tile phase cycles (zero, A incl. the point side, B, flush)
-            if (!fst) CK(hipMalloc(&fst, sizeof(unsigned long long) * 10 * 256));
+            unsigned long long* fst = fst_buf.get<unsigned long long>(sizeof(unsigned long long) * 10 * 256);
+            if (!fst) return hipErrorOutOfMemory;
             PL(K_SCHUR_TILE, (k_schur_tile<true, true, true, true, true>), dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale,
                W.pdata, W.S, W.rhs, fst, 0, W.part, (double*)nullptr, E);
             std::vector<unsigned long long> h5((size_t)5 * P.n_tiles);
@@ -2647,19 +2644,11 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
     const int n_sch = P.n_tiles + ((P.n_ap > 0 || W.fused) ? 1 : 0) + E.n_env;
     if (n_sch > 0)
     {
-        static int smode = -1;
-        static unsigned long long* sst = nullptr;
-        static int scap = 0;
-        if (smode < 0) {
-            const char* e = getenv("MIBA_SCHUR_STAMPS");
-            smode = (e && e[0] == '1') ? 1 : 0;
-        }
+        static const int smode = env_on("MIBA_SCHUR_STAMPS");
+        static DeviceScratch sst_buf;
         if (smode == 1) {
-            if (scap < P.n_tiles) {
-                if (sst) CK(hipFree(sst));
-                CK(hipMalloc(&sst, sizeof(unsigned long long) * 5 * P.n_tiles));
-                scap = P.n_tiles;
-            }
+            unsigned long long* sst = sst_buf.get<unsigned long long>(sizeof(unsigned long long) * 5 * std::max(P.n_tiles, 1));
+            if (!sst) return hipErrorOutOfMemory;
             if (W.fpl)  // (the opt-in fused point side, stamped)
                 OPL(K_SCHUR_TILE, (k_schur_tile<true, true, false, true>), (k_schur_tile<true, false, false, true>),
                     dim3(n_sch), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.S, W.rhs, sst,
@@ -2748,18 +2737,17 @@ hipError_t launch_build(const DevProblem& P, const BaConsts& c, DevWork& W, hipS
 template <int BW>
 static hipError_t launch_band(const DevProblem& P, DevWork& W, hipStream_t s, Prof* pf) {
     const size_t lds = sizeof(BandLds<BW>) + sizeof(int) * BAND_MAX_NB;
-    static bool attr_set = false;
-    static int stamp_mode = -1;
-    if (!attr_set) {
+    static DeviceOnce attr;
+    static DeviceScratch stamp_buf;
+    static const int stamp_mode = env_on("MIBA_CHOL_STAMPS");
+    CK(attr([]() -> hipError_t {
         CK(hipFuncSetAttribute((const void*)k_chol_band<BW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         CK(hipFuncSetAttribute((const void*)k_chol_band<BW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = true;
-        const char* e = getenv("MIBA_CHOL_STAMPS");
-        stamp_mode = (e && e[0] == '1') ? 1 : 0;
-    }
+        return hipSuccess;
+    }));
     if (stamp_mode == 1) {
-        static unsigned long long* dst = nullptr;
-        if (!dst) CK(hipMalloc(&dst, 8 * sizeof(unsigned long long)));
+        unsigned long long* dst = stamp_buf.get<unsigned long long>(8 * sizeof(unsigned long long));
+        if (!dst) return hipErrorOutOfMemory;
         PL(K_CHOL, (k_chol_band<BW, true>), dim3(1), dim3(TPB), lds, s, W.st, W.S, P.npad, P.npad / 16, W.fcol, W.rhs,
            W.chol_flag, dst);
         unsigned long long h[8];
@@ -2796,11 +2784,10 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
     // BCR: k_bcr_border already applied the camera / intrinsics step (one partial per BCR block)
     const bool fused_upd = P.solver == 2;
     const int nb_upd = fused_upd ? (P.nac + BCR_CAMS - 1) / BCR_CAMS : nblocks(P.nac + 1, TPB);
-    static int ndummy = -1;
-    if (ndummy < 0) {
-        const char* e = getenv("MIBA_DUMMY_LAUNCHES");  // diagnostic: extra empty launches per iteration
-        ndummy = e ? atoi(e) : 0;
-    }
+    static const int ndummy = [] {  // diagnostic: extra empty launches per iteration
+        const char* e = getenv("MIBA_DUMMY_LAUNCHES");
+        return e ? atoi(e) : 0;
+    }();
     for (int k = 0; k < ndummy; ++k) PL(K_DUMMY, k_dummy, dim3(1), dim3(64), 0, s, W.st);
     if (W.tail) {  // band solve + back-substitution + decision in one launch (ba_band.hip k_band_tail)
         const int nb_pt = W.sw ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts, 1) : pp_parts(P);

@@ -280,6 +280,9 @@ void ba_destroy(ba_context* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    // a prepare that returned early (e.g. BA_E_INVALID) may have left value copies queued on the copy stream:
+    // they read the staging buffer and write device buffers released below
+    if (ctx->copy_stream) hipStreamSynchronize(ctx->copy_stream);
     comm_destroy(ctx->W.comm);
     comm_destroy(ctx->comm_parked);
     for (auto& b : ctx->buf) b.release();
@@ -1094,7 +1097,10 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         }
         const size_t raw_off = (raw_bytes + 255) / 256 * 256;  // after the raw region, which may still be in flight
         if (ctx->stage_cap < raw_off + 4 * plan_ints) {
-            HIPCHECK(ctx, hipStreamSynchronize(s));  // growing frees the buffer the raw DMA reads
+            // growing frees the buffer the raw DMAs read: the index DMA on `stream`, the device plan's pixel /
+            // depth DMA on the copy stream
+            HIPCHECK(ctx, hipStreamSynchronize(s));
+            if (ctx->uv_pending) HIPCHECK(ctx, hipEventSynchronize(ctx->ev_uv));
             if (int rc = stage_ensure(ctx, raw_off + 4 * plan_ints, raw_bytes)) return rc;
         }
         int* sp = reinterpret_cast<int*>(ctx->stage + raw_off);
@@ -1517,7 +1523,7 @@ static int apply_spin_limit(ba_context* ctx) {
 // or process held CUs). The decision stopped the device loop without a termination and without counting the
 // iteration (x, radius and the trust-region state untouched): from now on this context runs the per-level
 // launches (no inter-workgroup waits), and the host re-enqueues the iteration. The in-flight iterations behind
-// the decision were no-ops. S / rhs were cleared for the next assembly by that iteration's own kernels.
+// the decision were no-ops. S / rhs are cleared here for the re-run's assembly.
 static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     hipStream_t s = ctx->stream;
     HIPCHECK(ctx, hipStreamSynchronize(s));
@@ -1529,6 +1535,14 @@ static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     ctx->bcr_fallback = true;
     if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
     HIPCHECK(ctx, bcr_reset_pull_slots(Bw, false, s));
+    // S and rhs as after a prepare: a band-tail chunk whose own wait also timed out may have zeroed S / rhs while
+    // the solve workgroup had not yet run, and the solve may then have written y into rhs behind the zeroing
+    // (ADVICE r5); the re-run's assembly must start from zeros
+    {
+        const DevProblem& P = ctx->P;
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RHS].p, 0, sizeof(double) * P.npad, s));
+    }
     S.done = 0;
     S.termination = -1;
     S.msg = MSG_NONE;
@@ -1554,35 +1568,67 @@ extern "C" int32_t ba_prepare(ba_context* ctx, const ba_problem* p) {
     return BA_OK;
 }
 
+// Sized out-structs (BA_API_VERSION 2): the caller's struct_size says how many bytes its struct has; write no more
+// than that, keep its struct_size, and refuse a size below the version's minimum.
+template <class T>
+static bool sized_out_ok(const T* out, int32_t min_size) {
+    return out && out->struct_size >= min_size;
+}
+template <class T>
+static void sized_copy_out(T* out, const T& full) {
+    const size_t n = std::min<size_t>((size_t)out->struct_size, sizeof(T));
+    const int32_t keep = out->struct_size;
+    std::memcpy(out, &full, n);
+    out->struct_size = keep;
+}
+
 extern "C" int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info) {
     if (!ctx || !info) return BA_E_INVALID;
-    *info = ctx->pinfo;
+    if (!sized_out_ok(info, BA_PREPARE_INFO_MIN_SIZE)) {
+        g_err = "ba_last_prepare: info->struct_size below BA_PREPARE_INFO_MIN_SIZE (set it with BA_PREPARE_INFO_INIT)";
+        return BA_E_INVALID;
+    }
+    sized_copy_out(info, ctx->pinfo);
     return BA_OK;
 }
 
 static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, double t0);
 
+// the LM loop into a full-size summary, copied out at the caller's size
+static int32_t solve_prepared_out(ba_context* ctx, ba_problem* p, ba_summary* out, double t0) {
+    ba_summary full{};
+    const int32_t rc = solve_prepared(ctx, p, &full, t0);
+    full.struct_size = (int32_t)sizeof(ba_summary);
+    sized_copy_out(out, full);
+    return rc;
+}
+
+static const char* const kSummarySizeErr =
+    "ba_summary.struct_size below BA_SUMMARY_MIN_SIZE (set it with BA_SUMMARY_INIT)";
+
 extern "C" int32_t ba_solve(ba_context* ctx, ba_problem* p, ba_summary* sum) {
     if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
     if (!sum) { ctx->err = "null summary"; return BA_E_INVALID; }
+    if (!sized_out_ok(sum, BA_SUMMARY_MIN_SIZE)) { ctx->err = kSummarySizeErr; return BA_E_INVALID; }
     miba_maybe_dump_window(p, &ctx->opts);
     const double t0 = now_ms();
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     if (int rc = apply_spin_limit(ctx)) return rc;
     int rc = prepare(ctx, p);
     if (rc) return rc;
-    return solve_prepared(ctx, p, sum, t0);
+    return solve_prepared_out(ctx, p, sum, t0);
 }
 
 extern "C" int32_t ba_solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum) {
     if (!ctx) { g_err = "null context"; return BA_E_INVALID; }
     if (!sum || !p) { ctx->err = "null argument"; return BA_E_INVALID; }
+    if (!sized_out_ok(sum, BA_SUMMARY_MIN_SIZE)) { ctx->err = kSummarySizeErr; return BA_E_INVALID; }
     if (!ctx->prepared || p->n_cams != ctx->prep_nc || p->n_points != ctx->prep_np || p->n_obs != ctx->prep_no) {
         ctx->err = "ba_solve_prepared: problem does not match the last ba_prepare()";
         return BA_E_INVALID;
     }
     HIPCHECK(ctx, hipSetDevice(ctx->device));
-    return solve_prepared(ctx, p, sum, now_ms());
+    return solve_prepared_out(ctx, p, sum, now_ms());
 }
 
 static int32_t solve_prepared(ba_context* ctx, ba_problem* p, ba_summary* sum, double t0) {

@@ -81,9 +81,12 @@ class BaProblem(C.Structure):
 
 
 class BaSummary(C.Structure):
-    """Mirror of ``ba_summary`` (subset of ceres::Solver::Summary)."""
+    """Mirror of ``ba_summary`` (subset of ceres::Solver::Summary). BA_API_VERSION 2: ``struct_size`` is set to
+    this mirror's size on construction (the library writes no more than that)."""
 
     _fields_ = [
+        ("struct_size", C.c_int32),
+        ("reserved0", C.c_int32),
         ("initial_cost", C.c_double),
         ("final_cost", C.c_double),
         ("num_successful_steps", C.c_int32),
@@ -106,8 +109,14 @@ class BaSummary(C.Structure):
         ("message", C.c_char * 160),
     ]
 
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if not self.struct_size:
+            self.struct_size = C.sizeof(type(self))
+
     def as_dict(self) -> dict:
-        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "message"}
+        d = {name: getattr(self, name) for name, _ in self._fields_
+             if name not in ("message", "struct_size", "reserved0")}
         d["message"] = self.message.decode(errors="replace")
         d["termination"] = TERMINATION_NAMES.get(self.termination_type, str(self.termination_type))
         return d
@@ -127,9 +136,11 @@ class BaKernelStat(C.Structure):
 
 
 class BaPrepareInfo(C.Structure):
-    """Mirror of ``ba_prepare_info`` (what the last prepare did; ba_last_prepare)."""
+    """Mirror of ``ba_prepare_info`` (what the last prepare did; ba_last_prepare). ``struct_size`` is set to this
+    mirror's size on construction."""
 
     _fields_ = [
+        ("struct_size", C.c_int32),
         ("plan_reused", C.c_int32),
         ("obs_uploaded", C.c_int32),
         ("host_threads", C.c_int32),
@@ -143,8 +154,13 @@ class BaPrepareInfo(C.Structure):
         ("tail", C.c_int32),
     ]
 
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if not self.struct_size:
+            self.struct_size = C.sizeof(type(self))
+
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "struct_size"}
 
 
 def default_options_py() -> BaOptions:

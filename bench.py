@@ -305,7 +305,8 @@ def rank_plan(gpus, latency, env, n_visible, argv, port):
     if latency:
         return "error", "--config C1 / C3 is the single-GPU latency bench (TUM-size windows are never sharded)"
     if n_visible < n:
-        return "error", f"--gpus {n} but only {n_visible} HIP device(s) visible: refusing to report a {n}-GPU number"
+        return "error", (f"--gpus {n} but only {n_visible} HIP device(s) visible (KFD topology, *_VISIBLE_DEVICES): "
+                         f"refusing to report a {n}-GPU number")
     procs = []
     for r in range(n):
         e = dict(env)
@@ -316,9 +317,97 @@ def rank_plan(gpus, latency, env, n_visible, argv, port):
     return "spawn", procs
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _visible_list(value: str, n: int) -> int:
+    """How many of n devices a *_VISIBLE_DEVICES list keeps: distinct in-range ordinals, or UUID-style entries."""
+    keep = set()
+    for item in (x.strip() for x in value.split(",")):
+        if not item:
+            continue
+        if item.isdigit():
+            if int(item) >= n:
+                break  # the runtimes stop at the first invalid ordinal
+            keep.add(int(item))
+        else:
+            keep.add(item)
+    return min(len(keep), n)
+
+
+def visible_gpus(env=None, topology: str | None = None, dri: str | None = None) -> int:
+    """HIP devices this process would see, counted WITHOUT touching HIP (no torch import, no libamdhip64, /dev/kfd
+    never opened): KFD topology nodes with a non-zero gpu_id whose render node exists in /dev/dri (a container sees
+    every node of the host in sysfs but only its own GPUs' render nodes), then ROCR_VISIBLE_DEVICES and
+    HIP_VISIBLE_DEVICES (else CUDA_VISIBLE_DEVICES), in that order. On ROCm torch, torch.cuda.device_count() falls
+    back to hipGetDeviceCount, which initialises HIP, whenever amdsmi cannot initialise; the
+    parent of the rank processes must not hold the GPU when it starts them. MIBA_KFD_TOPOLOGY / MIBA_DRI_DIR point
+    the count at another tree (tests)."""
+    env = os.environ if env is None else env
+    topology = topology or env.get("MIBA_KFD_TOPOLOGY", KFD_TOPOLOGY)
+    dri = dri or env.get("MIBA_DRI_DIR", "/dev/dri")
+    n = 0
+    for node in sorted(glob.glob(os.path.join(topology, "*"))):
+        try:
+            gpu_id = int(open(os.path.join(node, "gpu_id")).read().strip() or 0)
+        except (OSError, ValueError):
+            continue
+        if gpu_id == 0:
+            continue  # a CPU node
+        minor = None
+        try:
+            for line in open(os.path.join(node, "properties")):
+                k, _, v = line.partition(" ")
+                if k == "drm_render_minor":
+                    minor = int(v)
+        except (OSError, ValueError):
+            pass
+        if minor is not None and minor > 0 and os.path.isdir(dri) and \
+                not os.path.exists(os.path.join(dri, f"renderD{minor}")):
+            continue  # on the host, not in this container
+        n += 1
+    if env.get("ROCR_VISIBLE_DEVICES") is not None:
+        n = _visible_list(env["ROCR_VISIBLE_DEVICES"], n)
+    hip = env.get("HIP_VISIBLE_DEVICES", env.get("CUDA_VISIBLE_DEVICES"))
+    if hip is not None:
+        n = _visible_list(hip, n)
+    return n
+
+
+def parent_gpu_state(pid: str = "self") -> list:
+    """What of the GPU stack this process holds: /dev/kfd open, the HIP runtime mapped. Empty = nothing."""
+    held = []
+    try:
+        for fd in os.listdir(f"/proc/{pid}/fd"):
+            try:
+                if os.readlink(f"/proc/{pid}/fd/{fd}") == "/dev/kfd":
+                    held.append("/dev/kfd open")
+                    break
+            except OSError:
+                pass
+    except OSError:
+        pass
+    try:
+        with open(f"/proc/{pid}/maps") as f:
+            if any("libamdhip64" in line for line in f):
+                held.append("libamdhip64 mapped")
+    except OSError:
+        pass
+    return held
+
+
 def spawn_ranks(procs) -> int:
-    """Run the rank processes (rank 0's stdout is the bench line); a failed rank ends the others."""
+    """Run the rank processes (rank 0's stdout is the bench line); a failed rank ends the others. The parent must
+    not hold the GPU (an initialised HIP runtime in a parent of GPU processes is not safe on this pool)."""
     import subprocess
+    held = parent_gpu_state()
+    if held:
+        print(f"bench.py: the launching process holds the GPU ({', '.join(held)}): refusing to start ranks",
+              file=sys.stderr)
+        return 2
+    if os.environ.get("MIBA_BENCH_VERBOSE") == "1":
+        print(f"bench.py: parent {os.getpid()}: /dev/kfd not open, libamdhip64 not mapped; starting {len(procs)} ranks",
+              file=sys.stderr, flush=True)
     ps = [subprocess.Popen(cmd, env=env, stdout=None if r == 0 else subprocess.DEVNULL)
           for r, (cmd, env) in enumerate(procs)]
     rc = 0
@@ -354,8 +443,8 @@ def main():
     args = parse()
     latency = args.config in ("C1", "C3") and not args.problem
     if os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
-        import torch  # device_count() does not initialise the GPU on this image; nothing else is touched here
-        kind, what = rank_plan(args.gpus, latency, os.environ, torch.cuda.device_count(), sys.argv[1:], free_port())
+        # counted from sysfs: the parent never imports torch or loads the HIP runtime
+        kind, what = rank_plan(args.gpus, latency, os.environ, visible_gpus(), sys.argv[1:], free_port())
     else:
         kind, what = rank_plan(args.gpus, latency, os.environ, 0, sys.argv[1:], 0)
     if kind == "error":

@@ -32,13 +32,22 @@
 #ifndef MIBA_BA_H
 #define MIBA_BA_H
 
+#include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define BA_API_VERSION 1
+/* Version history:
+ *   1  (rounds 1-5) ba_summary / ba_prepare_info without a size field; ba_prepare_info grew lin_path (r4),
+ *      plan_device and tail (r5) under the same version.
+ *   2  ba_summary and ba_prepare_info lead with `struct_size`: the caller sets it to sizeof() of ITS struct
+ *      (BA_SUMMARY_INIT / BA_PREPARE_INFO_INIT), the library writes only that many bytes (fields a newer
+ *      library added past the caller's size stay untouched) and rejects a size below the *_MIN_SIZE of this
+ *      version with BA_E_INVALID. */
+#define BA_API_VERSION 2
 
 /* error codes */
 #define BA_OK 0
@@ -127,6 +136,8 @@ typedef struct ba_problem {
 #define BA_LS_BCR 2   /* block cyclic reduction over 64-dof camera blocks */
 
 typedef struct ba_summary {
+    int32_t struct_size;            /* in: sizeof(ba_summary) of the caller's header (BA_SUMMARY_INIT) */
+    int32_t reserved0;
     double initial_cost;
     double final_cost;
     int32_t num_successful_steps;   /* Ceres convention: includes iteration 0 */
@@ -148,6 +159,9 @@ typedef struct ba_summary {
     double time_total_ms;
     char message[160];
 } ba_summary;
+/* the smallest struct_size ba_solve / ba_solve_prepared accept: every field before `message` */
+#define BA_SUMMARY_MIN_SIZE ((int32_t)offsetof(ba_summary, message))
+#define BA_SUMMARY_INIT(s) (memset(&(s), 0, sizeof(s)), (s).struct_size = (int32_t)sizeof(s))
 
 /* Library / API identification. */
 int32_t ba_api_version(void);
@@ -168,7 +182,8 @@ const char* ba_last_error(const ba_context* ctx);
 int32_t ba_set_options(ba_context* ctx, const ba_options* opts);
 
 /* Solve one window in place (the replacement of ceres::Solve at :300).
- * Equivalent to ba_prepare() followed by ba_solve_prepared(). */
+ * Equivalent to ba_prepare() followed by ba_solve_prepared(). summary->struct_size must be set
+ * (BA_SUMMARY_INIT); min(struct_size, sizeof(ba_summary)) bytes are written. */
 int32_t ba_solve(ba_context* ctx, ba_problem* prob, ba_summary* summary);
 
 /* Split form of ba_solve for callers that re-solve a resident window:
@@ -182,6 +197,7 @@ int32_t ba_solve_prepared(ba_context* ctx, ba_problem* prob, ba_summary* summary
 
 /* What the last ba_prepare (or the prepare inside ba_solve / the debug hooks) did. */
 typedef struct ba_prepare_info {
+    int32_t struct_size;     /* in: sizeof(ba_prepare_info) of the caller's header (BA_PREPARE_INFO_INIT) */
     int32_t plan_reused;     /* 1: the window's structure matched the context's last plan (no plan rebuild) */
     int32_t obs_uploaded;    /* 1: observation values were uploaded (always on a rebuild; on a reuse only when
                                 some pixel / depth value changed) */
@@ -202,6 +218,10 @@ typedef struct ba_prepare_info {
     int32_t tail;            /* 1: the band solve's launch also runs the point back-substitution and the LM
                                 decision (bcr_path 5, small unsharded windows; MIBA_TAIL=0: separate launches) */
 } ba_prepare_info;
+/* the smallest struct_size ba_last_prepare accepts: the fields through total_ms (the round-3 layout) */
+#define BA_PREPARE_INFO_MIN_SIZE ((int32_t)(offsetof(ba_prepare_info, total_ms) + sizeof(double)))
+#define BA_PREPARE_INFO_INIT(s) (memset(&(s), 0, sizeof(s)), (s).struct_size = (int32_t)sizeof(s))
+/* Writes min(info->struct_size, sizeof(ba_prepare_info)) bytes; BA_E_INVALID below BA_PREPARE_INFO_MIN_SIZE. */
 int32_t ba_last_prepare(const ba_context* ctx, ba_prepare_info* info);
 
 /* Landmark sharding (one process per GPU). Every rank passes the SAME window

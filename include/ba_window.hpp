@@ -162,7 +162,8 @@ bool windowOptimize(int kf_i, int kf_f, KeyFrames& keyframes, Map3D& map, const 
         }
     }
     ba_problem prob = w.view();
-    ba_summary summary{};
+    ba_summary summary;
+    BA_SUMMARY_INIT(summary);
     // :300 — solved even when no observation is admissible: the IntrinsicsPrior block (:236-241) is always
     // added, so Ceres still pulls intrinsics_optimized toward intrinsics_initial (poses have no residual)
     const int32_t rc = solve(&prob, &summary);

@@ -872,6 +872,7 @@ static void trace_row(trace_t* tr, int it, double cost, double dc, double g, dou
 static int solve_impl(ba_problem* p, const ba_options* opt, ba_summary* sum, trace_t* tr) {
     const double t0 = now_ms();
     memset(sum, 0, sizeof(*sum));
+    sum->struct_size = (int32_t)sizeof(*sum);
     orc_t c;
     if (orc_init(&c, p, opt)) { orc_free(&c); return BA_E_INVALID; }
     sum->num_obs_admissible = c.n_adm;

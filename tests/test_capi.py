@@ -50,7 +50,7 @@ def test_defaults_equal_oracle_defaults(L):
 
 
 def test_api_version(L):
-    assert L.ba_api_version() == 1
+    assert L.ba_api_version() == 2  # ba.h version history: 2 = sized ba_summary / ba_prepare_info
     assert b"gfx950" in L.ba_build_info()
 
 

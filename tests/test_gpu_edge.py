@@ -191,6 +191,32 @@ def test_two_contexts_solve_concurrently_on_one_gpu():
         assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
 
 
+def test_first_solves_from_two_threads_in_a_fresh_process():
+    """the one-time launch setup (the 160 KB dynamic-LDS attribute of the band solve, its tail
+    launch, the split BCR and the per-level kernels) is per device and thread-safe. A fresh process — nothing set
+    up yet — starts four threads whose FIRST solves begin together (band + tail on C3 twice, the split BCR on C2,
+    the one-block band on C1); every solve returns BA_OK and matches the oracle."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "first_solve_worker.py"), "C3,C2,C1,C3"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert not res["hung"], res
+    paths = []
+    for cfg, o in zip(res["configs"], res["out"]):
+        assert o is not None and "error" not in o, (cfg, o)
+        sg, so = o["gpu"], o["oracle"]
+        paths.append(o["bcr_path"])
+        assert sg["termination"] == so["termination"], (cfg, sg, so)
+        assert sg["num_iterations"] == so["num_iterations"], cfg
+        assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (cfg, sg, so)
+    assert paths[0] == 5 and paths[1] >= 2, paths  # the band solve and the split BCR were both raced
+
+
 def test_cooperative_bcr_launch_matches_oracle(monkeypatch):
     """MIBA_BCR_COOP=1: k_bcr_split as a cooperative launch (the runtime refuses a grid that cannot be co-resident;
     off by default, it costs ~20 us per launch on MI355X). Same arithmetic: the solve matches the oracle."""
