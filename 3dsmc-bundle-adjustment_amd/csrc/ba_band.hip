@@ -775,6 +775,68 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
                         *reinterpret_cast<FinLds*>(lds));
 }
 
+// ---- the back-substitution and the decision in one launch (C4-size windows: DevWork::bsfin) ----------------------
+// k_backsub_chunk's chunks as workgroups 0..nb_bs-1 and k_final's reduction + LM decision as workgroup nb_bs, which is
+// dispatched last and waits until tail_flags[1] counts every chunk of this launch (the chunks wait on nothing, so the
+// wait always ends). The chunks read y and the candidates from the previous launch with plain loads and store only
+// their partials past the L2, drained before the count (backsub_body<O32, false, true>); the decision workgroup
+// reads them with agent-scope loads (final_body<2, true>). One launch less per LM iteration, and the reduction starts
+// the moment the last chunk has counted. A wait past the spin bound raises FLAG_TIMEOUT (the iteration is re-run
+// with the separate launches) after waiting for the chunks, as the band tail does.
+template <bool O32>
+__global__ __launch_bounds__(TPB) void k_backsub_final(DevProblem P, BaConsts c, LmState* __restrict__ st,
+                                                       const double* __restrict__ scale,
+                                                       const double* __restrict__ pdata, double* __restrict__ rhs,
+                                                       double* __restrict__ part, const int2* __restrict__ ztiles,
+                                                       int n_ztiles, double* __restrict__ S, int nb_bs, int nb_pt,
+                                                       int nb_upd, int* __restrict__ flag, double* __restrict__ scal,
+                                                       LmParams prm, const double* __restrict__ lin,
+                                                       double* __restrict__ log, unsigned* __restrict__ bcr_epoch,
+                                                       unsigned* __restrict__ tflags, unsigned seq) {
+    __shared__ union {
+        BsLds bs;
+        FinLds fin;
+    } L;
+    __shared__ int ok_s;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    // (the decision role tested first, on b == nb_bs: written the other way round the compiler gave the kernel 134
+    // VGPRs instead of the chunks' 126, 3 waves per SIMD instead of 4)
+    if (b == nb_bs) {
+        constexpr unsigned BOUND = 1u << 26;
+        if (tid == 0) {
+            const bool skip = skip_step(st);
+            ok_s = (skip || tail_wait(tflags + 1, seq * (unsigned)nb_bs, g_tail_spin_limit)) ? 1 : 0;
+            if (!ok_s) {
+                raise_flag(flag, FLAG_TIMEOUT);
+                (void)tail_wait(tflags + 1, seq * (unsigned)nb_bs, BOUND);  // every chunk done before rhs is zeroed
+            }
+        }
+        __syncthreads();
+        final_body<2, true>(P, st, nb_pt, nb_upd, nb_bs, part, flag, scal, prm, lin, log, rhs, bcr_epoch, L.fin);
+        return;
+    }
+    backsub_body<O32, false, true>(P, c, st, scale, pdata, rhs, nullptr, part, ztiles, n_ztiles, S, b, nb_bs, L.bs);
+    // thread 0 stored and drained this chunk's partials (or the chunk skipped: nothing to publish)
+    if (tid == 0) __hip_atomic_fetch_add(tflags + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_backsub_final(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int nb_pt,
+                                int nb_upd, unsigned* bcr_epoch, hipStream_t s, Prof* pf) {
+    const int nb_bs = P.n_bs_chunks;
+    ++W.tail_seq;
+    if (pf) pf->begin(K_BACKSUB_EVAL, s);
+    if (P.obs32)
+        hipLaunchKernelGGL(k_backsub_final<true>, dim3(nb_bs + 1), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs,
+                           W.part, W.env_tile, W.n_env, W.S, nb_bs, nb_pt, nb_upd, W.chol_flag, W.scal, prm, W.lin, W.log,
+                           bcr_epoch, W.tail_flags, W.tail_seq);
+    else
+        hipLaunchKernelGGL(k_backsub_final<false>, dim3(nb_bs + 1), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs,
+                           W.part, W.env_tile, W.n_env, W.S, nb_bs, nb_pt, nb_upd, W.chol_flag, W.scal, prm, W.lin, W.log,
+                           bcr_epoch, W.tail_flags, W.tail_seq);
+    if (pf) pf->end(s);
+    return hipGetLastError();
+}
+
 static size_t band_lds_bytes(int bc, int nb, int nac) { return sizeof(double) * (size_t)band_layout(6 * bc, nb, nac).total; }
 
 // The band path for this window: cameras per block (1..3), 0 when it does not apply. mode: MIBA_BCR_BAND

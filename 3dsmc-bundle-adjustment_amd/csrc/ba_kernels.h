@@ -361,6 +361,9 @@ struct DevWork {
     // tail_flags[0] (the solve's launch number) and [1] (back-substitution chunks done, monotonic within a solve;
     // both reset by launch_reset); tail_seq: tail launches of this solve (host side)
     int tail = 0;
+    // larger unsharded fused windows: the back-substitution chunks and the final reduction + decision in one launch
+    // (k_backsub_final), counted on tail_flags[1] / tail_seq like the band tail (never both)
+    int bsfin = 0;
     unsigned* tail_flags = nullptr;
     unsigned tail_seq = 0;
 };
@@ -491,6 +494,9 @@ hipError_t launch_band_tail(const DevProblem& P, const BaConsts& c, const LmPara
                             int nb_upd, hipStream_t s, Prof* pf);
 // workgroups of the tail launch (0: the window does not fit one resident round)
 int band_tail_blocks(const DevProblem& P, int bc);
+// the back-substitution chunks + the final reduction and decision in one launch (W.bsfin, unsharded fused windows)
+hipError_t launch_backsub_final(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int nb_pt,
+                                int nb_upd, unsigned* bcr_epoch, hipStream_t s, Prof* pf);
 hipError_t tail_set_spin_limit(unsigned limit);
 // k_bcr_split's pull slots: empty (split = true, Bw.persist >= 2) or zero (the per-level / persistent paths)
 hipError_t bcr_reset_pull_slots(const BcrWork& Bw, bool split, hipStream_t s);

@@ -2799,14 +2799,16 @@ hipError_t launch_update(const DevProblem& P, const BaConsts& c, const LmParams&
     const int nb_bs = P.n_bs_chunks;
     if (W.fused && P.n_ap == 0)  // an empty landmark shard: no back-substitution chunk zeroes S for the next assembly
         PL(K_MEMSET_S, k_env_zero, dim3(W.n_env), dim3(TPB), 0, s, W.st, W.env_tile, P.npad, W.S);
-    if (P.n_ap > 0)
-        OPL(K_BACKSUB_EVAL, k_backsub_chunk<true>, k_backsub_chunk<false>, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
-           W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     // the points' gradient max / bad partials: per point workgroup, or per Schur tile + non-tiled point workgroup
     const int nb_pt = W.sw ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts, 1)
                            : (W.fpl ? P.n_tiles + pp_blocks(P.n_ap - P.n_tiled_pts) : pp_parts(P));
     // the split BCR kernel's call epoch (the persistent kernel's is advanced by k_bcr_border)
     unsigned* const ep = (P.solver == 2 && W.bcr.persist >= 2) ? W.bcr.flags : nullptr;
+    if (W.bsfin && P.n_ap > 0 && W.fused && !W.comm.on())  // back-substitution + decision in one launch (ba_band.hip)
+        return launch_backsub_final(P, c, prm, W, nb_pt, nb_upd, ep, s, pf);
+    if (P.n_ap > 0)
+        OPL(K_BACKSUB_EVAL, k_backsub_chunk<true>, k_backsub_chunk<false>, dim3(nb_bs), dim3(TPB), 0, s, P, c, W.st, W.scale, W.pdata, W.rhs, W.delta,
+           W.part, W.env_tile, W.fused ? W.n_env : 0, W.S);
     if (!W.comm.on()) {
         PL(K_FINAL, k_final<2>, dim3(1), dim3(TPB_F), 0, s, P, W.st, nb_pt, nb_upd, P.n_ap > 0 ? nb_bs : 0, W.part,
            W.chol_flag, W.scal, prm, W.lin, W.log, W.fused ? W.rhs : (double*)nullptr, ep);

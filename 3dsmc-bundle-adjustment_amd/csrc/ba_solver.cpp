@@ -120,6 +120,7 @@ struct ba_context {
     int n_adm_all = 0;  // admissible observations over all landmark shards
     int sw_full = 0;    // DevWork::sw as the last full prepare chose it (a timeout re-run clears W.sw)
     int tail_full = 0;  // DevWork::tail likewise
+    int bsfin_full = 0;  // DevWork::bsfin likewise
     bool tail_possible = false;  // the window's LM loop can take the band tail launch (set before bcr_setup)
     int prep_nc = -1, prep_np = -1, prep_no = -1;
     int last_iter = -1;        // iterations of the last solve (ba_iteration_log rows - 1)
@@ -743,6 +744,7 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     // the full prepare chose again (no sticky fallback)
     ctx->W.sw = ctx->sw_full;
     ctx->W.tail = ctx->tail_full;
+    ctx->W.bsfin = ctx->bsfin_full;
     set_consts(ctx);
     ctx->pinfo.plan_reused = 1;
     ctx->pinfo.obs_uploaded = any_vals ? 1 : 0;
@@ -750,6 +752,7 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     ctx->pinfo.bcr_path = P.solver == 2 ? bcr_path_id(ctx->W.bcr) : -1;
     ctx->pinfo.lin_path = ctx->W.sw;
     ctx->pinfo.tail = ctx->W.tail;
+    ctx->pinfo.bsfin = ctx->W.bsfin;
     ctx->prepared = true;
     ctx->prep_nc = p->n_cams; ctx->prep_np = p->n_points; ctx->prep_no = p->n_obs;
     return 1;
@@ -1328,6 +1331,13 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             const char* e4 = std::getenv("MIBA_TAIL");
             W.tail = (P.solver == 2 && W.bcr.band && W.fused && !shard && !W.det_tbuf && band_tail_blocks(P, W.bcr.band) > 0 &&
                       !(e4 && e4[0] == '0')) ? 1 : 0;
+            // larger windows, opt-in (MIBA_BSFIN=1): the back-substitution chunks and the decision in one launch
+            // (k_backsub_final). Measured slower at C4 (4035-4070 vs 4154-4195 LM it/s, same box: the chunks'
+            // drained agent-scope partial stores and the decision workgroup's agent-scope loads cost more than the
+            // k_final launch they save) and even at C2, so k_backsub_chunk + k_final stay the default
+            const char* e5 = std::getenv("MIBA_BSFIN");
+            W.bsfin = (!W.tail && W.fused && !shard && !W.det_tbuf && n_ap > 0 && P.n_bs_chunks > 0 &&
+                       (e5 && e5[0] == '1')) ? 1 : 0;
             W.tail_flags = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 4);
             W.tail_seq = 0;
             HIPCHECK(ctx, hipMemsetAsync(W.tail_flags, 0, 2 * sizeof(unsigned), s));
@@ -1352,6 +1362,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->n_adm_all = n_adm_all;
         ctx->sw_full = W.sw;
         ctx->tail_full = W.tail;
+        ctx->bsfin_full = W.bsfin;
         set_consts(ctx);
         ctx->nblk_pt = nblk_pt;
         ctx->prepared = true;
@@ -1439,6 +1450,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         ctx->pinfo.bcr_path = P.solver == 2 ? bcr_path_id(ctx->W.bcr) : -1;
         ctx->pinfo.lin_path = ctx->W.sw;
     ctx->pinfo.tail = ctx->W.tail;
+    ctx->pinfo.bsfin = ctx->W.bsfin;
         return BA_OK;
     };
     int rc = finish();
@@ -1532,6 +1544,7 @@ static int bcr_timeout_retry(ba_context* ctx, LmState& S) {
     Bw.dense1 = 0;  // (k_bcr_dense1 waits only inside its workgroup: a forced spin bound can still time it out)
     ctx->W.sw = 0;  // the small-window Schur launch's envelope tiles wait for its camera side
     ctx->W.tail = 0;  // the band tail's chunks and decision wait for the solve / the chunks
+    ctx->W.bsfin = 0;  // the back-substitution launch's decision workgroup waits for its chunks
     ctx->bcr_fallback = true;
     if (Bw.flags) HIPCHECK(ctx, hipMemsetAsync(Bw.flags, 0, sizeof(unsigned) * (16 + 6 * Bw.nblk), s));
     HIPCHECK(ctx, bcr_reset_pull_slots(Bw, false, s));

@@ -187,7 +187,9 @@ __device__ __forceinline__ void backsub_pre(const DevProblem& P, const BaConsts&
         L.pt[pl][q] = v;
     }
 }
-template <bool O32, bool PUB = false>
+// PUB_OUT alone (k_backsub_final, C4-size windows): y and the candidates come from the previous launch (plain loads),
+// only the partials are stored past the L2 and drained for the decision workgroup of the same launch
+template <bool O32, bool PUB = false, bool PUB_OUT = PUB>
 __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                              const double* __restrict__ scale, const double* __restrict__ pdata,
                                              const double* __restrict__ y, const double* __restrict__ delta,
@@ -204,6 +206,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     // fused path: the reduced solve has consumed S; zero this chunk's share of its envelope tiles for the next
     // iteration's atomic assembly (k_final zeroes rhs, which still holds y here)
     for (int t = ch * n_ztiles / nch; !PUB && t < (ch + 1) * n_ztiles / nch; ++t) {  // (PUB: the caller, after)
+        // (k_backsub_final: S was read by the previous launch, so the chunks zero it here as k_backsub_chunk does)
         const int2 ij = ztiles[t];
         Sz[(size_t)(16 * ij.x + (threadIdx.x >> 4)) * P.npad + 16 * ij.y + (threadIdx.x & 15)] = 0.0;
     }
@@ -357,9 +360,9 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             double* q = part + slot[k] * P.part_stride + ch;
-            if constexpr (PUB) tail_st(q, pv[k]); else *q = pv[k];
+            if constexpr (PUB_OUT) tail_st(q, pv[k]); else *q = pv[k];
         }
-        if constexpr (PUB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the count
+        if constexpr (PUB_OUT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the count
     }
 }
 

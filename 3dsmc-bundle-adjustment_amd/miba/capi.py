@@ -152,6 +152,7 @@ class BaPrepareInfo(C.Structure):
         ("lin_path", C.c_int32),
         ("plan_device", C.c_int32),
         ("tail", C.c_int32),
+        ("bsfin", C.c_int32),
     ]
 
     def __init__(self, *args, **kw):

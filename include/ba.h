@@ -217,6 +217,8 @@ typedef struct ba_prepare_info {
     int32_t plan_device;     /* 1: the window's plan passes ran on the device (MIBA_DEVICE_PLAN; 0 on a reuse) */
     int32_t tail;            /* 1: the band solve's launch also runs the point back-substitution and the LM
                                 decision (bcr_path 5, small unsharded windows; MIBA_TAIL=0: separate launches) */
+    int32_t bsfin;           /* 1: the point back-substitution and the LM decision run in one launch (larger
+                                unsharded windows, k_backsub_final; opt-in, MIBA_BSFIN=1) — version 2 */
 } ba_prepare_info;
 /* the smallest struct_size ba_last_prepare accepts: the fields through total_ms (the round-3 layout) */
 #define BA_PREPARE_INFO_MIN_SIZE ((int32_t)(offsetof(ba_prepare_info, total_ms) + sizeof(double)))

@@ -160,6 +160,41 @@ def test_band_tail_timeout_reruns_with_the_separate_launches(monkeypatch):
     np.testing.assert_allclose(q.cams, q2.cams, rtol=0, atol=1e-10)
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_backsub_final_timeout_reruns_with_the_separate_launches(cfg, monkeypatch):
+    """The one-launch back-substitution + decision (k_backsub_final, larger windows) under a forced one-poll spin
+    bound: the decision workgroup's wait for its chunks times out (and so do the split BCR's hand-offs), the
+    iteration re-runs with the separate launches inside the same solve (BA_OK, oracle parity), and the next solve of
+    the window (plan cache) takes the one-launch path again."""
+    p = synthetic.make_config(cfg)
+    it = 5 if cfg == "C2" else 3
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=it))
+    monkeypatch.setenv("MIBA_BSFIN", "1")  # (opt-in: measured slower than the two launches at C4)
+    with _solver(max_num_iterations=it) as s:
+        s.solve(p.copy())
+        assert s.last_prepare()["bsfin"] == 1
+        monkeypatch.setenv("MIBA_BCR_SPIN_LIMIT", "1")
+        monkeypatch.setenv("MIBA_BCR", "launch")  # (no BCR hand-off waits: the decision workgroup's is the one forced)
+        q = p.copy()
+        sg = s.solve(q)
+        note = s.last_error()
+        monkeypatch.delenv("MIBA_BCR_SPIN_LIMIT")
+        monkeypatch.delenv("MIBA_BCR")
+        q2 = p.copy()
+        sg2 = s.solve(q2)
+        info2 = s.last_prepare()
+        note2 = s.last_error()
+    assert "re-run with the per-level BCR launches" in note, note
+    assert info2["bsfin"] == 1 and info2["bcr_path"] >= 2, info2  # (MIBA_BCR is in the plan key: a fresh plan)
+    assert note2 == "", note2
+    for g in (sg, sg2):
+        assert g["termination"] == so["termination"], (g, so)
+        assert g["num_iterations"] == so["num_iterations"]
+        assert g["num_successful_steps"] == so["num_successful_steps"]
+        assert abs(g["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (g, so)
+    np.testing.assert_allclose(q.cams, q2.cams, rtol=0, atol=1e-10)
+
+
 def test_two_contexts_solve_concurrently_on_one_gpu():
     """Two host threads, one context each, solving C2 windows at the same time on GPU 0: both resident BCR
     grids and every other launch share the device; both solves return BA_OK and match the oracle."""

@@ -438,6 +438,36 @@ def test_band_tail_launch_is_the_separate_launches(case, monkeypatch):
     assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sa, so)
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_backsub_final_launch_is_the_separate_launches(cfg, monkeypatch):
+    """Larger windows: the point back-substitution chunks and the final reduction + LM decision in one launch
+    (ba_band.hip k_backsub_final, ba_prepare_info.bsfin, opt-in MIBA_BSFIN=1; the decision workgroup waits for a
+    count of the chunks, whose partials are stored past the L2) against k_backsub_chunk + k_final (the default): the same bodies, the
+    same partial slots, so the same steps to rounding; and oracle parity (SPARSE_SCHUR back-substitution,
+    OptimizationUtils.cpp:300)."""
+    from miba.solver import Solver
+    p = synthetic.make_config(cfg)
+    iters = 6 if cfg == "C2" else 4
+    no_tol = dict(function_tolerance=0.0, parameter_tolerance=0.0, gradient_tolerance=0.0)
+    so = oracle.solve(p.copy(), oracle.default_options(max_num_iterations=iters, **no_tol))
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MIBA_BSFIN", mode)
+        q = p.copy()
+        with Solver(minimizer_progress_to_stdout=0, max_num_iterations=iters, **no_tol) as s:
+            res[mode] = (s.solve(q), q, s.iteration_log())
+            info = s.last_prepare()
+        assert info["bsfin"] == (mode == "1") and info["tail"] == 0 and info["bcr_path"] >= 2, (mode, info)
+    (sa, qa, la), (sb, qb, lb) = res["1"], res["0"]
+    assert sa["num_successful_steps"] == sb["num_successful_steps"] and sa["num_iterations"] == sb["num_iterations"]
+    assert abs(sa["final_cost"] - sb["final_cost"]) <= 1e-12 * sb["final_cost"], (sa, sb)
+    np.testing.assert_allclose(qa.cams, qb.cams, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(qa.points, qb.points, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(la, lb, rtol=1e-6, atol=1e-14)
+    assert sa["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sa["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"], (sa, so)
+
+
 def test_band_solve_on_one_block_windows(monkeypatch):
     """The band solve (with its tail launch, the default) also on a one-block window (C1, beside the
     small-window Schur launch) against k_bcr_dense1 (MIBA_BCR_BAND=0) and the oracle."""
