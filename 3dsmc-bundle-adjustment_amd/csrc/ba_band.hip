@@ -32,6 +32,8 @@
 // No inter-workgroup wait anywhere: the kernel cannot time out.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -190,7 +192,8 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
                                           int* __restrict__ flag, const BaConsts& c, const double* __restrict__ scale,
                                           const double* __restrict__ camdata, const double* __restrict__ lin,
                                           double* __restrict__ delta, double* __restrict__ part, int nb,
-                                          unsigned long long* __restrict__ tl, double* __restrict__ lds) {
+                                          unsigned long long* __restrict__ tl, double* __restrict__ lds,
+                                          unsigned* __restrict__ yflag = nullptr, unsigned yseq = 0) {
     constexpr int G = 6 * BC;
     constexpr int GG = G * G;
     constexpr int TPB = BAND_TPB, NW = BAND_TPB / 64;
@@ -619,7 +622,11 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
         const int e = tid + q * TPB;
         if (e < nx) lds[Ly.OPS + (e / 7) * BAND_OPS + 18 + e % 7] = xv[q];
     }
+    // the band tail: y drained by every thread, then published before the step (the chunks compute their candidate
+    // poses from y themselves, so the step runs beside them instead of ahead of them)
+    if (yflag) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (yflag && tid == 0) __hip_atomic_store(yflag, yseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int nupd = (nac + BCR_CAMS - 1) / BCR_CAMS;
     for (int w = wave; w < nupd; w += NW) {
         double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
@@ -701,7 +708,14 @@ __device__ __forceinline__ bool tail_wait(const unsigned* w, unsigned target, un
     }
 }
 
-template <int BC, bool O32>
+// Three hand-off words per launch (numbered by seq): tflags[0] = y published (the solve, before its camera step),
+// tflags[1] = back-substitution chunks done (counted), tflags[2] = the camera step's candidates and partials
+// published (the decision reads the partials).
+// STAMP (MIBA_BCR_STAMPS=1): the band solve's phase stamps in tl[0..BAND_STAMPS + BAND_FSTAMPS), then per workgroup b
+// s_memrealtime marks at tl[TAIL_ST0 + 8 b + k]: 0 start, 1 prologue done (chunks: backsub_pre; solve: step done),
+// 2 wait done, 3 body done (before the count / the flag), 4 exit
+static constexpr int TAIL_ST0 = 128;
+template <int BC, bool O32, bool STAMP = false>
 __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restrict__ st_c, DevProblem P, BaConsts c,
                                                         LmParams prm, double* __restrict__ S, double* __restrict__ rhs,
                                                         int* __restrict__ flag, const double* __restrict__ scale,
@@ -711,19 +725,31 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
                                                         const int2* __restrict__ ztiles, int n_ztiles, int nb_bs,
                                                         int nb_pt, int nb_upd, double* __restrict__ scal,
                                                         double* __restrict__ log, unsigned* __restrict__ tflags,
-                                                        unsigned seq) {
+                                                        unsigned seq, unsigned long long* __restrict__ tl) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int ok_s;
     LmState* const st = const_cast<LmState*>(st_c);
     const int b = blockIdx.x, tid = threadIdx.x;
+    unsigned long long tst[5] = {0, 0, 0, 0, 0};
+    auto mark = [&](int k) {
+        if constexpr (STAMP) if (tid == 0) tst[k] = realtime_now();
+    };
+    auto flush_marks = [&]() {
+        if constexpr (STAMP) if (tid == 0) for (int k = 0; k < 5; ++k) tl[TAIL_ST0 + 8 * b + k] = tst[k];
+    };
+    mark(0);
     if (b == 0) {
         // y, the candidate cameras and intrinsics, the step and the partials are stored past the L2 (PUB) and
         // drained by every thread before the count: no L2 write-back fence on the critical path (the consumers
         // read them with agent-scope loads)
-        band_body<BC, false, true>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, nullptr, lds);
+        band_body<BC, STAMP, true>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, tl, lds, tflags, seq);
+        mark(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(tflags, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mark(3);
+        if (tid == 0) __hip_atomic_store(tflags + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mark(4);
+        flush_marks();
         return;
     }
     if (tid >= 256) return;  // (the back-substitution and final bodies are written for 256 threads)
@@ -731,7 +757,12 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
     // a back-substitution chunk loads its records and point data and evaluates its y-free products before it waits
     BsPre<O32> pre;
     BsPreLds* const pl = reinterpret_cast<BsPreLds*>(reinterpret_cast<char*>(lds) + sizeof(BsLds));
-    if (b <= nb_bs) backsub_pre<O32>(P, c, st, scale, pdata, b - 1, *pl, pre);
+    double* const CL = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + sizeof(BsLds) + sizeof(BsPreLds));
+    if (b <= nb_bs) {
+        backsub_pre<O32>(P, c, st, scale, pdata, b - 1, *pl, pre);
+        cand_prefetch<O32>(P, st, scale, CL);
+    }
+    mark(1);
     // A wait past the spin bound marks the iteration for a re-run (FLAG_TIMEOUT) and then still waits for its
     // producer (which waits on nothing and runs ahead of its consumers in dispatch order) before this workgroup
     // touches S or rhs, which the re-run assembles onto
@@ -745,12 +776,14 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
             }
         }
         __syncthreads();
+        mark(2);
         if (ok_s) {
             backsub_body<O32, true>(P, c, st, scale, pdata, rhs, delta, part, ztiles, n_ztiles, S, b - 1, nb_bs,
-                                    *reinterpret_cast<BsLds*>(lds), pre, pl);
+                                    *reinterpret_cast<BsLds*>(lds), pre, pl, CL);
         } else if (tid == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flag) drained before the count
         }
+        mark(3);
         // thread 0 stored and drained this chunk's partials (PUB): count the chunk, no fence
         if (tid == 0) __hip_atomic_fetch_add(tflags + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // then this chunk's share of S's envelope tiles for the next iteration's assembly (the solve has read S;
@@ -760,19 +793,26 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
                 const int2 ij = ztiles[t];
                 S[(size_t)(16 * ij.x + (tid >> 4)) * P.npad + 16 * ij.y + (tid & 15)] = 0.0;
             }
+        mark(4);
+        flush_marks();
         return;
     }
-    // the final workgroup: every chunk of this launch has counted itself
+    // the final workgroup: every chunk of this launch has counted itself, and the solve's camera step is published
     if (tid == 0) {
-        ok_s = (skip || tail_wait(tflags + 1, seq * (unsigned)nb_bs, g_tail_spin_limit)) ? 1 : 0;
+        ok_s = (skip || (tail_wait(tflags + 1, seq * (unsigned)nb_bs, g_tail_spin_limit) &&
+                         tail_wait(tflags + 2, seq, g_tail_spin_limit))) ? 1 : 0;
         if (!ok_s) {
             raise_flag(flag, FLAG_TIMEOUT);
             (void)tail_wait(tflags + 1, seq * (unsigned)nb_bs, BOUND);  // every chunk done before rhs is zeroed
+            (void)tail_wait(tflags + 2, seq, BOUND);
         }
     }
     __syncthreads();
+    mark(2);
     final_body<2, true>(P, st, nb_pt, nb_upd, nb_bs, part, flag, scal, prm, lin, log, rhs, nullptr,
                         *reinterpret_cast<FinLds*>(lds));
+    mark(3);
+    flush_marks();
 }
 
 // ---- the back-substitution and the decision in one launch (C4-size windows: DevWork::bsfin) ----------------------
@@ -918,11 +958,16 @@ static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork&
     return hipGetLastError();
 }
 
+// the chunks' and the decision's dynamic LDS: BsLds | BsPreLds | the candidate table (cand_lds_doubles); FinLds
+static size_t tail_role_lds(const DevProblem& P) {
+    return std::max(sizeof(BsLds) + sizeof(BsPreLds) + sizeof(double) * cand_lds_doubles(P.n_cams, P.nac),
+                    sizeof(FinLds));
+}
+
 int band_tail_blocks(const DevProblem& P, int bc) {
     if (bc < 1 || bc > 3) return 0;
     const int n = P.n_bs_chunks + 2;
-    const size_t lds = std::max(band_lds_bytes(bc, (P.nac + bc - 1) / bc, P.nac),
-                                std::max(sizeof(BsLds) + sizeof(BsPreLds), sizeof(FinLds)));
+    const size_t lds = std::max(band_lds_bytes(bc, (P.nac + bc - 1) / bc, P.nac), tail_role_lds(P));
     // one resident round with room to spare (>= 256 CUs), the dynamic LDS beside the launch's static word
     return (P.n_ap > 0 && n <= 128 && lds <= 160 * 1024 - 256) ? n : 0;
 }
@@ -935,17 +980,62 @@ template <int BC, bool O32>
 static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const LmParams& prm, DevWork& W, int nb,
                                 int nb_pt, int nb_upd, hipStream_t s, Prof* pf) {
     static DeviceOnce attr;
+    static DeviceScratch stamp_buf;
+    static const int smode = env_on("MIBA_BCR_STAMPS");
     CKD(attr([] {
+        CKD(hipFuncSetAttribute((const void*)k_band_tail<BC, O32, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024 - 256));
         return hipFuncSetAttribute((const void*)k_band_tail<BC, O32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    160 * 1024 - 256);
     }));
-    const size_t lds = std::max(band_lds_bytes(BC, nb, P.nac), std::max(sizeof(BsLds) + sizeof(BsPreLds), sizeof(FinLds)));
+    const size_t lds = std::max(band_lds_bytes(BC, nb, P.nac), tail_role_lds(P));
     const int nb_bs = P.n_bs_chunks;
     ++W.tail_seq;
+    if (smode) {  // diagnostic: the band solve's phases and every tail workgroup's marks (MIBA_BCR_STAMPS=1)
+        const size_t nst = TAIL_ST0 + 8 * (size_t)(nb_bs + 2);
+        unsigned long long* dst = stamp_buf.get<unsigned long long>(nst * sizeof(unsigned long long));
+        if (!dst) return hipErrorOutOfMemory;
+        CKD(hipMemsetAsync(dst, 0, nst * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL((k_band_tail<BC, O32, true>), dim3(nb_bs + 2), dim3(BAND_TPB), lds, s, W.st, P, c, prm, W.S,
+                           W.rhs, W.chol_flag, W.scale, W.camdata, W.lin, W.delta, W.part, nb, W.pdata, W.env_tile,
+                           W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq, dst);
+        CKD(hipGetLastError());
+        std::vector<unsigned long long> h(nst);
+        CKD(hipMemcpyAsync(h.data(), dst, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        CKD(hipStreamSynchronize(s));
+        const unsigned long long* tw = h.data() + TAIL_ST0;
+        if (tw[0] && h[0]) {
+            const unsigned long long t0 = tw[0];  // the solve workgroup's start
+            auto us = [&](unsigned long long t) { return t ? (double)((long long)(t - t0)) / 100.0 : -1.0; };
+            std::fprintf(stderr, "band_tail<%d> nb=%d chunks=%d | solve wg: start 0 solved %.2f flag %.2f | solve phases:",
+                         BC, nb, nb_bs, us(tw[1]), us(tw[4]));
+            const unsigned long long bt0 = h[BAND_STAMPS - 1];
+            double prev = (double)((long long)(bt0 - t0)) / 100.0;
+            for (int k = 0; k < BAND_STAMPS - 1 && h[k]; ++k) {
+                const double t = (double)((long long)(h[k] - t0)) / 100.0;
+                std::fprintf(stderr, " %.2f", t - prev);
+                prev = t;
+            }
+            std::fprintf(stderr, "\n");
+            double mx[5] = {0, 0, 0, 0, 0}, mn[5] = {1e30, 1e30, 1e30, 1e30, 1e30};
+            for (int b = 1; b <= nb_bs; ++b)
+                for (int k = 0; k < 5; ++k) {
+                    const double v = us(tw[8 * b + k]);
+                    mx[k] = std::max(mx[k], v);
+                    mn[k] = std::min(mn[k], v);
+                }
+            std::fprintf(stderr, "  chunks (min..max us): start %.2f..%.2f pre %.2f..%.2f waited %.2f..%.2f body %.2f..%.2f "
+                                 "exit %.2f..%.2f\n", mn[0], mx[0], mn[1], mx[1], mn[2], mx[2], mn[3], mx[3], mn[4], mx[4]);
+            const unsigned long long* f = tw + 8 * (nb_bs + 1);
+            std::fprintf(stderr, "  final: start %.2f waited %.2f decided %.2f\n", us(f[0]), us(f[2]), us(f[3]));
+        }
+        return hipSuccess;
+    }
     if (pf) pf->begin(K_BCR_PERSIST, s);
     hipLaunchKernelGGL((k_band_tail<BC, O32>), dim3(nb_bs + 2), dim3(BAND_TPB), lds, s, W.st, P, c, prm, W.S, W.rhs,
                        W.chol_flag, W.scale, W.camdata, W.lin, W.delta, W.part, nb, W.pdata, W.env_tile,
-                       W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq);
+                       W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq,
+                       (unsigned long long*)nullptr);
     if (pf) pf->end(s);
     return hipGetLastError();
 }

@@ -103,6 +103,7 @@ struct DevProblem {
     int n_tiles, n_ovf_obs;
     int n_tiled_pts;  // active points [0, n_tiled_pts) belong to Schur tiles
     int n_seg, n_ap, n_adm, nac;
+    int n_cams;  // cameras of the window (the band tail's candidate-pose table)
     int n;     // reduced system size 6*nac + 4
     int npad;  // n rounded up to 16
     int kb;    // first intrinsics row = 6*nac
@@ -358,8 +359,9 @@ struct DevWork {
     unsigned sw_seq = 0;
     // the band solve's tail (small unsharded windows, default mode): the back-substitution chunks and the final
     // reduction + decision as workgroups of the band solve's launch (k_band_tail), behind two hand-off words
-    // tail_flags[0] (the solve's launch number) and [1] (back-substitution chunks done, monotonic within a solve;
-    // both reset by launch_reset); tail_seq: tail launches of this solve (host side)
+    // tail_flags[0] (the solve's launch number: y published), [1] (back-substitution chunks done, monotonic within a
+    // solve) and [2] (the solve's camera step published; all three reset by launch_reset); tail_seq: tail launches of
+    // this solve (host side)
     int tail = 0;
     // larger unsharded fused windows: the back-substitution chunks and the final reduction + decision in one launch
     // (k_backsub_final), counted on tail_flags[1] / tail_seq like the band tail (never both)

@@ -2560,7 +2560,7 @@ hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, con
                         const double* K0, int n_cams, int n_points, hipStream_t s) {
     if (W.sw_cnt) CK(hipMemsetAsync(W.sw_cnt, 0, sizeof(unsigned), s));  // the small-window launch's counter
     W.sw_seq = 0;
-    if (W.tail_flags) CK(hipMemsetAsync(W.tail_flags, 0, 2 * sizeof(unsigned), s));  // the band tail's hand-offs
+    if (W.tail_flags) CK(hipMemsetAsync(W.tail_flags, 0, 3 * sizeof(unsigned), s));  // the band tail's hand-offs
     W.tail_seq = 0;
     const int ncd = 7 * n_cams, npd = 3 * n_points;
     // fused path: S (npad^2, even: npad is a multiple of 16) and rhs are zeroed here too

@@ -1211,7 +1211,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         P.n_tiles = (int)tile_base.size(); P.n_ovf_obs = pl.n_ovf();
         P.n_tiled_pts = n_tiled;
         ctx->n_tiles = P.n_tiles; ctx->n_ovf_obs = P.n_ovf_obs; ctx->n_tiled_pts = n_tiled;
-        P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac;
+        P.n_seg = n_seg; P.n_ap = n_ap; P.n_adm = n_adm; P.nac = nac; P.n_cams = nc;
         P.n = n; P.npad = npad; P.kb = 6 * nac;
         P.off_pt = 6 * nac; P.off_k = 6 * nac + 3 * n_ap;
         {
@@ -1340,7 +1340,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
                        (e5 && e5[0] == '1')) ? 1 : 0;
             W.tail_flags = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 4);
             W.tail_seq = 0;
-            HIPCHECK(ctx, hipMemsetAsync(W.tail_flags, 0, 2 * sizeof(unsigned), s));
+            HIPCHECK(ctx, hipMemsetAsync(W.tail_flags, 0, 3 * sizeof(unsigned), s));
             const char* e2 = std::getenv("MIBA_SW");
             const int n_sw = P.n_tiles + 1 + n_seg + pp_blocks(n_ap - n_tiled, 1) + n_env;
             // one-block windows (<= BCR_CAMS active cameras) and the band tail's windows. The camera side hands

@@ -128,6 +128,26 @@ struct BsLds {
 struct BsPreLds {
     double pt[BS_PTS][PDATA + 6];
 };
+// Band tail (PUB): the candidate poses of every camera and the candidate intrinsics, computed by each chunk from y
+// (the band solve publishes y BEFORE its camera step, which then runs beside the chunks instead of ahead of them).
+// Before the wait: every camera's current pose (8 doubles per camera) and the active cameras' Jacobi scales; after it,
+// one thread per active camera overwrites its pose with T exp(-s y) (se3_plus, the step's own arithmetic: the same
+// values cam_step stores in the candidate slot) and one thread the intrinsics K - s_k y_k (intr_step's).
+// Layout after BsLds + BsPreLds in the tail launch's dynamic LDS: pose[n_cams][8] | K[4] | sc[nac][6].
+__host__ __device__ inline size_t cand_lds_doubles(int n_cams, int nac) { return 8 * (size_t)n_cams + 4 + 6 * (size_t)nac; }
+template <bool O32>
+__device__ __forceinline__ void cand_prefetch(const DevProblem& P, const LmState* __restrict__ st,
+                                              const double* __restrict__ scale, double* __restrict__ CL) {
+    if (skip_step(st)) return;
+    const int cur = st->cur;
+    const double* x = P.cams[cur];
+    for (int e = threadIdx.x; e < 7 * P.n_cams; e += TPB) CL[(e / 7) * 8 + e % 7] = x[e];
+    double* const sc = CL + 8 * (size_t)P.n_cams + 4;
+    for (int e = threadIdx.x; e < 6 * P.nac; e += TPB) sc[e] = scale[e];
+}
+// after the wait (y published): the candidate poses / intrinsics in place; the caller's next barrier publishes them
+__device__ __forceinline__ void cand_compute(const DevProblem& P, int cur, const double* __restrict__ scale,
+                                             const double* __restrict__ y, double* __restrict__ CL);
 // Band tail (PUB): what a back-substitution chunk can compute before the band solve's y exists — its observation
 // records, each thread's first observation's y-free product A = diag(s_p) Jp^T Jc diag(s_c) (3 x 6; v = A y_c
 // after the wait) and the chunk's point data in LDS — so only the y / candidate loads and short products follow it
@@ -195,7 +215,8 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
                                              const double* __restrict__ y, const double* __restrict__ delta,
                                              double* __restrict__ part, const int2* __restrict__ ztiles, int n_ztiles,
                                              double* __restrict__ Sz, int ch, int nch, BsLds& L,
-                                             const BsPre<O32>& pre = BsPre<O32>{}, BsPreLds* PL = nullptr) {
+                                             const BsPre<O32>& pre = BsPre<O32>{}, BsPreLds* PL = nullptr,
+                                             double* __restrict__ CL = nullptr) {
     const bool use_pre = PL != nullptr;
     const bool PRE = use_pre && pre.on;  // (block-uniform)
     auto& co = L.co;
@@ -279,6 +300,8 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
             for (int i = 0; i < 3; ++i) co[o - ob][i] = v[i];
         }
     }
+    // the band tail: this chunk's candidate poses / intrinsics from y (published by the barrier below / in block_sum)
+    if (CL) cand_compute(P, cur, scale, y, CL);
     if (big) block_sum<3>(bsum, lds, out);  // out[0..3) valid for every thread after this
     __syncthreads();
     // ---- phase 2
@@ -340,7 +363,9 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         const double* X = PRE ? &PL->pt[pl][PDATA + 3] : P.pts[cur] + 3 * P.pt_idx[ap];
         const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
         ObsEval en;
-        if constexpr (PUB) {
+        if (CL) {  // the band tail: the chunk's own candidate table (cand_compute)
+            eval_obs(c, CL + 8 * cam, xn, CL + 8 * (size_t)P.n_cams, ro.u(), ro.v(), ro.d(), en);
+        } else if constexpr (PUB) {
             double pose[7], kn[4];
 #pragma unroll
             for (int k = 0; k < 7; ++k) pose[k] = tail_ld(P.cams[cur ^ 1] + 7 * cam + k);
@@ -363,6 +388,27 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
             if constexpr (PUB_OUT) tail_st(q, pv[k]); else *q = pv[k];
         }
         if constexpr (PUB_OUT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the count
+    }
+}
+
+__device__ __forceinline__ void cand_compute(const DevProblem& P, int cur, const double* __restrict__ scale,
+                                             const double* __restrict__ y, double* __restrict__ CL) {
+    const double* const sc = CL + 8 * (size_t)P.n_cams + 4;
+    for (int t = threadIdx.x; t < P.nac; t += TPB) {
+        double* const xc = CL + 8 * (size_t)P.ac_cam[t];
+        double x[7], d[6], tp[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) x[j] = xc[j];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = -tail_ld(y + 6 * t + k) * sc[6 * t + k];  // cam_step's delta
+        se3_plus(x, d, tp);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) xc[j] = tp[j];
+    }
+    if (threadIdx.x == TPB - 1) {  // intr_step's candidate: K + (-y_k s_k)
+        double* const kc = CL + 8 * (size_t)P.n_cams;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) kc[m] = P.K[cur][m] + (-tail_ld(y + P.kb + m) * scale[P.off_k + m]);
     }
 }
 
