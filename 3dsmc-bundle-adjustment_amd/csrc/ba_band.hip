@@ -660,9 +660,7 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
         // (lanes >= 16 hold no term: a 16-lane butterfly in a fixed order)
         static_assert(BCR_CAMS + 1 <= 16, "the step's terms sit on lanes < 16");
 #pragma unroll
-        for (int off = 8; off > 0; off >>= 1)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off, 16);
+        for (int k = 0; k < 4; ++k) acc[k] = dpp_row_sum(acc[k]);
         if (lane == 0) {
             st_opt<PUB>(part + PART_UPD_SN2 * P.part_stride + w, acc[0]);
             st_opt<PUB>(part + PART_UPD_MCC * P.part_stride + w, acc[1]);
@@ -712,7 +710,7 @@ __device__ __forceinline__ bool tail_wait(const unsigned* w, unsigned target, un
 // tflags[1] = back-substitution chunks done (counted), tflags[2] = the camera step's candidates and partials
 // published (the decision reads the partials).
 // STAMP (MIBA_BCR_STAMPS=1): the band solve's phase stamps in tl[0..BAND_STAMPS + BAND_FSTAMPS), then per workgroup b
-// s_memrealtime marks at tl[TAIL_ST0 + 8 b + k]: 0 start, 1 prologue done (chunks: backsub_pre; solve: step done),
+// s_memrealtime marks at tl[TAIL_ST0 + 16 b + k]: 0 start, 1 prologue done (chunks: backsub_pre; solve: step done),
 // 2 wait done, 3 body done (before the count / the flag), 4 exit
 static constexpr int TAIL_ST0 = 128;
 template <int BC, bool O32, bool STAMP = false>
@@ -735,7 +733,7 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
         if constexpr (STAMP) if (tid == 0) tst[k] = realtime_now();
     };
     auto flush_marks = [&]() {
-        if constexpr (STAMP) if (tid == 0) for (int k = 0; k < 5; ++k) tl[TAIL_ST0 + 8 * b + k] = tst[k];
+        if constexpr (STAMP) if (tid == 0) for (int k = 0; k < 5; ++k) tl[TAIL_ST0 + 16 * b + k] = tst[k];
     };
     mark(0);
     if (b == 0) {
@@ -779,7 +777,8 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
         mark(2);
         if (ok_s) {
             backsub_body<O32, true>(P, c, st, scale, pdata, rhs, delta, part, ztiles, n_ztiles, S, b - 1, nb_bs,
-                                    *reinterpret_cast<BsLds*>(lds), pre, pl, CL);
+                                    *reinterpret_cast<BsLds*>(lds), pre, pl, CL,
+                                    STAMP ? tl + TAIL_ST0 + 16 * b + 8 : nullptr);
         } else if (tid == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flag) drained before the count
         }
@@ -810,7 +809,7 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
     __syncthreads();
     mark(2);
     final_body<2, true>(P, st, nb_pt, nb_upd, nb_bs, part, flag, scal, prm, lin, log, rhs, nullptr,
-                        *reinterpret_cast<FinLds*>(lds));
+                        *reinterpret_cast<FinLds*>(lds), STAMP ? tl + TAIL_ST0 + 16 * b + 5 : nullptr);
     mark(3);
     flush_marks();
 }
@@ -992,7 +991,7 @@ static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const Lm
     const int nb_bs = P.n_bs_chunks;
     ++W.tail_seq;
     if (smode) {  // diagnostic: the band solve's phases and every tail workgroup's marks (MIBA_BCR_STAMPS=1)
-        const size_t nst = TAIL_ST0 + 8 * (size_t)(nb_bs + 2);
+        const size_t nst = TAIL_ST0 + 16 * (size_t)(nb_bs + 2);
         unsigned long long* dst = stamp_buf.get<unsigned long long>(nst * sizeof(unsigned long long));
         if (!dst) return hipErrorOutOfMemory;
         CKD(hipMemsetAsync(dst, 0, nst * sizeof(unsigned long long), s));
@@ -1020,14 +1019,22 @@ static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const Lm
             double mx[5] = {0, 0, 0, 0, 0}, mn[5] = {1e30, 1e30, 1e30, 1e30, 1e30};
             for (int b = 1; b <= nb_bs; ++b)
                 for (int k = 0; k < 5; ++k) {
-                    const double v = us(tw[8 * b + k]);
+                    const double v = us(tw[16 * b + k]);
                     mx[k] = std::max(mx[k], v);
                     mn[k] = std::min(mn[k], v);
                 }
             std::fprintf(stderr, "  chunks (min..max us): start %.2f..%.2f pre %.2f..%.2f waited %.2f..%.2f body %.2f..%.2f "
                                  "exit %.2f..%.2f\n", mn[0], mx[0], mn[1], mx[1], mn[2], mx[2], mn[3], mx[3], mn[4], mx[4]);
-            const unsigned long long* f = tw + 8 * (nb_bs + 1);
-            std::fprintf(stderr, "  final: start %.2f waited %.2f decided %.2f\n", us(f[0]), us(f[2]), us(f[3]));
+            {  // inside the body of the chunk that finished last: phase 1 (+ candidates), 2, 3, reduced, drained
+                int bl = 1;
+                for (int b = 1; b <= nb_bs; ++b) if (tw[16 * b + 3] > tw[16 * bl + 3]) bl = b;
+                const unsigned long long* q = tw + 16 * bl + 8;
+                std::fprintf(stderr, "  last chunk %d: waited %.2f phase1 %.2f phase2 %.2f phase3 %.2f reduced %.2f drained %.2f\n",
+                             bl - 1, us(tw[16 * bl + 2]), us(q[0]), us(q[1]), us(q[2]), us(q[3]), us(q[4]));
+            }
+            const unsigned long long* f = tw + 16 * (nb_bs + 1);
+            std::fprintf(stderr, "  final: start %.2f waited %.2f | loads in %.2f reduced %.2f decided %.2f | exit %.2f\n",
+                         us(f[0]), us(f[2]), us(f[5]), us(f[6]), us(f[7]), us(f[3]));
         }
         return hipSuccess;
     }

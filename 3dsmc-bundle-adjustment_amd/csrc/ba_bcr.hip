@@ -856,10 +856,9 @@ __device__ __forceinline__ void border_apply(const LmState* __restrict__ st, con
         update_camera(P, c, cur, radius, scale, camdata, ac, ybl + 6 * tid, delta, acc);
     else if (i == 0 && tid == BCR_CAMS)
         update_intrinsics(P, c, cur, radius, scale, lin, yk, delta, acc);
+    // (only lanes < 16 hold a term: the row-0 sum by DPP is the total)
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+    for (int k = 0; k < 4; ++k) acc[k] = dpp_row_sum(acc[k]);
     if (tid == 0) {
         part[PART_UPD_SN2 * P.part_stride + i] = acc[0];
         part[PART_UPD_MCC * P.part_stride + i] = acc[1];
@@ -894,10 +893,9 @@ __device__ __forceinline__ void block_step(const LmState* __restrict__ st, const
         update_camera(P, c, cur, radius, scale, camdata, ac, ybl + 6 * tid, delta, acc);
     else if (intr && tid == BCR_CAMS)
         update_intrinsics(P, c, cur, radius, scale, lin, yk, delta, acc);
+    // (only lanes < 16 hold a term: the row-0 sum by DPP is the total)
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+    for (int k = 0; k < 4; ++k) acc[k] = dpp_row_sum(acc[k]);
     if (tid == 0) {
         part[PART_UPD_SN2 * P.part_stride + i] = acc[0];
         part[PART_UPD_MCC * P.part_stride + i] = acc[1];
@@ -2370,10 +2368,9 @@ __global__ __launch_bounds__(TPB_D1) void k_bcr_dense1(const LmState* __restrict
             double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sn2, mcc, cand cost, |x_cand|^2
             if (lane < P.nac) cam_step(P, c, cur, radius, cops, lane, vz + 6 * lane, delta, acc);
             else if (lane == BCR_CAMS) intr_step(P, c, cur, radius, iops, vz + P.kb, delta, acc);
+            // (only lanes <= BCR_CAMS hold a term: the row-0 sum by DPP is the total)
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], off);
+            for (int k = 0; k < 4; ++k) acc[k] = dpp_row_sum(acc[k]);
             if (lane == 0) {
                 part[PART_UPD_SN2 * P.part_stride] = acc[0];
                 part[PART_UPD_MCC * P.part_stride] = acc[1];

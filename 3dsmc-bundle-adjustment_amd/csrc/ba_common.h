@@ -9,16 +9,27 @@
 
 #include "ba_device.h"
 #include "ba_kernels.h"
+#include "ba_solve_util.h"
 
 namespace miba {
 
 // ---------------------------------------------------------------- reductions
+// The xor butterfly (ds_bpermute per step and half). Kept for the block sums of the kernels instantiated for both
+// observation layouts (k_point_prep, k_backsub_chunk, the Schur tiles' intrinsics workgroup): with the DPP sum there,
+// the obs32 and f64 instantiations of a deterministic solve stopped agreeing in the last bit
+// (test_obs32_records_match_f64_arrays_bitwise, bisected to ba_tail.h's block_sum), for a reason not found.
 template <int NV>
 __device__ __forceinline__ void wave_sum(double (&v)[NV]) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off);
+}
+// DPP wave sums: the decision's reductions (block_sum_nw) and the band tail's chunk sums (block_sum_dpp)
+template <int NV>
+__device__ __forceinline__ void wave_sum_dpp(double (&v)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = dpp_wave_sum(v[i]);
 }
 
 // Wave reduce-scatter by recursive halving: at the step with lane offset OFF a lane keeps
@@ -58,7 +69,7 @@ struct HalveRemain<N, 0> { static constexpr int value = N; };
 // NW-wave variants (k_final runs 16 waves); lds holds NW * NV doubles. Wave sums added in wave order.
 template <int NW, int NV>
 __device__ __forceinline__ void block_sum_nw(double (&v)[NV], double* lds, double* out) {
-    wave_sum<NV>(v);
+    wave_sum_dpp<NV>(v);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0)
 #pragma unroll
@@ -75,8 +86,7 @@ __device__ __forceinline__ void block_sum_nw(double (&v)[NV], double* lds, doubl
 
 template <int NW>
 __device__ __forceinline__ double block_max_nw(double v, double* lds) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    v = dpp_wave_max(v);
     if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
     __syncthreads();
     double r = lds[0];

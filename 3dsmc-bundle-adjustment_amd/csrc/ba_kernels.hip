@@ -1368,12 +1368,11 @@ __device__ __forceinline__ void schur_tile_body(DevProblem P, BaConsts c, const 
             double fp_kk[14];
 #pragma unroll
             for (int i = 0; i < 14; ++i) fp_kk[i] = lane < CHUNK_PTS ? kkL[14 * lane + i] : 0.0;
-            wave_sum<14>(fp_kk);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                fp_gmax = fmax(fp_gmax, __shfl_xor(fp_gmax, off));
-                fp_bad = fmax(fp_bad, __shfl_xor(fp_bad, off));
-            }
+            // (DPP: the fused point side runs in default mode only, never in the deterministic solves whose obs32
+            // and f64 instantiations are compared bit for bit)
+            wave_sum_dpp<14>(fp_kk);
+            fp_gmax = dpp_wave_max(fp_gmax);
+            fp_bad = dpp_wave_max(fp_bad);
             if (lane == 0) {
 #pragma unroll
                 for (int i = 0; i < 14; ++i) zeL[i] = fp_kk[i];  // (zeL is free after the last chunk)

@@ -18,6 +18,63 @@ __device__ __forceinline__ unsigned long long realtime_now() {
     return t;
 }
 
+// Wave reductions by DPP moves (gfx9 DPP controls, two 32-bit moves per f64) instead of __shfl_xor, which HIP
+// lowers to ds_bpermute: an LDS-crossbar round trip per step and half, on the critical path of every workgroup-wide
+// sum (a 5-value block sum took ~1 us in the band tail's back-substitution chunks, MIBA_BCR_STAMPS). Called in
+// uniform control flow with all 64 lanes active. Every lane of a row ends with the bitwise same value (the pairings
+// are symmetric and f64 addition commutes), so the order is fixed per lane and run to run.
+enum : int {
+    DPP_QP_X1 = 0xB1,       // quad_perm [1,0,3,2]: lane ^ 1
+    DPP_QP_X2 = 0x4E,       // quad_perm [2,3,0,1]: lane ^ 2
+    DPP_ROW_MIRROR = 0x140, // lane 15 - i within the row of 16
+    DPP_ROW_HMIRROR = 0x141,  // lane 7 - i within each half row of 8
+    DPP_ROW_BCAST15 = 0x142,  // lane 15 of row r -> row r + 1 (row_mask selects the rows written)
+    DPP_ROW_BCAST31 = 0x143,  // lane 31 -> rows 2, 3
+};
+// x from the DPP source lane; lanes of rows outside ROW_MASK get `old`
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double x, double old) {
+    const long long u = __double_as_longlong(x), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)u, CTRL, ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(u >> 32), CTRL, ROW_MASK, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// the sum over each row of 16 lanes, in every lane of the row
+// (fp contract off: the adds must not fuse with a caller's product into an FMA, whose rounding would then depend on
+// the inlining context — the obs32 and f64 instantiations of a kernel must sum bit for bit alike)
+__device__ __forceinline__ double dpp_row_sum(double x) {
+#pragma clang fp contract(off)
+    x += dpp_f64<DPP_QP_X1>(x, 0.0);
+    x += dpp_f64<DPP_QP_X2>(x, 0.0);
+    x += dpp_f64<DPP_ROW_HMIRROR>(x, 0.0);
+    x += dpp_f64<DPP_ROW_MIRROR>(x, 0.0);
+    return x;
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const long long u = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)u, l), hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// the sum over the wave, in every lane: the row sums r0..r3 by DPP, then the rows combined by two xor exchanges
+// ((r0 + r1) + (r2 + r3), the same bits in every lane). (A lane-63 total by row_bcast:15 / row_bcast:31 and a
+// v_readlane broadcast made the obs32 and f64 instantiations of a kernel differ in the last bit:
+// test_obs32_records_match_f64_arrays_bitwise.)
+__device__ __forceinline__ double dpp_wave_sum(double x) {
+#pragma clang fp contract(off)
+    x = dpp_row_sum(x);
+    x += __shfl_xor(x, 16);
+    x += __shfl_xor(x, 32);
+    return x;
+}
+__device__ __forceinline__ double dpp_wave_max(double x) {
+    x = fmax(x, dpp_f64<DPP_QP_X1>(x, x));
+    x = fmax(x, dpp_f64<DPP_QP_X2>(x, x));
+    x = fmax(x, dpp_f64<DPP_ROW_HMIRROR>(x, x));
+    x = fmax(x, dpp_f64<DPP_ROW_MIRROR>(x, x));
+    x = fmax(x, dpp_f64<DPP_ROW_BCAST15, 0xa>(x, x));
+    x = fmax(x, dpp_f64<DPP_ROW_BCAST31, 0xc>(x, x));
+    return readlane_f64(x, 63);
+}
 // v from lane l to every lane (v_readlane on both halves of the f64)
 __device__ __forceinline__ double bcast_b(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);

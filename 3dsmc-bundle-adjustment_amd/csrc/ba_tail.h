@@ -7,6 +7,7 @@
 #include "ba_common.h"
 #include "ba_device.h"
 #include "ba_kernels.h"
+#include "ba_solve_util.h"
 
 namespace miba {
 
@@ -68,6 +69,22 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* lds /*4*NV*/,
 }
 
 
+// block_sum with the DPP wave sum (the band tail's chunks: default mode only, one instantiation per layout is never
+// compared bitwise with the other)
+template <int NV>
+__device__ __forceinline__ void block_sum_dpp(double (&v)[NV], double* lds /*4*NV*/, double* out /*NV*/) {
+    wave_sum_dpp<NV>(v);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < NV; i += blockDim.x)
+        out[i] = lds[0 * NV + i] + lds[1 * NV + i] + lds[2 * NV + i] + lds[3 * NV + i];
+    __syncthreads();
+}
+
+
 // Block (256 threads) sum of NV values via the wave reduce-scatter; out[0..NV) valid after return.
 // lds must hold 4 * NV doubles. Fixed summation order (deterministic).
 template <int NV>
@@ -87,8 +104,7 @@ __device__ __forceinline__ void block_sum_rs(double (&v)[NV], double* lds, doubl
 
 
 __device__ __forceinline__ double block_max(double v, double* lds) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    v = dpp_wave_max(v);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) lds[wave] = v;
     __syncthreads();
@@ -216,7 +232,11 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
                                              double* __restrict__ part, const int2* __restrict__ ztiles, int n_ztiles,
                                              double* __restrict__ Sz, int ch, int nch, BsLds& L,
                                              const BsPre<O32>& pre = BsPre<O32>{}, BsPreLds* PL = nullptr,
-                                             double* __restrict__ CL = nullptr) {
+                                             double* __restrict__ CL = nullptr,
+                                             unsigned long long* __restrict__ bst = nullptr) {
+    auto bmark = [&](int k) {  // (diagnostic stamps: band tail, MIBA_BCR_STAMPS=1)
+        if (bst && threadIdx.x == 0) bst[k] = realtime_now();
+    };
     const bool use_pre = PL != nullptr;
     const bool PRE = use_pre && pre.on;  // (block-uniform)
     auto& co = L.co;
@@ -304,6 +324,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     if (CL) cand_compute(P, cur, scale, y, CL);
     if (big) block_sum<3>(bsum, lds, out);  // out[0..3) valid for every thread after this
     __syncthreads();
+    bmark(0);
     // ---- phase 2
     if (tid < npts) {
         const int ap = apb + tid;
@@ -344,6 +365,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         }
     }
     __syncthreads();
+    bmark(1);
     // ---- phase 3
     (void)delta;
     it = 0;
@@ -378,7 +400,10 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         if (en.ok) acc[2] += en.cost; else acc[3] = 1.0;
     }
     if (!isfinite(acc[0]) || !isfinite(acc[1])) acc[3] = 1.0;
-    block_sum<5>(acc, lds, out);
+    bmark(2);
+    if constexpr (PUB) block_sum_dpp<5>(acc, lds, out);
+    else block_sum<5>(acc, lds, out);
+    bmark(3);
     if (tid == 0) {
         const double pv[5] = {out[0], out[1], out[2], out[3] > 0.0 ? 1.0 : 0.0, out[4]};
         const int slot[5] = {PART_BS_SN2, PART_BS_MCC, PART_BS_COST, PART_BS_BAD, PART_BS_XN2};
@@ -388,6 +413,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
             if constexpr (PUB_OUT) tail_st(q, pv[k]); else *q = pv[k];
         }
         if constexpr (PUB_OUT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the count
+        bmark(4);
     }
 }
 
@@ -428,7 +454,8 @@ __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restr
                                            int nblk_bs, const double* __restrict__ part,
                                            const int* __restrict__ chol_flag, double* __restrict__ scal,
                                            const LmParams& prm, const double* __restrict__ lin, double* __restrict__ log,
-                                           double* __restrict__ rhs_z, unsigned* __restrict__ bcr_epoch, FinLds& L) {
+                                           double* __restrict__ rhs_z, unsigned* __restrict__ bcr_epoch, FinLds& L,
+                                           unsigned long long* __restrict__ fst = nullptr) {
     double* const lds = L.lds;
     double* const out = L.out;
     double* const red = L.red;
@@ -475,9 +502,11 @@ __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restr
     if (bcr_epoch && threadIdx.x == 0 && !S0.stop_next) *bcr_epoch += 1;
     if (rhs_z)  // fused path: y has been consumed; rhs is the next assembly's atomic target
         for (int i = threadIdx.x; i < P.npad; i += TPB_F) rhs_z[i] = 0.0;
+    if (fst && threadIdx.x == 0) fst[0] = realtime_now();  // (diagnostic stamps: band tail, MIBA_BCR_STAMPS=1)
     block_sum_nw<NW_F, 4>(acc, lds, out);
     gm = block_max_nw<NW_F>(gm, red);
     bad = block_max_nw<NW_F>(bad, red);
+    if (fst && threadIdx.x == 0) fst[1] = realtime_now();
     if (threadIdx.x == 0) {
         double sc[SC_N] = {};
         sc[SC_XN2] = out[3];
@@ -489,6 +518,7 @@ __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restr
 #pragma unroll
         for (int k = 0; k < SC_N; ++k) scal[k] = sc[k];
         lm_decide_pre(S0, st, prm, lin0, lin1, sc, log);
+        if (fst) fst[2] = realtime_now();
     }
 }
 
