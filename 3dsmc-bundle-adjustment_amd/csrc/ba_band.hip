@@ -110,14 +110,6 @@ __device__ __forceinline__ double ubc(double v, bool hi) {
         return bcast_half(v, J, hi);
     }
 }
-// compile-time loop (the DPP lane select is an immediate)
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        sfor<B + 1, E>(f);
-    }
-}
 // 4x4 border system as border_solve4 (bk = [b_k | S_kk lower packed], red[m * 5 + c] = (B^T [u | V])[m][c]), the
 // Cholesky pivots by v_rsq_f64 + one Newton step and the solves by products: no square root or division on the path
 // (border_solve4's IEEE square roots and divisions took ~1.5 us here). bad: a non-positive pivot.
@@ -395,7 +387,9 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
                     dn = ubc<U, j + 1>(__builtin_fma(-l, l, a[j + 1]), hi);
                     sfor<j + 1, G>([&](auto kc) {
                         constexpr int k = decltype(kc)::value;
-                        a[k] = __builtin_fma(-l, ubc<U, k>(l, hi), a[k]);
+                        // a 16-lane unit: one v_fmac_f64_dpp per column (row_newbcast hands lane k's l to the FMA)
+                        if constexpr (U == 16) fnma_row_bcast<k, k == j + 1>(a[k], l, l);
+                        else a[k] = __builtin_fma(-l, ubc<U, k>(l, hi), a[k]);
                     });
                 }
             });

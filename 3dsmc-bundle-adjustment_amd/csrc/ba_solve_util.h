@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 namespace miba {
 
@@ -81,6 +82,30 @@ __device__ __forceinline__ double bcast_b(double v, int l) {
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
     return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// compile-time loop (a DPP lane select is an immediate)
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+
+// a -= lr[lane K of this lane's 16-lane row] * l in ONE v_fmac_f64_dpp: row_newbcast (the DPP64 control of gfx90a+)
+// hands src0 from lane K of the row to every lane of it. NOP: two wait states first — a DPP read of a VGPR that a VALU
+// wrote in the previous two cycles is a hazard the compiler's hazard recognizer does not see through inline assembly
+// (callers put it on the first DPP read after the source was produced; the later reads of the same source follow
+// other DPP instructions).
+template <int K, bool NOP>
+__device__ __forceinline__ void fnma_row_bcast(double& a, double lr, double l) {
+    static_assert(K >= 0 && K < 16, "row_newbcast selects a lane of the 16-lane row");
+    if constexpr (NOP)
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+            : "+v"(a) : "v"(lr), "v"(l), "i"(K));
+    else
+        asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(a) : "v"(lr), "v"(l), "i"(K));
 }
 
 // 4x4 border system (C - sum B^T V) y_k = b_k - sum B^T u on one thread: bk = [b_k | S_kk lower packed],

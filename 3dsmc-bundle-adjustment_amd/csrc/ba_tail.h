@@ -135,7 +135,7 @@ __device__ __forceinline__ void tail_st(double* p, double v) {
 
 struct BsLds {
     double co[BS_OBS][3];
-    double dpl[BS_PTS][3];
+    double xnl[BS_PTS][3];  // the chunk's candidate points x + delta (phase 2 -> phase 3: no point load in phase 3)
     double lds[4 * 5];
     double out[5];
 };
@@ -240,7 +240,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     const bool use_pre = PL != nullptr;
     const bool PRE = use_pre && pre.on;  // (block-uniform)
     auto& co = L.co;
-    auto& dpl = L.dpl;
+    auto& xnl = L.xnl;
     double* const lds = L.lds;
     double* const out = L.out;
     if (skip_step(st)) return;
@@ -301,7 +301,8 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         if (ac >= 0) {
             ObsEval ev;
             double jc[18], jp[9], jk[8];
-            lin_obs(c, P.cams[cur] + 7 * cam, P.pts[cur] + 3 * P.pt_idx[ap], K, ro.u(), ro.v(), ro.d(), ev, jc, jp, jk);
+            // (the point through po_pt, loaded beside the record: one dependent load level less than pt_idx[ap])
+            lin_obs(c, P.cams[cur] + 7 * cam, P.pts[cur] + 3 * P.po_pt[o], K, ro.u(), ro.v(), ro.d(), ev, jc, jp, jk);
             const double* sc = scale + 6 * ac;
             const double* yc = y + 6 * ac;
             const double* sp = scale + P.off_pt + 3 * ap;
@@ -358,7 +359,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
             const double dp = -sp[i] * yp;
             const double xn = X[i] + dp;
             Xn[i] = xn;
-            dpl[tid][i] = dp;
+            xnl[tid][i] = xn;
             const double df = X[i] - xn;
             acc[0] += df * df;
             acc[4] += xn * xn;
@@ -382,8 +383,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         }
         const int cam = ro.idx();
         const int pl = ap - apb;
-        const double* X = PRE ? &PL->pt[pl][PDATA + 3] : P.pts[cur] + 3 * P.pt_idx[ap];
-        const double xn[3] = {X[0] + dpl[pl][0], X[1] + dpl[pl][1], X[2] + dpl[pl][2]};
+        const double xn[3] = {xnl[pl][0], xnl[pl][1], xnl[pl][2]};  // X + delta_p, as phase 2 stored it
         ObsEval en;
         if (CL) {  // the band tail: the chunk's own candidate table (cand_compute)
             eval_obs(c, CL + 8 * cam, xn, CL + 8 * (size_t)P.n_cams, ro.u(), ro.v(), ro.d(), en);

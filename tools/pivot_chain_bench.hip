@@ -8,6 +8,9 @@
 //   3  variant 0 with the trailing updates of columns j + 2.. fed by an LDS broadcast of the multipliers
 //   4  variant 0 with pivot j - 1's trailing updates issued inside pivot j's chain (sched_barrier fences; same L)
 //   5  variant 4 without the fences
+//   6  variant 0 with the trailing updates of columns j + 2.. as one v_fmac_f64_dpp each: the multipliers of lanes
+//      0-15 copied to every 16-lane row (ds_bpermute), then row_newbcast:k hands lane k's l to the FMA (no v_readlane)
+//   7  variant 6 with column j + 1 by DPP as well (only the next pivot's value by v_readlane)
 // Reports ns and shader cycles per pivot and the max |L L^T - A| of the last repetition.
 // build: hipcc --offload-arch=gfx950 -O3 tools/pivot_chain_bench.hip -o /tmp/pcb && /tmp/pcb
 #include <hip/hip_runtime.h>
@@ -32,9 +35,60 @@ __device__ __forceinline__ unsigned long long clk() {
     return t;
 }
 
+// a -= lr[lane K of this lane's 16-lane row] * l  (one v_fmac_f64_dpp; the DPP64 control row_newbcast); NOP: the two
+// wait states a DPP read needs after a VALU write of its source (lr comes from ds_bpermute, but a copy may intervene)
+template <int K, bool NOP>
+__device__ __forceinline__ void fnma_row_bcast(double& a, double lr, double l) {
+    if constexpr (NOP)
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(a) : "v"(lr), "v"(l), "i"(K));
+    else
+        asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(a) : "v"(lr), "v"(l), "i"(K));
+}
+template <int J, int K>
+__device__ __forceinline__ void trail_dpp(double (&a)[16], double lr, double l) {
+    if constexpr (K < 16) {
+        fnma_row_bcast<K, K == J>(a[K], lr, l);
+        trail_dpp<J, K + 1>(a, lr, l);
+    }
+}
+template <int J, int V>
+__device__ __forceinline__ void chain_dpp_step(double (&a)[16], double& my_inv, double& dn) {
+    const int r = threadIdx.x & 63;
+    const double d = dn;
+    const double y = __builtin_amdgcn_rsq(d);
+    const double e = __builtin_fma(-d * y, y, 1.0);
+    const double l = __builtin_fma(0.5 * a[J] * y, e, a[J] * y);
+    my_inv = (r == J) ? __builtin_fma(0.5 * y, e, y) : my_inv;
+    a[J] = l;
+    if constexpr (J < 15) {
+        dn = bcast(__builtin_fma(-l, l, a[J + 1]), J + 1);
+        const double lr = __shfl(l, r & 15);  // row 0's multipliers in every row
+        if constexpr (V == 6) {
+            a[J + 1] = __builtin_fma(-l, bcast(l, J + 1), a[J + 1]);
+            trail_dpp<J + 2, J + 2>(a, lr, l);
+        } else {
+            trail_dpp<J + 1, J + 1>(a, lr, l);
+        }
+    }
+}
+template <int J, int V>
+__device__ __forceinline__ void chain_dpp(double (&a)[16], double& my_inv, double& dn) {
+    if constexpr (J < 16) {
+        chain_dpp_step<J, V>(a, my_inv, dn);
+        chain_dpp<J + 1, V>(a, my_inv, dn);
+    }
+}
+
 template <int V>
 __device__ __forceinline__ void chain(double (&a)[16], double& my_inv, double* lb) {
     const int r = threadIdx.x & 63;
+    if constexpr (V == 6 || V == 7) {
+        double dn = bcast(a[0], 0);
+        chain_dpp<0, V>(a, my_inv, dn);
+        return;
+    }
     if constexpr (V == 3) {
         // the next column by v_readlane (on the chain); columns j + 2.. by an LDS broadcast of the multipliers
         // (lanes 0-15 store l, every lane reads l_k two at a time with uniform-address ds_read_b128): the
@@ -173,7 +227,7 @@ __global__ __launch_bounds__(64) void k_bench(const double* __restrict__ A, doub
     for (int it = 0; it < reps; ++it) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) a[c] = a0[c] + sink * 1e-300;  // depends on the previous repetition
-        if constexpr (V >= 4) chain_pipe<V>(a, my_inv); else chain<V>(a, my_inv, lb);
+        if constexpr (V == 4 || V == 5) chain_pipe<V>(a, my_inv); else chain<V>(a, my_inv, lb);
         sink = bcast(a[15], 63);
     }
     const unsigned long long c1 = clk(), t1 = rt();
@@ -201,16 +255,19 @@ int main() {
     (void)hipMalloc(&dA, 8 * A.size()); (void)hipMalloc(&dL, 8 * A.size()); (void)hipMalloc(&dt, 16);
     (void)hipMemcpy(dA, A.data(), 8 * A.size(), hipMemcpyHostToDevice);
     const int reps = 2000;
-    const char* names[6] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)",
-                            "LDS-broadcast trailing", "deferred trailing, fenced", "deferred trailing, unfenced"};
+    const char* names[8] = {"rsq chain (kernel)", "rcp next-pivot chain", "chain only (lower bound)",
+                            "LDS-broadcast trailing", "deferred trailing, fenced", "deferred trailing, unfenced",
+                            "DPP64 trailing (j+2..)", "DPP64 trailing (j+1..)"};
     for (int round = 0; round < 2; ++round)
-        for (int v = 0; v < 6; ++v) {
+        for (int v = 0; v < 8; ++v) {
             if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 2) hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 3) hipLaunchKernelGGL(k_bench<3>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 4) hipLaunchKernelGGL(k_bench<4>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             if (v == 5) hipLaunchKernelGGL(k_bench<5>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 6) hipLaunchKernelGGL(k_bench<6>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
+            if (v == 7) hipLaunchKernelGGL(k_bench<7>, dim3(1), dim3(64), 0, 0, dA, dL, dt, reps);
             unsigned long long t[2];
             std::vector<double> L(64 * 16);
             (void)hipMemcpy(t, dt, 16, hipMemcpyDeviceToHost);
