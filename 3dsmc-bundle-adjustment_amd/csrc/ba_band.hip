@@ -597,12 +597,30 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
             double w = ((w0 - w1) - w2) - w3;
             const double* Li = Dm + i * GG;
             double yv = 0.0;
-            sfor<0, G>([&](auto Rc) {
-                constexpr int R = G - 1 - decltype(Rc)::value;
-                const double yR = ubc<U, R>(w, hi) * RI[i * G + R];
-                yv = ul == R ? yR : yv;
-                if (ul < R) w = __builtin_fma(-Li[R * G + r], yR, w);
-            });
+            if constexpr (U == 16) {
+                // a 16-lane unit: y_R = w_R / L_RR on lane R, and w_r += w_R (-L_Rr / L_RR) on every lane in ONE
+                // v_fmac_f64_dpp (row_newbcast:R hands lane R's w to the row; the coefficients are loaded and formed
+                // first, off the chain) — one dependent instruction per step instead of the broadcast, the product and
+                // the FMA. (Lanes >= R take updates they never read again.)
+                double rv[G], cf[G];
+                sfor<0, G>([&](auto Rc) {
+                    constexpr int R = decltype(Rc)::value;
+                    rv[R] = RI[i * G + R];
+                    cf[R] = -Li[R * G + r] * rv[R];
+                });
+                sfor<0, G>([&](auto Rc) {
+                    constexpr int R = G - 1 - decltype(Rc)::value;
+                    yv = ul == R ? w * rv[R] : yv;
+                    if constexpr (R > 0) fmac_self_row_bcast<R>(w, cf[R]);
+                });
+            } else {
+                sfor<0, G>([&](auto Rc) {
+                    constexpr int R = G - 1 - decltype(Rc)::value;
+                    const double yR = ubc<U, R>(w, hi) * RI[i * G + R];
+                    yv = ul == R ? yR : yv;
+                    if (ul < R) w = __builtin_fma(-Li[R * G + r], yR, w);
+                });
+            }
             if (act && ul < G) YV[i * G + ul] = yv;
         }
         __syncthreads();

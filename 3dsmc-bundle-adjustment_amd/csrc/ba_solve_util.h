@@ -108,6 +108,14 @@ __device__ __forceinline__ void fnma_row_bcast(double& a, double lr, double l) {
         asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(a) : "v"(lr), "v"(l), "i"(K));
 }
 
+// w += w[lane K of this lane's 16-lane row] * c (one v_fmac_f64_dpp reading its own destination through row_newbcast);
+// the two wait states first: w was written by the VALU instruction just before (the previous step of the caller's chain)
+template <int K>
+__device__ __forceinline__ void fmac_self_row_bcast(double& w, double c) {
+    static_assert(K >= 0 && K < 16, "row_newbcast selects a lane of the 16-lane row");
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(c), "i"(K));
+}
+
 // 4x4 border system (C - sum B^T V) y_k = b_k - sum B^T u on one thread: bk = [b_k | S_kk lower packed],
 // red[m * 5 + c] = (B^T [u | V])[m][c]. bad: a non-positive pivot (replaced by 1).
 __device__ __forceinline__ void border_solve4(const double* bk, const double* red, double* yk, bool& bad) {
