@@ -234,76 +234,108 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
     // last camera dof. Cameras: their step operands (the pose after the camera index), on the threads from the top.
     const int nrow = nb * G;
     {
-        // the 2G doubles of S row dr at columns (j - 1) G .. j G + G - 1, element e = 2G dr + cc: consecutive threads
-        // read consecutive columns (a thread per row read 2G lines per wave and instruction: 4.2 us at C3)
+        // The 2G doubles of S row dr at columns (j - 1) G .. j G + G - 1, element e = 2G dr + cc: consecutive threads
+        // read consecutive columns (a thread per row read 2G lines per wave and instruction: 4.2 us at C3). The first
+        // pass of these, this thread's border row and rhs entry, its camera's step operands and its bk / intrinsics
+        // operand are ALL loaded before any is stored to LDS: one memory round trip for the load phase instead of one
+        // per loop (each loop waited for its own loads); larger windows' further passes / rows / cameras follow.
         constexpr int NL = 8;
         const int ne2 = nrow * 2 * G;
-        for (int e0 = 0; e0 < ne2; e0 += NL * TPB) {
-            double v[NL];
-#pragma unroll
-            for (int q = 0; q < NL; ++q) {
-                const int e = e0 + q * TPB + tid;
+        auto s_load = [&](int e) {
+            const int dr = e / (2 * G), cc = e - dr * (2 * G), j = dr / G, r = dr - j * G;
+            const int col = (j - 1) * G + cc;
+            const bool okc = e < ne2 && dr < ncd && col >= 0 && (cc < G || cc - G <= r);
+            const double v = S[okc ? (size_t)dr * ld + col : 0];
+            return okc ? v : ((e < ne2 && dr >= ncd && cc - G == r) ? 1.0 : 0.0);  // identity past the dofs
+        };
+        auto s_store = [&](int e, double v) {
+            if (e < ne2) {
                 const int dr = e / (2 * G), cc = e - dr * (2 * G), j = dr / G, r = dr - j * G;
-                const int col = (j - 1) * G + cc;
-                const bool okc = e < ne2 && dr < ncd && col >= 0 && (cc < G || cc - G <= r);
-                v[q] = S[okc ? (size_t)dr * ld + col : 0];
-                v[q] = okc ? v[q] : ((e < ne2 && dr >= ncd && cc - G == r) ? 1.0 : 0.0);  // identity past the dofs
+                lds[(cc < G ? Ly.CL : Ly.D) + j * GG + r * G + (cc < G ? cc : cc - G)] = v;
             }
+        };
+        // border entries S[kb + k][dr] and rhs[dr] (coalesced over dr)
+        auto b_load = [&](int dr, double (&bb)[5]) {
+            const bool ok = dr < ncd;
 #pragma unroll
-            for (int q = 0; q < NL; ++q) {
-                const int e = e0 + q * TPB + tid;
-                if (e < ne2) {
-                    const int dr = e / (2 * G), cc = e - dr * (2 * G), j = dr / G, r = dr - j * G;
-                    lds[(cc < G ? Ly.CL : Ly.D) + j * GG + r * G + (cc < G ? cc : cc - G)] = v[q];
-                }
+            for (int k = 0; k < 4; ++k) bb[k] = S[(size_t)(ncd + k) * ld + (ok ? dr : 0)];
+            bb[4] = rhs[ok ? dr : 0];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) bb[k] = ok ? bb[k] : 0.0;
+        };
+        auto b_store = [&](int dr, const double (&bb)[5]) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) BBm[dr * 4 + k] = bb[k];
+            BV[dr] = bb[4];
+        };
+        // the cameras' step operands (load_cam_step_ops), on the threads from the top
+        auto c_load = [&](int t, double (&o)[18]) {
+            const double* cd = camdata + (size_t)t * CAMDATA;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                o[k] = scale[6 * (size_t)t + k];
+                o[6 + k] = cd[k * 6 - (k * (k - 1)) / 2];
+                o[12 + k] = cd[45 + k];
             }
-        }
-    }
-    for (int dr = tid; dr < nrow; dr += TPB) {  // border entries S[kb + k][dr] and rhs[dr] (coalesced over dr)
-        const bool ok = dr < ncd;
-        double bb[4];
+            return P.ac_cam[t];
+        };
+        auto c_store = [&](int t, const double (&o)[18], int cam) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            bb[k] = S[(size_t)(ncd + k) * ld + (ok ? dr : 0)];
-            bb[k] = ok ? bb[k] : 0.0;
-        }
-        double bv = rhs[ok ? dr : 0];
-        bv = ok ? bv : 0.0;
+            for (int k = 0; k < 18; ++k) lds[Ly.OPS + t * BAND_OPS + k] = o[k];
+            AC[t] = cam;
+        };
+        double v[NL];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) BBm[dr * 4 + k] = bb[k];
-        BV[dr] = bv;
-    }
-    for (int t = TPB - 1 - tid; t < nac; t += TPB) {  // the cameras' step operands (load_cam_step_ops)
-        const int cam = P.ac_cam[t];
-        const double* cd = camdata + (size_t)t * CAMDATA;
-        double o[18];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            o[k] = scale[6 * (size_t)t + k];
-            o[6 + k] = cd[k * 6 - (k * (k - 1)) / 2];
-            o[12 + k] = cd[45 + k];
+        for (int q = 0; q < NL; ++q) v[q] = s_load(q * TPB + tid);
+        const bool hb = tid < nrow;
+        double bb0[5];
+        b_load(hb ? tid : 0, bb0);
+        const int t0 = TPB - 1 - tid;
+        const bool hc = t0 < nac;
+        double o0[18];
+        const int cam0 = c_load(hc ? t0 : 0, o0);
+        // bk = [b_k | S_kk lower packed] (14) | intrinsics' step operands (20)
+        const bool hk = tid >= TPB / 2 && tid < TPB / 2 + 34;
+        double kv = 0.0;
+        int kdst = 0;
+        if (hk) {
+            const int f = tid - TPB / 2;
+            const double* p;
+            size_t idx;
+            if (f < 4) {
+                p = rhs; idx = ncd + f; kdst = Ly.BK + f;
+            } else if (f < 14) {
+                const int q2 = f - 4, mm = q2 < 1 ? 0 : q2 < 3 ? 1 : q2 < 6 ? 2 : 3, l = q2 - mm * (mm + 1) / 2;
+                p = S; idx = (size_t)(ncd + mm) * ld + ncd + l; kdst = Ly.BK + f;
+            } else {
+                const int g = f - 14, kind = g >> 2, m = g & 3;
+                p = kind == 0 ? P.K[cur] : kind == 1 ? scale : kind == 4 ? P.prior : lin;
+                idx = kind == 0 ? m : kind == 1 ? P.off_k + m : kind == 2 ? 2 + 4 * m - (m * (m - 1)) / 2 : kind == 3 ? 12 + m : m;
+                kdst = Ly.IOPS + g;
+            }
+            kv = p[idx];
         }
 #pragma unroll
-        for (int k = 0; k < 18; ++k) lds[Ly.OPS + t * BAND_OPS + k] = o[k];
-        AC[t] = cam;
-    }
-    if (tid >= TPB / 2 && tid < TPB / 2 + 34) {  // bk = [b_k | S_kk lower packed] (14) | intrinsics' step operands (20)
-        const int f = tid - TPB / 2;
-        const double* p;
-        size_t idx;
-        int dst;
-        if (f < 4) {
-            p = rhs; idx = ncd + f; dst = Ly.BK + f;
-        } else if (f < 14) {
-            const int q2 = f - 4, mm = q2 < 1 ? 0 : q2 < 3 ? 1 : q2 < 6 ? 2 : 3, l = q2 - mm * (mm + 1) / 2;
-            p = S; idx = (size_t)(ncd + mm) * ld + ncd + l; dst = Ly.BK + f;
-        } else {
-            const int g = f - 14, kind = g >> 2, m = g & 3;
-            p = kind == 0 ? P.K[cur] : kind == 1 ? scale : kind == 4 ? P.prior : lin;
-            idx = kind == 0 ? m : kind == 1 ? P.off_k + m : kind == 2 ? 2 + 4 * m - (m * (m - 1)) / 2 : kind == 3 ? 12 + m : m;
-            dst = Ly.IOPS + g;
+        for (int q = 0; q < NL; ++q) s_store(q * TPB + tid, v[q]);
+        if (hb) b_store(tid, bb0);
+        if (hc) c_store(t0, o0, cam0);
+        if (hk) lds[kdst] = kv;
+        for (int e0 = NL * TPB; e0 < ne2; e0 += NL * TPB) {
+#pragma unroll
+            for (int q = 0; q < NL; ++q) v[q] = s_load(e0 + q * TPB + tid);
+#pragma unroll
+            for (int q = 0; q < NL; ++q) s_store(e0 + q * TPB + tid, v[q]);
         }
-        lds[dst] = p[idx];
+        for (int dr = tid + TPB; dr < nrow; dr += TPB) {
+            double bb[5];
+            b_load(dr, bb);
+            b_store(dr, bb);
+        }
+        for (int t = t0 + TPB; t < nac; t += TPB) {
+            double o[18];
+            const int cam = c_load(t, o);
+            c_store(t, o, cam);
+        }
     }
     if (skip) return;
     const double radius = st->radius;

@@ -193,6 +193,14 @@ __device__ inline double intr_lin(const DevProblem& P, const BaConsts& c, const 
 // Point tail of the Schur preparation, from the point's sums acc = V packed (6) | e (3) | Kt (12):
 // gradient max-norm term, scaled + LM-damped V~, G = chol(V~)^-1, e~, K~, D~ -> rec[PDATA]; with
 // want_kk also the intrinsics Schur terms -Zk Zk^T (10 packed), -Zk ze (4) -> kk.
+// 1/sqrt(x) to full f64 precision: v_rsq_f64 + two Newton steps
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = y * (1.5 - 0.5 * x * y * y);
+    y = y * (1.5 - 0.5 * x * y * y);
+    return y;
+}
+
 __device__ __forceinline__ void point_tail(const DevProblem& P, const BaConsts& c, double radius,
                                            const double* __restrict__ scale, int ap, const double* X,
                                            const double* acc, bool want_kk, double* rec, double* kk, double& gmax,
@@ -218,16 +226,17 @@ __device__ __forceinline__ void point_tail(const DevProblem& P, const BaConsts& 
     // V~ = L L^T ; G = L^-1 (lower), V~^-1 = G^T G
 #pragma unroll
     for (int i = 0; i < 6; ++i) rec[i] = 0.0;  // g00 g10 g11 g20 g21 g22
+    // the pivots' reciprocal square roots by v_rsq_f64 + two Newton steps (rsqrt_nr) instead of IEEE square roots
+    // and divisions: ~40 dependent operations on the point's chain instead of ~80
     const bool pd = v00 > 0.0;
-    const double L00 = sqrt(v00);
-    const double L10 = v01 / L00, L20 = v02 / L00;
+    const double i00 = rsqrt_nr(v00);  // 1 / L00
+    const double L10 = v01 * i00, L20 = v02 * i00;
     const double l11 = v11 - L10 * L10;
-    const double L11 = sqrt(l11);
-    const double L21 = (v12 - L20 * L10) / L11;
+    const double i11 = rsqrt_nr(l11);
+    const double L21 = (v12 - L20 * L10) * i11;
     const double l22 = v22 - L20 * L20 - L21 * L21;
-    const double L22 = sqrt(l22);
+    const double i22 = rsqrt_nr(l22);
     if (pd && l11 > 0.0 && l22 > 0.0 && isfinite(l22)) {
-        const double i00 = 1 / L00, i11 = 1 / L11, i22 = 1 / L22;
         rec[0] = i00;
         rec[1] = -L10 * i00 * i11;
         rec[2] = i11;
@@ -270,14 +279,6 @@ __device__ __forceinline__ double bcast(double v, int l) {
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
     return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
-// 1/sqrt(x) to full f64 precision: v_rsq_f64 + two Newton steps
-__device__ __forceinline__ double rsqrt_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    y = y * (1.5 - 0.5 * x * y * y);
-    y = y * (1.5 - 0.5 * x * y * y);
-    return y;
 }
 
 // In-register 16x16 Cholesky by one wave: lane r (r < 16; replicated above) holds row r.
