@@ -840,10 +840,10 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
         flush_marks();
         return;
     }
-    // the final workgroup: every chunk of this launch has counted itself, and the solve's camera step is published
+    // the final workgroup: the solve's camera step is published; the chunks' partials are polled in final_body
+    // (POLL: flag-free slots, no count on this path)
     if (tid == 0) {
-        ok_s = (skip || (tail_wait(tflags + 1, seq * (unsigned)nb_bs, g_tail_spin_limit) &&
-                         tail_wait(tflags + 2, seq, g_tail_spin_limit))) ? 1 : 0;
+        ok_s = (skip || tail_wait(tflags + 2, seq, g_tail_spin_limit)) ? 1 : 0;
         if (!ok_s) {
             raise_flag(flag, FLAG_TIMEOUT);
             (void)tail_wait(tflags + 1, seq * (unsigned)nb_bs, BOUND);  // every chunk done before rhs is zeroed
@@ -852,8 +852,9 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
     }
     __syncthreads();
     mark(2);
-    final_body<2, true>(P, st, nb_pt, nb_upd, nb_bs, part, flag, scal, prm, lin, log, rhs, nullptr,
-                        *reinterpret_cast<FinLds*>(lds), STAMP ? tl + TAIL_ST0 + 16 * b + 5 : nullptr);
+    final_body<2, true, true>(P, st, nb_pt, nb_upd, nb_bs, part, flag, scal, prm, lin, log, rhs, nullptr,
+                              *reinterpret_cast<FinLds*>(lds), STAMP ? tl + TAIL_ST0 + 16 * b + 5 : nullptr,
+                              TailPoll{ok_s ? g_tail_spin_limit : 0u, tflags + 1, seq * (unsigned)nb_bs});
     mark(3);
     flush_marks();
 }

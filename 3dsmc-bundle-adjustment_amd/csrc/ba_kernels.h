@@ -52,7 +52,10 @@ enum {
     PART_BS_XN2,
     PART_INIT_XN2,
     PART_PT_KK,                     // 14 slots: intrinsics Schur terms of k_point_prep (10 packed + 4)
-    PART_NSLOTS = PART_PT_KK + 14
+    // 5 slots: the band tail's back-substitution partials (sn2, mcc, cost, bad, |x_cand|^2), handed to its decision
+    // workgroup flag-free — an empty slot holds BCR_Y_EMPTY (set at prepare, re-set by the decision after reading)
+    PART_TAIL = PART_PT_KK + 14,
+    PART_NSLOTS = PART_TAIL + 5
 };
 // final scalars
 enum { SC_MCC = 0, SC_CAND, SC_SN2, SC_GMAX_PT, SC_BAD, SC_XN2, SC_N = 8 };

@@ -626,6 +626,14 @@ static int upload_params(ba_context* ctx, const ba_problem* p, hipStream_t s) {
     return BA_OK;
 }
 
+// The band tail's flag-free partial slots (PART_TAIL, ba_kernels.h) start empty: the BCR_Y_EMPTY pattern in every
+// double (its two 32-bit halves are equal, so one 32-bit fill)
+static hipError_t empty_tail_slots(double* part, int stride, hipStream_t s) {
+    static_assert((BCR_Y_EMPTY >> 32) == (BCR_Y_EMPTY & 0xffffffffull), "a 32-bit fill writes the pattern");
+    return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(part + (size_t)PART_TAIL * stride), (int)BCR_Y_EMPTY_D32,
+                             2 * 5 * (size_t)stride, s);
+}
+
 // The MIBA_* settings ba_prepare reads (layout / solver choices): part of the plan cache key.
 static unsigned long long env_key() {
     static const char* const names[] = {"MIBA_OBS32", "MIBA_TILE_PTS", "MIBA_SUBSEG", "MIBA_SOLVER", "MIBA_DENSE_CHOL",
@@ -738,6 +746,7 @@ static int prepare_reuse(ba_context* ctx, const ba_problem* p, double tp0) {
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_S].p, 0, sizeof(double) * (size_t)P.npad * P.npad, s));
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_RHS].p, 0, sizeof(double) * P.npad, s));
     HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * P.part_stride, s));
+    HIPCHECK(ctx, empty_tail_slots(ctx->buf[B_PART].as<double>(), P.part_stride, s));
     if (P.solver == 2 && ctx->bcr_fallback)
         if (int rc = bcr_setup(ctx)) return rc;
     // a hand-off timeout cleared the small-window launch for the rest of that solve: the next one takes the path
@@ -1181,6 +1190,7 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
         HIPCHECK(ctx, ctx->buf[B_STATE].ensure(sizeof(LmState)));
         HIPCHECK(ctx, ctx->buf[B_LOG].ensure(sizeof(double) * LOG_W * (std::max(o.max_num_iterations, 0) + 2)));
         HIPCHECK(ctx, hipMemsetAsync(ctx->buf[B_PART].p, 0, sizeof(double) * PART_NSLOTS * part_stride, s));
+        HIPCHECK(ctx, empty_tail_slots(ctx->buf[B_PART].as<double>(), part_stride, s));
 
         DevProblem& P = ctx->P;
         P.cams[0] = ctx->buf[B_CAMS0].as<double>(); P.cams[1] = ctx->buf[B_CAMS1].as<double>();

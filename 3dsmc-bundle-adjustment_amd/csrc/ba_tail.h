@@ -406,7 +406,10 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     bmark(3);
     if (tid == 0) {
         const double pv[5] = {out[0], out[1], out[2], out[3] > 0.0 ? 1.0 : 0.0, out[4]};
-        const int slot[5] = {PART_BS_SN2, PART_BS_MCC, PART_BS_COST, PART_BS_BAD, PART_BS_XN2};
+        // (the band tail, PUB: the decision workgroup polls these slots for its values — no count on its path)
+        const int slot[5] = {PUB ? PART_TAIL : PART_BS_SN2, PUB ? PART_TAIL + 1 : PART_BS_MCC,
+                             PUB ? PART_TAIL + 2 : PART_BS_COST, PUB ? PART_TAIL + 3 : PART_BS_BAD,
+                             PUB ? PART_TAIL + 4 : PART_BS_XN2};
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             double* q = part + slot[k] * P.part_stride + ch;
@@ -449,13 +452,24 @@ struct FinLds {
     double out[4];
     double red[NW_F];
 };
-template <int UNR, bool PUB = false>
+// The band tail's decision (POLL): the back-substitution chunks' partials are not counted and then loaded — each
+// thread polls its chunks' PART_TAIL slots until they hold values (flag-free: an empty slot holds BCR_Y_EMPTY, which no
+// f64 arithmetic produces), so the reduction starts one store-to-load hop after the last chunk's store instead of a
+// drain, a count, a poll of the count and a load round trip; then it empties the slots for the next launch. A poll
+// past the spin bound raises FLAG_TIMEOUT (the iteration is re-run with the separate launches) and waits for the
+// chunks' count (every chunk done) before anything is emptied or zeroed.
+struct TailPoll {
+    unsigned lim;            // polls before the timeout
+    const unsigned* count;   // the chunks' count word
+    unsigned target;         // its value once every chunk of this launch has counted
+};
+template <int UNR, bool PUB = false, bool POLL = false>
 __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restrict__ st, int nblk_pt, int nblk_upd,
                                            int nblk_bs, const double* __restrict__ part,
                                            const int* __restrict__ chol_flag, double* __restrict__ scal,
                                            const LmParams& prm, const double* __restrict__ lin, double* __restrict__ log,
                                            double* __restrict__ rhs_z, unsigned* __restrict__ bcr_epoch, FinLds& L,
-                                           unsigned long long* __restrict__ fst = nullptr) {
+                                           unsigned long long* __restrict__ fst = nullptr, TailPoll tp = TailPoll{}) {
     double* const lds = L.lds;
     double* const out = L.out;
     double* const red = L.red;
@@ -467,8 +481,9 @@ __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restr
     double lin0 = 0.0, lin1 = 0.0;
     if (threadIdx.x == 0) {
         S0 = *st;
-        cf = PUB ? __hip_atomic_load(const_cast<int*>(chol_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                 : *chol_flag;
+        if constexpr (!POLL)  // (POLL: after the chunks' partials, which follow any chunk's timeout flag)
+            cf = PUB ? __hip_atomic_load(const_cast<int*>(chol_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : *chol_flag;
         lin0 = lin[0];
         lin1 = lin[1];
     }
@@ -483,6 +498,57 @@ __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restr
         acc[2] += LD(part + PART_UPD_COST * stp + i);
         acc[3] += LD(part + PART_UPD_XN2 * stp + i);
     }
+    if constexpr (POLL) {
+        // (skip_step: the chunks stored nothing; the partials are not read)
+        const bool skip = done || __builtin_amdgcn_readfirstlane(st->stop_next);
+        bool ok = true;
+        for (int i = threadIdx.x; i < nblk_bs && !skip; i += TPB_F) {
+            unsigned long long u[5];
+            const unsigned long long* q[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) q[k] = reinterpret_cast<const unsigned long long*>(part + (PART_TAIL + k) * stp + i);
+            for (unsigned n = 0;; ++n) {
+                bool pend = false;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    u[k] = __hip_atomic_load(const_cast<unsigned long long*>(q[k]), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                    pend = pend || u[k] == BCR_Y_EMPTY;
+                }
+                if (!pend) break;
+                if (n >= tp.lim) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) break;
+            acc[0] += __longlong_as_double((long long)u[0]);
+            acc[1] += __longlong_as_double((long long)u[1]);
+            acc[2] += __longlong_as_double((long long)u[2]);
+            acc[3] += __longlong_as_double((long long)u[4]);
+            bad = fmax(bad, __longlong_as_double((long long)u[3]));
+        }
+        __shared__ int fin_ok;
+        if (threadIdx.x == 0) fin_ok = 1;
+        __syncthreads();
+        if (!ok) fin_ok = 0;
+        __syncthreads();
+        if (!fin_ok && threadIdx.x == 0) {
+            raise_flag(const_cast<int*>(chol_flag), FLAG_TIMEOUT);
+            for (unsigned n = 0; n < (1u << 26); ++n) {  // every chunk done before the slots are emptied, rhs zeroed
+                if (__hip_atomic_load(const_cast<unsigned*>(tp.count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                    tp.target)
+                    break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (!fin_ok) __syncthreads();
+        if (!skip)  // the slots empty again for the next launch (its chunks store after this launch has ended)
+            for (int i = threadIdx.x; i < nblk_bs; i += TPB_F)
+#pragma unroll
+                for (int k = 0; k < 5; ++k) tail_st(const_cast<double*>(part) + (PART_TAIL + k) * stp + i,
+                                                    __longlong_as_double((long long)BCR_Y_EMPTY));
+        if (threadIdx.x == 0)
+            cf = __hip_atomic_load(const_cast<int*>(chol_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
 #pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_bs; i += TPB_F) {
         acc[0] += LD(part + PART_BS_SN2 * stp + i);
@@ -490,6 +556,7 @@ __device__ __forceinline__ void final_body(const DevProblem& P, LmState* __restr
         acc[2] += LD(part + PART_BS_COST * stp + i);
         acc[3] += LD(part + PART_BS_XN2 * stp + i);
         bad = fmax(bad, LD(part + PART_BS_BAD * stp + i));
+    }
     }
 #pragma unroll UNR
     for (int i = threadIdx.x; i < nblk_pt; i += TPB_F) {
