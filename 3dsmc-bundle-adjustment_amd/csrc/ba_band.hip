@@ -185,7 +185,8 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
                                           const double* __restrict__ camdata, const double* __restrict__ lin,
                                           double* __restrict__ delta, double* __restrict__ part, int nb,
                                           unsigned long long* __restrict__ tl, double* __restrict__ lds,
-                                          unsigned* __restrict__ yflag = nullptr, unsigned yseq = 0) {
+                                          unsigned* __restrict__ yflag = nullptr, unsigned yseq = 0,
+                                          double* __restrict__ ybuf = nullptr) {
     constexpr int G = 6 * BC;
     constexpr int GG = G * G;
     constexpr int TPB = BAND_TPB, NW = BAND_TPB / 64;
@@ -660,7 +661,8 @@ __device__ __forceinline__ void band_body(const LmState* __restrict__ st, const 
     stamp();  // 2K + 4: back-substitution
     // ---- y to rhs (the points' back-substitution reads it); the step (block_step's arithmetic and grouping: wave w =
     // cameras [10 w, 10 w + 10), w = 0 also the intrinsics; part slot w)
-    for (int d = tid; d < ncd + 4; d += TPB) st_opt<PUB>(rhs + d, d < ncd ? YV[d] : yk[d - ncd]);
+    // (the band tail: y to its flag-free hand-off buffer, which the chunks poll; else to rhs)
+    for (int d = tid; d < ncd + 4; d += TPB) st_opt<PUB>((ybuf ? ybuf : rhs) + d, d < ncd ? YV[d] : yk[d - ncd]);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int e = tid + q * TPB;
@@ -767,7 +769,8 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
                                                         const int2* __restrict__ ztiles, int n_ztiles, int nb_bs,
                                                         int nb_pt, int nb_upd, double* __restrict__ scal,
                                                         double* __restrict__ log, unsigned* __restrict__ tflags,
-                                                        unsigned seq, unsigned long long* __restrict__ tl) {
+                                                        unsigned seq, unsigned long long* __restrict__ tl,
+                                                        double* __restrict__ tail_y) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int ok_s;
     LmState* const st = const_cast<LmState*>(st_c);
@@ -780,11 +783,18 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
         if constexpr (STAMP) if (tid == 0) for (int k = 0; k < 5; ++k) tl[TAIL_ST0 + 16 * b + k] = tst[k];
     };
     mark(0);
+    // y of this launch in buffer (seq & 1) of tail_y; the other one (this launch's successor's) is emptied by the solve
+    double* const ybuf = tail_y + (size_t)(seq & 1u) * P.npad;
     if (b == 0) {
+        {  // the next launch's y buffer: read by the previous launch's chunks, which have all finished
+            double* const ynext = tail_y + (size_t)((seq + 1u) & 1u) * P.npad;
+            for (int d = tid; d < P.npad; d += BAND_TPB) tail_st(ynext + d, __longlong_as_double((long long)BCR_Y_EMPTY));
+        }
         // y, the candidate cameras and intrinsics, the step and the partials are stored past the L2 (PUB) and
         // drained by every thread before the count: no L2 write-back fence on the critical path (the consumers
         // read them with agent-scope loads)
-        band_body<BC, STAMP, true>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, tl, lds, tflags, seq);
+        band_body<BC, STAMP, true>(st, P, S, rhs, flag, c, scale, camdata, lin, delta, part, nb, tl, lds, tflags, seq,
+                                   ybuf);
         mark(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -810,19 +820,36 @@ __global__ __launch_bounds__(BAND_TPB) void k_band_tail(const LmState* __restric
     // touches S or rhs, which the re-run assembles onto
     constexpr unsigned BOUND = 1u << 26;
     if (b <= nb_bs) {
-        if (tid == 0) {
-            ok_s = skip ? 1 : (tail_wait(tflags, seq, g_tail_spin_limit) ? 1 : 0);
-            if (!ok_s) {
-                raise_flag(flag, FLAG_TIMEOUT);
-                (void)tail_wait(tflags, seq, BOUND);
+        // y polled straight from its hand-off buffer into this chunk's LDS (flag-free: every value is the solve's f64
+        // arithmetic, an unwritten one BCR_Y_EMPTY) — one store-to-load hop instead of the flag's and then y's
+        double* const yl = CL + cand_lds_doubles(P.n_cams, P.nac);
+        bool yok = true;
+        if (!skip)
+            for (int d = tid; d < P.kb + 4; d += 256) {
+                const unsigned long long* q = reinterpret_cast<const unsigned long long*>(ybuf + d);
+                unsigned long long u = 0;
+                for (unsigned n = 0;; ++n) {
+                    u = __hip_atomic_load(const_cast<unsigned long long*>(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (u != BCR_Y_EMPTY) break;
+                    if (n >= g_tail_spin_limit) { yok = false; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (!yok) break;
+                yl[d] = __longlong_as_double((long long)u);
             }
-        }
+        if (tid == 0) ok_s = 1;
         __syncthreads();
+        if (!yok) ok_s = 0;
+        __syncthreads();
+        if (!ok_s && tid == 0) {
+            raise_flag(flag, FLAG_TIMEOUT);
+            (void)tail_wait(tflags, seq, BOUND);  // (the solve's y flag: it has run before S or rhs is touched)
+        }
         mark(2);
         if (ok_s) {
-            backsub_body<O32, true>(P, c, st, scale, pdata, rhs, delta, part, ztiles, n_ztiles, S, b - 1, nb_bs,
-                                    *reinterpret_cast<BsLds*>(lds), pre, pl, CL,
-                                    STAMP ? tl + TAIL_ST0 + 16 * b + 8 : nullptr);
+            backsub_body<O32, true, true, true>(P, c, st, scale, pdata, yl, delta, part, ztiles, n_ztiles, S, b - 1,
+                                                nb_bs, *reinterpret_cast<BsLds*>(lds), pre, pl, CL,
+                                                STAMP ? tl + TAIL_ST0 + 16 * b + 8 : nullptr);
         } else if (tid == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flag) drained before the count
         }
@@ -1002,9 +1029,9 @@ static hipError_t launch_band_t(const DevProblem& P, const BaConsts& c, DevWork&
     return hipGetLastError();
 }
 
-// the chunks' and the decision's dynamic LDS: BsLds | BsPreLds | the candidate table (cand_lds_doubles); FinLds
+// the chunks' and the decision's dynamic LDS: BsLds | BsPreLds | the candidate table (cand_lds_doubles) | y; FinLds
 static size_t tail_role_lds(const DevProblem& P) {
-    return std::max(sizeof(BsLds) + sizeof(BsPreLds) + sizeof(double) * cand_lds_doubles(P.n_cams, P.nac),
+    return std::max(sizeof(BsLds) + sizeof(BsPreLds) + sizeof(double) * (cand_lds_doubles(P.n_cams, P.nac) + P.kb + 4),
                     sizeof(FinLds));
 }
 
@@ -1042,7 +1069,7 @@ static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const Lm
         CKD(hipMemsetAsync(dst, 0, nst * sizeof(unsigned long long), s));
         hipLaunchKernelGGL((k_band_tail<BC, O32, true>), dim3(nb_bs + 2), dim3(BAND_TPB), lds, s, W.st, P, c, prm, W.S,
                            W.rhs, W.chol_flag, W.scale, W.camdata, W.lin, W.delta, W.part, nb, W.pdata, W.env_tile,
-                           W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq, dst);
+                           W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq, dst, W.tail_y);
         CKD(hipGetLastError());
         std::vector<unsigned long long> h(nst);
         CKD(hipMemcpyAsync(h.data(), dst, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1087,7 +1114,7 @@ static hipError_t launch_tail_t(const DevProblem& P, const BaConsts& c, const Lm
     hipLaunchKernelGGL((k_band_tail<BC, O32>), dim3(nb_bs + 2), dim3(BAND_TPB), lds, s, W.st, P, c, prm, W.S, W.rhs,
                        W.chol_flag, W.scale, W.camdata, W.lin, W.delta, W.part, nb, W.pdata, W.env_tile,
                        W.fused ? W.n_env : 0, nb_bs, nb_pt, nb_upd, W.scal, W.log, W.tail_flags, W.tail_seq,
-                       (unsigned long long*)nullptr);
+                       (unsigned long long*)nullptr, W.tail_y);
     if (pf) pf->end(s);
     return hipGetLastError();
 }

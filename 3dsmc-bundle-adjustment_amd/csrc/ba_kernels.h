@@ -371,6 +371,10 @@ struct DevWork {
     int bsfin = 0;
     unsigned* tail_flags = nullptr;
     unsigned tail_seq = 0;
+    // the band tail's y, handed to its back-substitution chunks flag-free: buffer (tail_seq & 1) of two npad-double
+    // buffers, an unwritten value holding BCR_Y_EMPTY; the solve workgroup empties the other buffer (read by the
+    // previous launch) for the next launch, launch_reset empties both at a solve's start
+    double* tail_y = nullptr;
 };
 
 // kernel ids for per-launch HIP-event profiling (ba_kernel_stats)

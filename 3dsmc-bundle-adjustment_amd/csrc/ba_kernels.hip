@@ -2561,6 +2561,8 @@ hipError_t launch_reset(const DevProblem& P, DevWork& W, const LmState& st0, con
     W.sw_seq = 0;
     if (W.tail_flags) CK(hipMemsetAsync(W.tail_flags, 0, 3 * sizeof(unsigned), s));  // the band tail's hand-offs
     W.tail_seq = 0;
+    if (W.tail_y)  // both y buffers empty (the pattern's two 32-bit halves are equal)
+        CK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(W.tail_y), (int)BCR_Y_EMPTY_D32, 2 * 2 * (size_t)P.npad, s));
     const int ncd = 7 * n_cams, npd = 3 * n_points;
     // fused path: S (npad^2, even: npad is a multiple of 16) and rhs are zeroed here too
     const size_t nS2 = W.fused ? (size_t)P.npad * P.npad / 2 : 0;

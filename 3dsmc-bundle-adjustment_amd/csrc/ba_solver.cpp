@@ -65,7 +65,7 @@ enum BufId {
     B_CAMDATA, B_SEGINTR, B_LIN, B_SCALE, B_CNP, B_PDATA, B_S, B_RHS, B_DELTA, B_PART, B_SCAL, B_FLAG,
     B_BCR, B_CAMDATA_LOC, B_ENV_LOC, B_RED, B_PREP, B_CAMPART, B_STATE, B_LOG, B_CAMS_INIT, B_PTS_INIT, B_K_INIT,
     B_DBG0, B_DBG1, B_DBG2, B_DBG3, B_DET_TBUF, B_PO_REC, B_CO_REC,
-    B_RAW_ADM, B_DP_SCRATCH, B_DP_PO_DEST, B_DP_CO_DEST, B_DP_CAM_AC, B_DP_PT_IDX, B_DP_OVF, B_DP_SUM,
+    B_RAW_ADM, B_DP_SCRATCH, B_DP_PO_DEST, B_DP_CO_DEST, B_DP_CAM_AC, B_DP_PT_IDX, B_DP_OVF, B_DP_SUM, B_TAIL_Y,
     B_COUNT
 };
 
@@ -1349,6 +1349,12 @@ static int prepare_core(ba_context* ctx, const ba_problem* p, bool force_det) {
             W.bsfin = (!W.tail && W.fused && !shard && !W.det_tbuf && n_ap > 0 && P.n_bs_chunks > 0 &&
                        (e5 && e5[0] == '1')) ? 1 : 0;
             W.tail_flags = reinterpret_cast<unsigned*>(ctx->buf[B_FLAG].as<int>() + 4);
+            // the band tail's y hand-off: two npad-double buffers by launch parity (flag-free, emptied by launch_reset)
+            W.tail_y = nullptr;
+            if (W.tail) {
+                HIPCHECK(ctx, ctx->buf[B_TAIL_Y].ensure(sizeof(double) * 2 * (size_t)P.npad));
+                W.tail_y = ctx->buf[B_TAIL_Y].as<double>();
+            }
             W.tail_seq = 0;
             HIPCHECK(ctx, hipMemsetAsync(W.tail_flags, 0, 3 * sizeof(unsigned), s));
             const char* e2 = std::getenv("MIBA_SW");

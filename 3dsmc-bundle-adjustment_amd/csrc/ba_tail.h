@@ -162,6 +162,8 @@ __device__ __forceinline__ void cand_prefetch(const DevProblem& P, const LmState
     for (int e = threadIdx.x; e < 6 * P.nac; e += TPB) sc[e] = scale[e];
 }
 // after the wait (y published): the candidate poses / intrinsics in place; the caller's next barrier publishes them
+// (YL: y is the chunk's LDS copy, plain loads; else y in memory, read past the L2)
+template <bool YL = false>
 __device__ __forceinline__ void cand_compute(const DevProblem& P, int cur, const double* __restrict__ scale,
                                              const double* __restrict__ y, double* __restrict__ CL);
 // Band tail (PUB): what a back-substitution chunk can compute before the band solve's y exists — its observation
@@ -224,8 +226,9 @@ __device__ __forceinline__ void backsub_pre(const DevProblem& P, const BaConsts&
     }
 }
 // PUB_OUT alone (k_backsub_final, C4-size windows): y and the candidates come from the previous launch (plain loads),
-// only the partials are stored past the L2 and drained for the decision workgroup of the same launch
-template <bool O32, bool PUB = false, bool PUB_OUT = PUB>
+// only the partials are stored past the L2 and drained for the decision workgroup of the same launch. YL (the band
+// tail): y is the chunk's own LDS copy of the polled y (plain loads)
+template <bool O32, bool PUB = false, bool PUB_OUT = PUB, bool YL = false>
 __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
                                              const double* __restrict__ scale, const double* __restrict__ pdata,
                                              const double* __restrict__ y, const double* __restrict__ delta,
@@ -277,7 +280,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
             if (ac >= 0) {
                 double yv[6];
 #pragma unroll
-                for (int d = 0; d < 6; ++d) yv[d] = tail_ld(y + 6 * ac + d);
+                for (int d = 0; d < 6; ++d) yv[d] = YL ? y[6 * ac + d] : tail_ld(y + 6 * ac + d);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     double a = 0.0;
@@ -308,7 +311,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
             const double* sp = scale + P.off_pt + 3 * ap;
             double jy[3], sy[6];
 #pragma unroll
-            for (int d = 0; d < 6; ++d) sy[d] = sc[d] * (PUB ? tail_ld(yc + d) : yc[d]);
+            for (int d = 0; d < 6; ++d) sy[d] = sc[d] * ((PUB && !YL) ? tail_ld(yc + d) : yc[d]);
             jc_times(jc, sy, jy);
 #pragma unroll
             for (int i = 0; i < 3; ++i) v[i] = sp[i] * (jp[i] * jy[0] + jp[3 + i] * jy[1] + jp[6 + i] * jy[2]);
@@ -322,7 +325,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         }
     }
     // the band tail: this chunk's candidate poses / intrinsics from y (published by the barrier below / in block_sum)
-    if (CL) cand_compute(P, cur, scale, y, CL);
+    if (CL) cand_compute<YL>(P, cur, scale, y, CL);
     if (big) block_sum<3>(bsum, lds, out);  // out[0..3) valid for every thread after this
     __syncthreads();
     bmark(0);
@@ -336,7 +339,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
         const double* sp = PRE ? &PL->pt[tid][PDATA] : scale + P.off_pt + 3 * ap;
         double yk[4];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) yk[m] = PUB ? tail_ld(y + P.kb + m) : y[P.kb + m];
+        for (int m = 0; m < 4; ++m) yk[m] = (PUB && !YL) ? tail_ld(y + P.kb + m) : y[P.kb + m];
         double t[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -420,6 +423,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     }
 }
 
+template <bool YL>
 __device__ __forceinline__ void cand_compute(const DevProblem& P, int cur, const double* __restrict__ scale,
                                              const double* __restrict__ y, double* __restrict__ CL) {
     const double* const sc = CL + 8 * (size_t)P.n_cams + 4;
@@ -429,7 +433,7 @@ __device__ __forceinline__ void cand_compute(const DevProblem& P, int cur, const
 #pragma unroll
         for (int j = 0; j < 7; ++j) x[j] = xc[j];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) d[k] = -tail_ld(y + 6 * t + k) * sc[6 * t + k];  // cam_step's delta
+        for (int k = 0; k < 6; ++k) d[k] = -(YL ? y[6 * t + k] : tail_ld(y + 6 * t + k)) * sc[6 * t + k];  // cam_step's delta
         se3_plus(x, d, tp);
 #pragma unroll
         for (int j = 0; j < 7; ++j) xc[j] = tp[j];
@@ -437,7 +441,7 @@ __device__ __forceinline__ void cand_compute(const DevProblem& P, int cur, const
     if (threadIdx.x == TPB - 1) {  // intr_step's candidate: K + (-y_k s_k)
         double* const kc = CL + 8 * (size_t)P.n_cams;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) kc[m] = P.K[cur][m] + (-tail_ld(y + P.kb + m) * scale[P.off_k + m]);
+        for (int m = 0; m < 4; ++m) kc[m] = P.K[cur][m] + (-(YL ? y[P.kb + m] : tail_ld(y + P.kb + m)) * scale[P.off_k + m]);
     }
 }
 
