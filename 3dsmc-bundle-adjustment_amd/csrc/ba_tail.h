@@ -176,6 +176,7 @@ struct BsPre {
     double A[18];
     int r_ap[BS_OBS / TPB];
     ObsRaw<O32> r_o[BS_OBS / TPB];
+    int pi;             // point index of this thread's point (tid < the chunk's points): phase 2's store address
 };
 template <bool O32>
 __device__ __forceinline__ void backsub_pre(const DevProblem& P, const BaConsts& c, const LmState* __restrict__ st,
@@ -190,6 +191,7 @@ __device__ __forceinline__ void backsub_pre(const DevProblem& P, const BaConsts&
     const int ob = P.pt_ptr[apb], oe = P.pt_ptr[ape];
     if (oe - ob > BS_OBS) return;  // a single big point: the plain path after the wait
     B.on = true;
+    B.pi = tid < ape - apb ? P.pt_idx[apb + tid] : 0;
     constexpr int NR = BS_OBS / TPB;
     int it = 0;
     for (int o = ob + tid; o < oe; o += TPB, ++it) {
@@ -268,6 +270,9 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     constexpr int NR = BS_OBS / TPB;
     int r_ap[NR];
     ObsRaw<O32> r_o[NR];  // camera index, pixel, depth
+    // this thread's point index for phase 2, loaded before phase 1 (phase 2 then gathers its point in one trip,
+    // not pt_idx and then the point); the band tail's prologue loaded it already
+    const int pi_ph2 = PRE ? pre.pi : (tid < npts ? P.pt_idx[apb + tid] : 0);
     // ---- phase 1
     double bsum[3] = {0.0, 0.0, 0.0};
     int it = 0;
@@ -332,7 +337,7 @@ __device__ __forceinline__ void backsub_body(const DevProblem& P, const BaConsts
     // ---- phase 2
     if (tid < npts) {
         const int ap = apb + tid;
-        const int pi = P.pt_idx[ap];
+        const int pi = pi_ph2;
         const double* X = PRE ? &PL->pt[tid][PDATA + 3] : P.pts[cur] + 3 * pi;
         double* Xn = P.pts[cur ^ 1] + 3 * pi;
         const double* pd = PRE ? &PL->pt[tid][0] : pdata + (size_t)ap * PDATA;
